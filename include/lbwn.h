@@ -1,0 +1,139 @@
+/* lbwn — MI355X-native WaveNet hot path, C ABI.
+ *
+ * Drop-in boundary for hrbigelow/lb-wavenet's TensorFlow graph builders.  The reference
+ * has no FFI (it is pure Python over TensorFlow 1.x C++ kernels); each entry point below
+ * replaces the TF kernel sequence built at the cited reference line.  Host code (the
+ * Python `lbwn` package, or any C/C++ caller) owns every buffer; the library never
+ * allocates device memory, never synchronises, and is stateless except for the opaque
+ * plan (shapes + workspace carving).  All device pointers are fp32 [B][T][C]
+ * channels-last unless noted; int32 for µ-law codes and voice ids.  Every call is
+ * stream-ordered on the caller's hipStream_t (passed as void*; NULL = default stream).
+ * Return value: 0 on success, otherwise a hipError_t or 22 (EINVAL); the message is
+ * available from lbwn_last_error() (thread-local).  Errors mirror the reference's
+ * "print to stderr + exit(1)" checks (arch.py:147-161) as return codes instead.
+ */
+#ifndef LBWN_H
+#define LBWN_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LBWN_ABI_VERSION 1
+
+/* par/arch*.json after normalisation (tmodel.py:10-23, arch.py:31-103). */
+typedef struct lbwn_arch {
+  int n_blocks, n_block_layers;
+  int n_quant, n_res, n_dil, n_skip, n_post;
+  int n_gc_embed, n_gc_category; /* n_gc_embed == 0: no global conditioning */
+  int n_lc_in, n_lc_out;         /* n_lc_out == 0: no local conditioning     */
+  int n_lc_upsample;
+  int lc_upsample[8];
+  int use_bias;
+} lbwn_arch;
+
+/* Device pointers into a caller-owned flat fp32 buffer, reference layouts
+ * (arch.py:85-103).  Per-layer tensors of one kind are contiguous over the
+ * L = n_blocks*n_block_layers layers in (block, layer) order, e.g. sig = SIGNAL_0_0,
+ * SIGNAL_0_1, ... each [2][n_res][n_dil].  Bias pointers are NULL when !use_bias; GC/LC
+ * pointers are NULL when the arch has no GC/LC. */
+typedef struct lbwn_params {
+  float* pre;   float* pre_b;          /* PRE [Q][Cr], PRE_BIAS [Cr]                    */
+  float* sig;   float* sig_b;          /* SIGNAL [L][2][Cr][Cd], SIGNAL_BIAS [L][Cd]     */
+  float* gate;  float* gate_b;         /* GATE   [L][2][Cr][Cd], GATE_BIAS   [L][Cd]     */
+  float* res;   float* res_b;          /* RESIDUAL [L][Cd][Cr], RESIDUAL_BIAS [L][Cr]    */
+  float* skip;  float* skip_b;         /* SKIP [L][Cd][Cs], SKIP_BIAS [L][Cs]            */
+  float* gc_embed;                     /* GC_EMBED [n_cat+1][Ge]                         */
+  float* gc_sig; float* gc_gate;       /* GC_SIGNAL/GC_GATE [L][Ge][Cd]                  */
+  float* lc_sig; float* lc_gate;       /* LC_SIGNAL/LC_GATE [L][Clc][Cd]                 */
+  float* lc_up[8];                     /* LC_UPSAMPLE_i [s_i][Clc][dim2]                 */
+  float* post1; float* post1_b;        /* POST1 [Cs][Cp], POST1_BIAS [Cp]                */
+  float* post2; float* post2_b;        /* POST2 [Cp][Q],  POST2_BIAS [Q]                 */
+} lbwn_params;
+
+const char* lbwn_last_error(void);
+int lbwn_abi_version(void);
+
+/* ---- plan: the WaveNetTrain graph for a fixed (arch, batch_sz, slice_sz) ------------ */
+typedef struct lbwn_plan lbwn_plan;
+/* replaces WaveNetTrain.__init__ + build() graph construction (tmodel.py:8-48, :292-340) */
+int lbwn_plan_create(const lbwn_arch* arch, int batch_sz, int slice_sz, lbwn_plan** out);
+void lbwn_plan_destroy(lbwn_plan* plan);
+size_t lbwn_plan_workspace_bytes(const lbwn_plan* plan);
+/* Byte offset/size of a named workspace tensor (for parity tests / debugging):
+ * "x" [L][B][H+T][n_res] (layer inputs with D-sep halo, H = 2^(n_block_layers-1)),
+ * "z" [M][L·n_dil] (gate outputs; dZ after backward), "s" [M][n_skip] (skip sum; dS after
+ * backward), "r2" [M][n_post], "logits" [M][n_quant] (dlogits after forward).  */
+int lbwn_plan_tensor(const lbwn_plan* plan, const char* name, size_t* offset, size_t* bytes);
+/* receptive field F = n_blocks·Σ2^l (tmodel.py:50-51) */
+int lbwn_recep_field_sz(const lbwn_arch* arch);
+
+/* Forward + loss of one slice (tmodel.py:292-328 + _loss_fcn :218-289).
+ *   wav_q  int32 [B][T] µ-law codes; ids int32 [B][T] (0 = invalid window);
+ *   mel    fp32 [B][T/hop][n_lc_in] or NULL;  save fp32 D-sep state, layers packed in
+ *          (block, layer) order, each SAVE_{d}_{b}_{bl} [B][d][n_res]; read (prepend) and
+ *          updated in place (tmodel.py:122-127, :163-166).
+ *   stats  fp32[4] out: Σ masked xent, n_valid, Σ|argmax diff|·mask, 1/n_valid (0 if none).
+ * The plan's workspace keeps the activations for lbwn_train_backward. */
+int lbwn_train_forward(lbwn_plan* plan, const lbwn_params* params, void* workspace, const int* wav_q,
+                       const int* ids, const float* mel, float* save, float* stats, void* stream);
+
+/* Gradients of Σ masked xent (NOT divided by n_valid, no l2 term: both are applied in
+ * lbwn_adam_tf1, so data-parallel ranks can all-reduce raw sums).  Replaces
+ * compute_gradients (tmodel.py:354-358).  Must follow lbwn_train_forward on the same
+ * workspace/stream.  grads: every pointer of the struct is fully overwritten. */
+int lbwn_train_backward(lbwn_plan* plan, const lbwn_params* params, const lbwn_params* grads, void* workspace,
+                        const int* wav_q, const int* ids, const float* mel, void* stream);
+
+/* tf.train.AdamOptimizer.apply_gradients (train.py:178, :186), TF1 semantics, over the
+ * flat buffers [0, n_total); elements [0, n_weights) are non-BIAS trainables and get the
+ * l2 term (tmodel.py:250-261): g = raw·inv_n + l2_factor·θ with inv_n = 1/stats[1]
+ * (0 if stats[1] == 0).  counters int64[4]: [0] GLOBAL_STEP, [1] VALID_SAMPLES,
+ * [2] Adam applies so far (t-1), [3] reserved.  lr_t = lr·√(1-β2^t)/(1-β1^t) is derived
+ * on device, so the call is graph-capturable.  Then counters advance by (1, n_valid, 1). */
+int lbwn_adam_tf1(float* params, const float* grads, float* m, float* v, int64_t n_weights, int64_t n_total,
+                  float lr, float beta1, float beta2, float eps, float l2_factor, const float* stats,
+                  int64_t* counters, void* stream);
+
+/* ---- fine-grained kernels (parity tests, custom drivers) ------------------------------ */
+/* ops.mu_encode_np (ops.py:23-28, tf32=0, float64 math) / ops.mu_encode (ops.py:4-9, tf32=1) */
+int lbwn_mulaw_encode(const float* x, int* q, int64_t n, int n_quanta, int tf32, void* stream);
+/* ops.mu_decode (ops.py:12-20) */
+int lbwn_mulaw_decode(const int* q, float* x, int64_t n, int n_quanta, void* stream);
+
+/* ops.conv1x1 and every 1x1 product (ops.py:41-55): C[M][N] = epi(A·B).
+ * a_kcontig: A stored A[m*lda+k] (else A[k*lda+m]); b_kcontig: B stored B[n*ldb+k]
+ * (else B[k*ldb+n]).  Epilogue: +bias[n], relu, zero where mask[m*ldm+n] <= 0, += C.
+ * relu_a applies relu to A on load.  split_k > 1 needs slab_ws of split_k·M·N floats. */
+int lbwn_gemm_f32(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig,
+                  float* C, int64_t ldc, int M, int N, int K, const float* bias, int relu_a, int relu_out,
+                  const float* mask, int64_t ldm, int accumulate, int split_k, float* slab_ws, void* stream);
+
+/* One residual layer forward (tmodel.py:117-184): x_in is the [B][H+T][n_res] halo
+ * buffer whose rows [H-d, H) hold SAVE; writes z [M][*] (row stride ldz) and, if x_out,
+ * x_out body rows (x + z·RES + b). gc_tab [n_cat+1][2·n_dil] / ids, cond [M][2·n_dil]
+ * (row stride ldcond) are optional conditioning adds. */
+int lbwn_layer_forward(const float* x_in, float* x_out, float* z, int64_t ldz, const float* w_sig,
+                       const float* w_gate, const float* b_sig, const float* b_gate, const float* w_res,
+                       const float* b_res, const float* gc_tab, const int* ids, const float* cond,
+                       int64_t ldcond, int B, int T, int H, int dilation, int n_res, int n_dil, void* stream);
+
+/* D-separation prepend/save for all layers at once (tmodel.py:122-127, :165). */
+int lbwn_dsep_prepend(float* x_all, int64_t x_layer_stride, const float* save, int n_layers, int n_block_layers,
+                      int B, int T, int H, int n_res, void* stream);
+int lbwn_dsep_save(const float* x_all, int64_t x_layer_stride, float* save, int n_layers, int n_block_layers,
+                   int B, int T, int H, int n_res, void* stream);
+
+/* softmax_cross_entropy_with_logits_v2 on logits[:, :-1] vs one-hot(wav_q[:, 1:]) with
+ * mask ids[:, 1:] != 0 (tmodel.py:228-249).  Overwrites logits with the unnormalised
+ * gradient (softmax - onehot)·mask when write_grad; stats as lbwn_train_forward.
+ * partial_ws: 3·2048 floats. */
+int lbwn_head_xent(float* logits, const int* wav_q, const int* ids, int B, int T, int Q, int write_grad,
+                   float* stats, float* partial_ws, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LBWN_H */

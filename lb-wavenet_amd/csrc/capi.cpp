@@ -1,0 +1,100 @@
+// extern "C" surface of liblbwn.so (declared in include/lbwn.h).
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/lbwn.h"
+#include "common.h"
+#include "kernels.h"
+
+static thread_local char g_err[1024] = "";
+
+void lbwn_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+extern "C" {
+
+const char* lbwn_last_error(void) { return g_err; }
+int lbwn_abi_version(void) { return LBWN_ABI_VERSION; }
+
+int lbwn_adam_tf1(float* params, const float* grads, float* m, float* v, int64_t n_weights, int64_t n_total,
+                  float lr, float beta1, float beta2, float eps, float l2_factor, const float* stats,
+                  int64_t* counters, void* stream) {
+  LBWN_REQUIRE(params && grads && m && v && counters, "adam_tf1: null argument");
+  LBWN_REQUIRE(n_weights >= 0 && n_weights <= n_total, "adam_tf1: bad sizes");
+  hipStream_t st = (hipStream_t)stream;
+  int e = lbwn_adam_launch2(params, grads, m, v, (long)n_weights, (long)n_total, lr, beta1, beta2, eps, l2_factor,
+                            stats, (const long long*)counters, st);
+  if (e) return e;
+  if (stats) return lbwn_counters_launch((long long*)counters, stats, 1, st);
+  return 0;
+}
+
+int lbwn_mulaw_encode(const float* x, int* q, int64_t n, int n_quanta, int tf32, void* stream) {
+  LBWN_REQUIRE(n >= 0 && n_quanta >= 2, "mulaw_encode: bad arguments");
+  if (n == 0) return 0;
+  return lbwn_mulaw_encode_launch(x, q, (long)n, n_quanta, tf32, (hipStream_t)stream);
+}
+
+int lbwn_mulaw_decode(const int* q, float* x, int64_t n, int n_quanta, void* stream) {
+  LBWN_REQUIRE(n >= 0 && n_quanta >= 2, "mulaw_decode: bad arguments");
+  if (n == 0) return 0;
+  return lbwn_mulaw_decode_launch(q, x, (long)n, n_quanta, (hipStream_t)stream);
+}
+
+int lbwn_gemm_f32(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig, float* C,
+                  int64_t ldc, int M, int N, int K, const float* bias, int relu_a, int relu_out, const float* mask,
+                  int64_t ldm, int accumulate, int split_k, float* slab_ws, void* stream) {
+  lbwn_gemm_args g;
+  memset(&g, 0, sizeof(g));
+  g.A = A; g.lda = (long)lda; g.B = B; g.ldb = (long)ldb; g.C = C; g.ldc = (long)ldc;
+  g.M = M; g.N = N; g.K = K; g.bias = bias; g.relu_a = relu_a; g.relu_out = relu_out;
+  g.mask = mask; g.ldm = (long)ldm; g.accumulate = accumulate;
+  return lbwn_gemm_launch(g, a_kcontig, b_kcontig, split_k, slab_ws, (hipStream_t)stream);
+}
+
+int lbwn_layer_forward(const float* x_in, float* x_out, float* z, int64_t ldz, const float* w_sig,
+                       const float* w_gate, const float* b_sig, const float* b_gate, const float* w_res,
+                       const float* b_res, const float* gc_tab, const int* ids, const float* cond, int64_t ldcond,
+                       int B, int T, int H, int dilation, int n_res, int n_dil, void* stream) {
+  LBWN_REQUIRE(x_in && z && w_sig && w_gate && w_res, "layer_forward: null argument");
+  LBWN_REQUIRE(!gc_tab || ids, "layer_forward: gc_tab needs ids");
+  lbwn_layer_args a;
+  memset(&a, 0, sizeof(a));
+  a.x_in = x_in; a.x_out = x_out; a.z = z; a.ldz = (long)ldz;
+  a.w_sig = w_sig; a.w_gate = w_gate; a.b_sig = b_sig; a.b_gate = b_gate; a.w_res = w_res; a.b_res = b_res;
+  a.gc_tab = gc_tab; a.ids = ids; a.cond = cond; a.ldcond = (long)ldcond;
+  a.B = B; a.T = T; a.H = H; a.d = dilation; a.Cr = n_res; a.Cd = n_dil;
+  return lbwn_layer_fwd_launch(a, (hipStream_t)stream);
+}
+
+int lbwn_dsep_prepend(float* x_all, int64_t xls, const float* save, int n_layers, int nbl, int B, int T, int H,
+                      int n_res, void* stream) {
+  LBWN_REQUIRE(H >= (1 << (nbl - 1)), "dsep_prepend: halo %d < max dilation", H);
+  return lbwn_dsep_prepend_launch(x_all, (long)xls, save, n_layers, nbl, B, T, H, n_res, (hipStream_t)stream);
+}
+
+int lbwn_dsep_save(const float* x_all, int64_t xls, float* save, int n_layers, int nbl, int B, int T, int H,
+                   int n_res, void* stream) {
+  LBWN_REQUIRE(H >= (1 << (nbl - 1)), "dsep_save: halo %d < max dilation", H);
+  return lbwn_dsep_save_launch(x_all, (long)xls, save, n_layers, nbl, B, T, H, n_res, (hipStream_t)stream);
+}
+
+int lbwn_head_xent(float* logits, const int* wav_q, const int* ids, int B, int T, int Q, int write_grad, float* stats,
+                   float* partial_ws, void* stream) {
+  LBWN_REQUIRE(logits && wav_q && ids && stats && partial_ws, "head_xent: null argument");
+  LBWN_REQUIRE(T >= 2, "head_xent: slice_sz must be >= 2");
+  lbwn_head_args h;
+  h.logits = logits; h.q = wav_q; h.ids = ids; h.B = B; h.T = T; h.Q = Q; h.partial = partial_ws;
+  h.write_grad = write_grad;
+  int nb = 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (int e = lbwn_head_launch(h, &nb, st)) return e;
+  return lbwn_stats_reduce_launch(partial_ws, nb, stats, st);
+}
+
+}  // extern "C"

@@ -1,0 +1,228 @@
+// fp32 MFMA GEMM for every 1x1 channel-mixing product of the WaveNet step:
+//   skip    S  = Zcat·SKIPcat        (tmodel.py:171-184 summed over layers, tmodel.py:316-320)
+//   head    H1 = relu(S)·POST1, logits = relu(H1)·POST2   (tmodel.py:187-215)
+//   and their backward products (weight grads are split-K over the M = B·T positions).
+// C[M][N] = epi( Σ_k A[m][k]·B[k][n] ).  A is stored either k-contiguous (A[m*lda+k]) or
+// m-contiguous (A[k*lda+m]); B either n-contiguous (B[k*ldb+n]) or k-contiguous
+// (B[n*ldb+k]).  The LDS image follows the global layout (no transposing stage), and the
+// MFMA k-order is permuted so a k-contiguous operand feeds four v_mfma_f32_32x32x2_f32
+// steps from one ds_read_b128: at step j of an 8-deep group, lane half h uses k = 8g+4h+j.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 16, NT = 256;
+constexpr int KCS = BK + 4;  // padded row (floats) of a k-contiguous LDS image: 80 B -> conflict-free b128
+
+template <bool KC, int BMN>
+struct Stage {
+  // per-thread registers for one BK tile of one operand (2 x float4)
+  floatx4 v[2];
+  static constexpr int LDS_FLOATS = KC ? BMN * KCS : BK * BMN;
+
+  LBWN_DEV void load(const float* __restrict__ P, long ld, int mn0, int MN, int k0, int K, int tid,
+                     bool relu, const int* codes = nullptr) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int r, c;  // r: index along M/N, c: along K
+      if (KC) { r = tid / 4 + 64 * i; c = (tid % 4) * 4; }
+      else    { c = tid / 32 + 8 * i; r = (tid % 32) * 4; }
+      int gr = mn0 + r, gk = k0 + c;
+      floatx4 x = {0.f, 0.f, 0.f, 0.f};
+      if (KC) {
+        if (gr < MN && gk < K) x = *(const floatx4*)(P + (long)gr * ld + gk);
+      } else if (codes) {
+        if (gk < K) {
+          const int cd = codes[gk] - gr;
+          x[0] = cd == 0 ? 1.f : 0.f; x[1] = cd == 1 ? 1.f : 0.f;
+          x[2] = cd == 2 ? 1.f : 0.f; x[3] = cd == 3 ? 1.f : 0.f;
+        }
+      } else {
+        if (gk < K && gr < MN) x = *(const floatx4*)(P + (long)gk * ld + gr);
+      }
+      if (relu) {
+        x[0] = fmaxf(x[0], 0.f); x[1] = fmaxf(x[1], 0.f);
+        x[2] = fmaxf(x[2], 0.f); x[3] = fmaxf(x[3], 0.f);
+      }
+      v[i] = x;
+    }
+  }
+  LBWN_DEV void store(float* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (KC) { int r = tid / 4 + 64 * i, c = (tid % 4) * 4; *(floatx4*)(lds + r * KCS + c) = v[i]; }
+      else    { int c = tid / 32 + 8 * i, r = (tid % 32) * 4; *(floatx4*)(lds + c * BMN + r) = v[i]; }
+    }
+  }
+  // fragment for rows [base, base+32) of group g: element j = value at k = 8g+4h+j
+  LBWN_DEV floatx4 frag(const float* lds, int base, int g, int lane) const {
+    int i = lane & 31, h = lane >> 5;
+    if (KC) return *(const floatx4*)(lds + (base + i) * KCS + 8 * g + 4 * h);
+    floatx4 f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f[j] = lds[(8 * g + 4 * h + j) * BMN + base + i];
+    return f;
+  }
+};
+
+// XCD-aware bijective remap: blocks b and b+8 share an XCD under round-robin dispatch, so
+// give each XCD a contiguous run of tiles (tiles sharing an A row-panel are adjacent).
+LBWN_DEV int xcd_remap(int bid, int nwg) {
+  int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+template <bool A_KC, bool B_KC>
+__global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(lbwn_gemm_args g) {
+  using SA = Stage<A_KC, BM>;
+  using SB = Stage<B_KC, BN>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * (SA::LDS_FLOATS + SB::LDS_FLOATS)];
+  auto As = [&](int i) { return smem + i * SA::LDS_FLOATS; };
+  auto Bs = [&](int i) { return smem + 2 * SA::LDS_FLOATS + i * SB::LDS_FLOATS; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  const int kz0 = blockIdx.z * g.k_per_split;
+  const int kz1 = min(g.K, kz0 + g.k_per_split);
+  const int ntiles = (kz1 - kz0 + BK - 1) / BK;
+
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  SA sa;
+  SB sb;
+  if (ntiles > 0) {
+    sa.load(g.A, g.lda, m0, g.M, kz0, kz1, tid, g.relu_a, g.a_codes);
+    sb.load(g.B, g.ldb, n0, g.N, kz0, kz1, tid, false);
+    sa.store(As(0), tid);
+    sb.store(Bs(0), tid);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < ntiles) {
+      const int k0 = kz0 + (kt + 1) * BK;
+      sa.load(g.A, g.lda, m0, g.M, k0, kz1, tid, g.relu_a, g.a_codes);
+      sb.load(g.B, g.ldb, n0, g.N, k0, kz1, tid, false);
+    }
+#pragma unroll
+    for (int gg = 0; gg < BK / 8; ++gg) {
+      floatx4 fa[2], fb[2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) fa[mi] = sa.frag(As(cur), wm * 64 + mi * 32, gg, lane);
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) fb[ni] = sb.frag(Bs(cur), wn * 64 + ni * 32, gg, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = mfma32(fa[mi][j], fb[ni][j], acc[mi][ni]);
+    }
+    if (kt + 1 < ntiles) {
+      sa.store(As(cur ^ 1), tid);
+      sb.store(Bs(cur ^ 1), tid);
+    }
+    __syncthreads();
+  }
+
+  // epilogue
+  const int h = lane >> 5, ci = lane & 31;
+  float* C = g.C + (long)blockIdx.z * g.split_stride;
+  const bool raw = g.split_stride != 0;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int col = n0 + wn * 64 + ni * 32 + ci;
+      if (col >= g.N) continue;
+      const float bv = (!raw && g.bias) ? g.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + mi * 32 + acc_row(r, h);
+        if (row >= g.M) continue;
+        float v = acc[mi][ni][r];
+        const long o = (long)row * g.ldc + col;
+        if (!raw) {
+          v += bv;
+          if (g.relu_out) v = fmaxf(v, 0.f);
+          if (g.mask && !(g.mask[(long)row * g.ldm + col] > 0.f)) v = 0.f;
+          if (g.accumulate) v += C[o];
+        }
+        C[o] = v;
+      }
+    }
+}
+
+// Σ over split slabs + epilogue; vectorised over n (N % 4 == 0).
+__global__ void splitk_reduce_kernel(lbwn_gemm_args g, const float* __restrict__ slabs, int splits) {
+  const long n4 = g.N / 4;
+  const long total = (long)g.M * n4;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int row = (int)(e / n4), col = (int)(e % n4) * 4;
+    floatx4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < splits; ++z) s += *(const floatx4*)(slabs + (long)z * g.M * g.N + (long)row * g.N + col);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = s[j];
+      if (g.bias) v += g.bias[col + j];
+      if (g.relu_out) v = fmaxf(v, 0.f);
+      if (g.mask && !(g.mask[(long)row * g.ldm + col + j] > 0.f)) v = 0.f;
+      float* c = g.C + (long)row * g.ldc + col + j;
+      if (g.accumulate) v += *c;
+      *c = v;
+    }
+  }
+}
+
+}  // namespace
+
+int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
+                     hipStream_t st) {
+  LBWN_REQUIRE(a.M > 0 && a.N > 0 && a.K > 0, "gemm: empty shape M=%d N=%d K=%d", a.M, a.N, a.K);
+  LBWN_REQUIRE(a.K % 4 == 0 || !a_kcontig, "gemm: K %% 4 != 0 with k-contiguous A");
+  LBWN_REQUIRE(a.K % 4 == 0 || !b_kcontig, "gemm: K %% 4 != 0 with k-contiguous B");
+  LBWN_REQUIRE(a.M % 4 == 0 || a_kcontig, "gemm: M %% 4 != 0 with m-contiguous A");
+  LBWN_REQUIRE(a.N % 4 == 0, "gemm: N %% 4 != 0");
+  LBWN_REQUIRE(a.lda % 4 == 0 && a.ldb % 4 == 0, "gemm: lda/ldb must be multiples of 4");
+  LBWN_REQUIRE(a.a_codes == nullptr || !a_kcontig, "gemm: one-hot A must be m-contiguous");
+  LBWN_REQUIRE((a.a_codes || (((uintptr_t)a.A) & 15) == 0) && (((uintptr_t)a.B) & 15) == 0,
+               "gemm: A/B not 16-B aligned");
+  if (split_k < 1) split_k = 1;
+  lbwn_gemm_args g = a;
+  int kps = (a.K + split_k - 1) / split_k;
+  kps = (kps + BK - 1) / BK * BK;
+  split_k = (a.K + kps - 1) / kps;
+  g.k_per_split = kps;
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  dim3 grid(tiles, 1, split_k);
+  if (split_k > 1) {
+    LBWN_REQUIRE(slab_ws != nullptr, "gemm: split-K needs a slab workspace");
+    g.C = slab_ws;
+    g.ldc = a.N;
+    g.split_stride = (long)a.M * a.N;
+  } else {
+    g.split_stride = 0;
+  }
+  if (a_kcontig && b_kcontig) gemm_f32_kernel<true, true><<<grid, NT, 0, st>>>(g);
+  else if (a_kcontig) gemm_f32_kernel<true, false><<<grid, NT, 0, st>>>(g);
+  else if (b_kcontig) gemm_f32_kernel<false, true><<<grid, NT, 0, st>>>(g);
+  else gemm_f32_kernel<false, false><<<grid, NT, 0, st>>>(g);
+  LBWN_CHECK_LAUNCH();
+  if (split_k > 1) {
+    const long total = (long)a.M * (a.N / 4);
+    int blocks = (int)std::min<long>((total + 255) / 256, 4096);
+    splitk_reduce_kernel<<<blocks, 256, 0, st>>>(a, slab_ws, split_k);
+    LBWN_CHECK_LAUNCH();
+  }
+  return 0;
+}

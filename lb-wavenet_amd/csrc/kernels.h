@@ -1,0 +1,93 @@
+// Internal launch interfaces shared by the kernel TUs and the engine (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct lbwn_gemm_args {
+  const float* A; long lda;
+  const float* B; long ldb;
+  float* C; long ldc;
+  int M, N, K;
+  const float* bias;   // [N] nullable
+  const float* mask;   // mask[m*ldm+n] > 0 keeps the value; nullable
+  long ldm;
+  int relu_a, relu_out, accumulate;
+  const int* a_codes;  // m-contiguous A only: A[k][m] = (a_codes[k] == m)  (one-hot, tmodel.py:64-65)
+  int k_per_split;     // set by the launcher
+  long split_stride;   // set by the launcher
+};
+int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
+                     hipStream_t st);
+
+// One residual layer (tmodel.py:117-184).  x buffers are [B][H+T][Cr]; rows [H-d, H) of
+// x_in hold the D-separation state SAVE_l (prepended by lbwn_dsep_prepend).
+struct lbwn_layer_args {
+  const float* x_in;
+  float* x_out;             // nullable (last layer's residual output is dead)
+  float* z; long ldz;       // Zcat column block of this layer
+  const float* w_sig; const float* w_gate;  // [2][Cr][Cd]
+  const float* b_sig; const float* b_gate;  // [Cd] nullable
+  const float* w_res; const float* b_res;   // [Cd][Cr], [Cr] nullable
+  const float* gc_tab;      // [ncat+1][2*Cd] (sig | gate) nullable
+  const int* ids;           // [B][T]
+  const float* cond; long ldcond;  // [M][2*Cd] nullable (LC projection)
+  int B, T, H, d, Cr, Cd;
+  // ---- backward only ----
+  const float* dz_skip; long lddz;   // [M] rows of dS·SKIP_lᵀ (column block of dZ)
+  const float* g_a; const float* g_c0; int g_d;  // dx_{l+1}[t] = g_a[t] + g_c0[t+g_d]; nullable => 0
+  float* out_a; float* out_c0;                    // [M][Cr]
+  float* slab;              // per-block weight-grad partials [nblocks][slab_stride]
+  int slab_stride;
+  float* dv_out; long lddv; // [M][2Cd] nullable (needed for LC grads)
+  float* gc_dtab;           // [ncat+1][2Cd] atomically accumulated (nullable)
+  // ---- deferred reduction of the previous (deeper) layer's slab ----
+  const float* red_slab; int red_nparts; int red_stride;
+  float* red_dsig; float* red_dgate; float* red_dres;
+  float* red_dbsig; float* red_dbgate; float* red_dbres;
+};
+constexpr int LBWN_LAYER_POS = 128;   // positions per layer-kernel block
+int lbwn_layer_fwd_launch(const lbwn_layer_args& a, hipStream_t st);
+int lbwn_layer_bwd_launch(const lbwn_layer_args& a, hipStream_t st);
+int lbwn_layer_slab_stride();
+int lbwn_layer_nblocks(int B, int T);
+int lbwn_layer_reduce_launch(const lbwn_layer_args& a, hipStream_t st);  // standalone reduction
+
+// D-separation state transfer for ALL layers at once.
+int lbwn_dsep_prepend_launch(float* xall, long xlayer_stride, const float* save, int L, int nbl,
+                             int B, int T, int H, int Cr, hipStream_t st);
+int lbwn_dsep_save_launch(const float* xall, long xlayer_stride, float* save, int L, int nbl, int B,
+                          int T, int H, int Cr, hipStream_t st);
+
+int lbwn_embed_launch(const int* q, const float* pre, const float* pre_b, float* x0, int B, int T, int H,
+                      int Cr, int Q, hipStream_t st);
+int lbwn_embed_bwd_launch(const int* q, const float* ga, const float* gc0, int gd, float* dpre,
+                          float* dpre_b, float* ws, int B, int T, int Cr, int Q, hipStream_t st);
+
+struct lbwn_head_args {
+  float* logits;            // [M][Q] in: logits, out: dlogits (unnormalised: (softmax-onehot)·mask)
+  const int* q;             // [B][T] targets (mu-law codes)
+  const int* ids;           // [B][T]
+  int B, T, Q;
+  float* partial;           // [nblocks][3] (sum_xent, n_valid, sum |argmax diff|)
+  int write_grad;
+};
+int lbwn_head_launch(const lbwn_head_args& a, int* nblocks_out, hipStream_t st);
+int lbwn_stats_reduce_launch(const float* partial, int nparts, float* stats, hipStream_t st);
+
+int lbwn_colsum_launch(const float* X, long ldx, int M, int N, float* out, int accumulate, float* ws,
+                       hipStream_t st);
+int lbwn_colsum_ws_floats(int M, int N);
+int lbwn_sum_bias_launch(const float* b, int L, int N, float* out, hipStream_t st);
+int lbwn_fill_launch(float* p, float v, long n, hipStream_t st);
+
+int lbwn_adam_launch2(float* params, const float* grads, float* m, float* v, long n_weights, long n_total,
+                      float lr, float b1, float b2, float eps, float l2, const float* stats,
+                      const long long* counters, hipStream_t st);
+int lbwn_counters_launch(long long* counters, const float* stats, int adam_applied, hipStream_t st);
+int lbwn_shift_add_launch(float* out, const float* a, const float* c0, int gd, int B, int T, int C,
+                          hipStream_t st);
+int lbwn_head_nblocks(long M);
+
+int lbwn_mulaw_encode_launch(const float* x, int* q, long n, int n_quanta, int tf32, hipStream_t st);
+int lbwn_mulaw_decode_launch(const int* q, float* x, long n, int n_quanta, hipStream_t st);
+int lbwn_bcast_rows_launch(float* dst, int L, int N, hipStream_t st);

@@ -1,0 +1,373 @@
+// Byte-/bandwidth-bound kernels around the residual stack:
+//   D-separation prepend/save (tmodel.py:122-127, :165), PRE embedding (tmodel.py:53-66,
+//   :86-102), the softmax-xent head with the invalid-window mask (tmodel.py:218-289),
+//   column sums for bias grads, TF1 Adam (train.py:178, :186) and the µ-law codec
+//   (ops.py:4-39).
+#include <math.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+// ---- D-separation state ----------------------------------------------------------------
+// SAVE for layer l (dilation d_l = 2^(l % nbl)) is [B][d_l][Cr], layers packed in order.
+// x buffers: xall + l*xlayer_stride, per stream [H+T][Cr]; SAVE_l occupies rows [H-d, H).
+
+LBWN_DEV long save_offset(int l, int nbl, int B, int Cr) {
+  // Σ_{l'<l} d_{l'} = (l / nbl)·(2^nbl - 1) + (2^(l % nbl) - 1)
+  const long s = (long)(l / nbl) * ((1L << nbl) - 1) + ((1L << (l % nbl)) - 1);
+  return s * B * Cr;
+}
+
+template <bool TO_X>
+__global__ void dsep_kernel(float* xall, long xls, float* save, int nbl, int B, int T, int H, int Cr) {
+  const int l = blockIdx.y;
+  const int d = 1 << (l % nbl);
+  const long n = (long)B * d * Cr;
+  float* sv = save + save_offset(l, nbl, B, Cr);
+  float* xl = xall + l * xls;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % Cr);
+    const long r = e / Cr;
+    const int i = (int)(r % d), b = (int)(r / d);
+    if (TO_X) {
+      xl[((long)b * (H + T) + (H - d + i)) * Cr + c] = sv[e];              // prepend
+    } else {
+      sv[e] = xl[((long)b * (H + T) + (H + T - d + i)) * Cr + c];          // save: last d rows of [SAVE ++ x]
+    }
+  }
+}
+
+// ---- embedding -------------------------------------------------------------------------
+
+__global__ void embed_kernel(const int* __restrict__ q, const float* __restrict__ pre, const float* pre_b,
+                             float* x0, int B, int T, int H, int Cr, int Q) {
+  const long n = (long)B * T * Cr;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % Cr);
+    const long m = e / Cr;
+    const int b = (int)(m / T), t = (int)(m % T);
+    int code = q[m];
+    code = code < 0 ? 0 : (code >= Q ? Q - 1 : code);
+    float v = pre[(long)code * Cr + c];
+    if (pre_b) v += pre_b[c];
+    x0[((long)b * (H + T) + H + t) * Cr + c] = v;
+  }
+}
+
+// out[m] = a[m] + (t+gd < T ? c0[m+gd] : 0)   (dx of a layer input from (g + dcur, dprev))
+__global__ void shift_add_kernel(float* out, const float* a, const float* c0, int gd, int B, int T, int C) {
+  const long n = (long)B * T * C;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const long m = e / C;
+    const int t = (int)(m % T);
+    float v = a[e];
+    if (t + gd < T) v += c0[e + (long)gd * C];
+    out[e] = v;
+  }
+}
+
+// ---- softmax cross-entropy head ------------------------------------------------------------
+// One wave per position row; dlogits (unnormalised) written in place.
+
+LBWN_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+LBWN_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void head_kernel(lbwn_head_args a) {
+  __shared__ float part[4][3];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long M = (long)a.B * a.T;
+  float s_xent = 0.f, s_valid = 0.f, s_diff = 0.f;
+  for (long m = (long)blockIdx.x * 4 + w; m < M; m += (long)gridDim.x * 4) {
+    float* row = a.logits + m * a.Q;
+    const int t = (int)(m % a.T);
+    if (t == a.T - 1) {  // logits_out[:, :-1] (tmodel.py:231): the last position has no target
+      if (a.write_grad)
+        for (int c = lane; c < a.Q; c += 64) row[c] = 0.f;
+      continue;
+    }
+    const int tgt = a.q[m + 1];
+    const bool valid = a.ids[m + 1] != 0;   // tmodel.py:232
+    // max + first argmax
+    float mx = -INFINITY;
+    int am = 0x7fffffff;
+    for (int c = lane; c < a.Q; c += 64) {
+      const float v = row[c];
+      if (v > mx) { mx = v; am = c; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float om = __shfl_xor(mx, o);
+      const int oa = __shfl_xor(am, o);
+      if (om > mx || (om == mx && oa < am)) { mx = om; am = oa; }
+    }
+    float se = 0.f;
+    for (int c = lane; c < a.Q; c += 64) se += expf(row[c] - mx);
+    se = wave_sum(se);
+    const float lse = mx + logf(se);
+    const float xent = lse - row[tgt];
+    if (a.write_grad) {
+      const float inv = 1.f / se;
+      for (int c = lane; c < a.Q; c += 64) {
+        float g = expf(row[c] - mx) * inv - (c == tgt ? 1.f : 0.f);
+        row[c] = valid ? g : 0.f;
+      }
+    }
+    if (lane == 0 && valid) {
+      s_xent += xent;
+      s_valid += 1.f;
+      s_diff += fabsf((float)(tgt - am));
+    }
+  }
+  if (lane == 0) {
+    part[w][0] = s_xent;
+    part[w][1] = s_valid;
+    part[w][2] = s_diff;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int k = threadIdx.x;
+    a.partial[blockIdx.x * 3 + k] = ((part[0][k] + part[1][k]) + part[2][k]) + part[3][k];
+  }
+}
+
+// stats[0] = Σxent, [1] = n_valid, [2] = Σ|diff|, [3] = 1/n_valid (0 if none)
+__global__ void stats_reduce_kernel(const float* partial, int nparts, float* stats) {
+  __shared__ double sh[3][256];
+  double s[3] = {0, 0, 0};
+  for (int p = threadIdx.x; p < nparts; p += blockDim.x)
+    for (int k = 0; k < 3; ++k) s[k] += partial[p * 3 + k];
+  for (int k = 0; k < 3; ++k) sh[k][threadIdx.x] = s[k];
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st)
+      for (int k = 0; k < 3; ++k) sh[k][threadIdx.x] += sh[k][threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    stats[0] = (float)sh[0][0];
+    stats[1] = (float)sh[1][0];
+    stats[2] = (float)sh[2][0];
+    stats[3] = sh[1][0] > 0 ? (float)(1.0 / sh[1][0]) : 0.f;
+  }
+}
+
+// ---- column sums (bias gradients), deterministic two-pass ------------------------------------
+
+constexpr int CS_ROWS = 256;  // rows per partial
+__global__ void colsum_partial_kernel(const float* __restrict__ X, long ldx, int M, int N, float* part) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int r0 = blockIdx.y * CS_ROWS;
+  if (n >= N) return;
+  float s = 0.f;
+  const int r1 = min(M, r0 + CS_ROWS);
+  for (int r = r0; r < r1; ++r) s += X[(long)r * ldx + n];
+  part[(long)blockIdx.y * N + n] = s;
+}
+__global__ void colsum_final_kernel(const float* part, int nparts, int N, float* out, int accumulate) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int p = 0; p < nparts; ++p) s += part[(long)p * N + n];
+  out[n] = accumulate ? out[n] + s : s;
+}
+
+__global__ void sum_bias_kernel(const float* b, int L, int N, float* out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int l = 0; l < L; ++l) s += b[(long)l * N + n];
+  out[n] = s;
+}
+
+__global__ void fill_kernel(float* p, float v, long n) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) p[e] = v;
+}
+
+// ---- TF1 Adam over the flat parameter buffer --------------------------------------------------
+// grads hold Σ-xent gradients; g = raw·(1/n_valid) + l2·θ for the weight region
+// [0, n_weights) (non-BIAS vars, tmodel.py:250-261); biases get no l2 term.
+// counters[2] (int64) is Adam's apply count t-1; lr_t = lr·√(1-β2^t)/(1-β1^t).
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ gr, float* __restrict__ m,
+                            float* __restrict__ v, long nw, long n, float lr, float b1, float b2, float eps,
+                            float l2, const float* stats, const long long* counters) {
+  const double t = (double)(counters[2] + 1);
+  const float lr_t = (float)((double)lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t)));
+  const float inv = stats ? (stats[1] > 0.f ? 1.f / stats[1] : 0.f) : 1.f;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const float th = p[e];
+    float g = gr[e] * inv;
+    if (e < nw) g += l2 * th;
+    const float mm = b1 * m[e] + (1.f - b1) * g;
+    const float vv = b2 * v[e] + (1.f - b2) * g * g;
+    m[e] = mm;
+    v[e] = vv;
+    p[e] = th - lr_t * mm / (sqrtf(vv) + eps);
+  }
+}
+
+// counters: [0] GLOBAL_STEP, [1] VALID_SAMPLES, [2] Adam t-1 (tmodel.py:282-287)
+__global__ void counters_kernel(long long* counters, const float* stats, int adam_applied) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    counters[0] += 1;
+    counters[1] += (long long)stats[1];
+    counters[2] += adam_applied;
+  }
+}
+
+// ---- µ-law ---------------------------------------------------------------------------------
+
+__global__ void mulaw_encode_kernel(const float* x, int* q, long n, int nq, int tf32) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    if (tf32) {  // ops.py:4-9, float32 throughout
+      const float mu = (float)(nq - 1), xv = x[e];
+      const float sg = xv > 0.f ? 1.f : (xv < 0.f ? -1.f : 0.f);
+      const float amp = sg * log1pf(mu * fabsf(xv)) / log1pf(mu);
+      q[e] = (int)((amp + 1.f) * 0.5f * mu + 0.5f);
+    } else {  // ops.py:23-28, numpy float64
+      const double mu = (double)(nq - 1), xv = (double)x[e];
+      const double sg = xv > 0 ? 1.0 : (xv < 0 ? -1.0 : 0.0);
+      const double amp = sg * log1p(mu * fabs(xv)) / log1p(mu);
+      q[e] = (int)((amp + 1.0) * 0.5 * mu + 0.5);
+    }
+  }
+}
+
+__global__ void mulaw_decode_kernel(const int* q, float* x, long n, int nq) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
+    const float mu = (float)(nq - 1), inv_mu = 1.f / mu;  // ops.py:12-20
+    const float a = (2.f * (float)q[e] - 1.f) * inv_mu - 1.f;
+    const float sg = a > 0.f ? 1.f : (a < 0.f ? -1.f : 0.f);
+    x[e] = sg * (powf(1.f + mu, fabsf(a)) - 1.f) * inv_mu;
+  }
+}
+
+inline int grid_for(long n, int per = 256, int cap = 8192) {
+  long g = (n + per - 1) / per;
+  if (g < 1) g = 1;
+  return (int)(g > cap ? cap : g);
+}
+
+}  // namespace
+
+int lbwn_dsep_prepend_launch(float* xall, long xls, const float* save, int L, int nbl, int B, int T, int H,
+                             int Cr, hipStream_t st) {
+  dim3 grid(grid_for((long)B * (1 << (nbl - 1)) * Cr, 256, 256), L);
+  dsep_kernel<true><<<grid, 256, 0, st>>>(xall, xls, const_cast<float*>(save), nbl, B, T, H, Cr);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_dsep_save_launch(const float* xall, long xls, float* save, int L, int nbl, int B, int T, int H, int Cr,
+                          hipStream_t st) {
+  dim3 grid(grid_for((long)B * (1 << (nbl - 1)) * Cr, 256, 256), L);
+  dsep_kernel<false><<<grid, 256, 0, st>>>(const_cast<float*>(xall), xls, save, nbl, B, T, H, Cr);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_embed_launch(const int* q, const float* pre, const float* pre_b, float* x0, int B, int T, int H, int Cr,
+                      int Q, hipStream_t st) {
+  embed_kernel<<<grid_for((long)B * T * Cr), 256, 0, st>>>(q, pre, pre_b, x0, B, T, H, Cr, Q);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_shift_add_launch(float* out, const float* a, const float* c0, int gd, int B, int T, int C,
+                          hipStream_t st) {
+  shift_add_kernel<<<grid_for((long)B * T * C), 256, 0, st>>>(out, a, c0, gd, B, T, C);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_head_launch(const lbwn_head_args& a, int* nblocks_out, hipStream_t st) {
+  const long M = (long)a.B * a.T;
+  const int nb = (int)std::min<long>((M + 3) / 4, 2048);
+  head_kernel<<<nb, 256, 0, st>>>(a);
+  LBWN_CHECK_LAUNCH();
+  if (nblocks_out) *nblocks_out = nb;
+  return 0;
+}
+int lbwn_head_nblocks(long M) { return (int)std::min<long>((M + 3) / 4, 2048); }
+
+int lbwn_stats_reduce_launch(const float* partial, int nparts, float* stats, hipStream_t st) {
+  stats_reduce_kernel<<<1, 256, 0, st>>>(partial, nparts, stats);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_colsum_ws_floats(int M, int N) { return ((M + CS_ROWS - 1) / CS_ROWS) * N; }
+
+int lbwn_colsum_launch(const float* X, long ldx, int M, int N, float* out, int accumulate, float* ws,
+                       hipStream_t st) {
+  const int np = (M + CS_ROWS - 1) / CS_ROWS;
+  dim3 g1((N + 255) / 256, np);
+  colsum_partial_kernel<<<g1, 256, 0, st>>>(X, ldx, M, N, ws);
+  colsum_final_kernel<<<(N + 255) / 256, 256, 0, st>>>(ws, np, N, out, accumulate);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_sum_bias_launch(const float* b, int L, int N, float* out, hipStream_t st) {
+  sum_bias_kernel<<<(N + 255) / 256, 256, 0, st>>>(b, L, N, out);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_fill_launch(float* p, float v, long n, hipStream_t st) {
+  fill_kernel<<<grid_for(n), 256, 0, st>>>(p, v, n);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_adam_launch2(float* params, const float* grads, float* m, float* v, long nw, long n, float lr, float b1,
+                      float b2, float eps, float l2, const float* stats, const long long* counters,
+                      hipStream_t st) {
+  adam_kernel<<<grid_for(n, 256, 4096), 256, 0, st>>>(params, grads, m, v, nw, n, lr, b1, b2, eps, l2, stats,
+                                                      counters);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_counters_launch(long long* counters, const float* stats, int adam_applied, hipStream_t st) {
+  counters_kernel<<<1, 64, 0, st>>>(counters, stats, adam_applied);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_mulaw_encode_launch(const float* x, int* q, long n, int nq, int tf32, hipStream_t st) {
+  mulaw_encode_kernel<<<grid_for(n), 256, 0, st>>>(x, q, n, nq, tf32);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_mulaw_decode_launch(const int* q, float* x, long n, int nq, hipStream_t st) {
+  mulaw_decode_kernel<<<grid_for(n), 256, 0, st>>>(q, x, n, nq);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+namespace {
+__global__ void bcast_rows_kernel(float* dst, int L, int N) {
+  // dst[l][n] = dst[0][n] for l in [1, L)
+  const long n_all = (long)(L - 1) * N;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n_all; e += (long)gridDim.x * blockDim.x)
+    dst[N + e] = dst[e % N];
+}
+}  // namespace
+
+int lbwn_bcast_rows_launch(float* dst, int L, int N, hipStream_t st) {
+  if (L <= 1) return 0;
+  bcast_rows_kernel<<<grid_for((long)(L - 1) * N), 256, 0, st>>>(dst, L, N);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}

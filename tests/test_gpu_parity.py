@@ -1,0 +1,274 @@
+"""HIP path vs the CPU oracle (float64), through the C-ABI.  Tolerances: 1e-5 absolute on
+conv activations z (north_star), relative 1e-4 (scaled by the tensor's max) on deeper
+quantities that accumulate 50 layers of fp32 rounding; bit-exact on integer/mask work."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from lbwn import _lib
+from lbwn.arch import load_arch, normalize_arch
+from lbwn.optim import AdamOptimizer
+from lbwn.tmodel import WaveNetTrain
+from oracle import wavenet_ref as R
+from tests.conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+def arch3():
+    return load_arch(os.path.join(ROOT, 'par', 'arch3.json'))
+
+
+def small_arch(nb=2, nbl=4, Cr=32, Cd=32, Cs=64, Cp=32, Q=256):
+    return normalize_arch(dict(n_blocks=nb, n_block_layers=nbl, n_quant=Q, n_res=Cr, n_dil=Cd, n_skip=Cs,
+                               n_post=Cp, n_gc_embed=0, n_gc_category=0, use_bias=True))
+
+
+def make_net(arch, B, seed=0, bias_scale=0.1, l2=1e-3):
+    net = WaveNetTrain(**arch, batch_sz=B, l2_factor=l2, print_interval=0, seed=seed)
+    net.init_vars(seed, bias_scale=bias_scale)
+    return net
+
+
+def oracle_params(net):
+    P = {n: v.detach().cpu().double().numpy() for n, v in net.vars.items()}
+    S = {n: v.detach().cpu().double().numpy() for n, v in net.save_vars.items()}
+    return P, S
+
+
+def rand_batch(arch, B, T, seed=0, invalid=37):
+    rng = np.random.default_rng(seed)
+    q = rng.integers(0, arch['n_quant'], size=(B, T)).astype(np.int32)
+    ids = np.ones((B, T), np.int32)
+    ids[:, :invalid] = 0
+    if B > 1:
+        ids[1, T // 2:T // 2 + 11] = 0
+    return q, ids
+
+
+def close(a, b, rel, name=''):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    scale = max(1.0, float(np.max(np.abs(b))))
+    err = float(np.max(np.abs(a - b))) if a.size else 0.0
+    assert err <= rel * scale, '%s: max err %.3g > %.3g (scale %.3g)' % (name, err, rel * scale, scale)
+
+
+# ---- GEMM ------------------------------------------------------------------------------
+
+@pytest.mark.parametrize('akc,bkc', [(1, 0), (1, 1), (0, 0), (0, 1)])
+@pytest.mark.parametrize('split', [1, 3])
+def test_gemm_layouts(lib, akc, bkc, split):
+    M, N, K = 300, 136, 200
+    g = torch.Generator().manual_seed(1)
+    A = torch.randn(M, K, generator=g, dtype=torch.float64)
+    Bm = torch.randn(K, N, generator=g, dtype=torch.float64)
+    bias = torch.randn(N, generator=g, dtype=torch.float64)
+    mask = (torch.rand(M, N, generator=g) > 0.3).double()
+    C0 = torch.randn(M, N, generator=g, dtype=torch.float64)
+    ref = torch.relu(torch.relu(A) @ Bm + bias) * mask + C0
+    Ad = (A if akc else A.t()).contiguous().float().to(DEV)
+    Bd = (Bm.t() if bkc else Bm).contiguous().float().to(DEV)
+    Cd = C0.float().to(DEV).contiguous()
+    md = mask.float().to(DEV)
+    bd = bias.float().to(DEV)
+    ws = torch.empty(split * M * N, device=DEV)
+    _lib.check(lib.lbwn_gemm_f32(Ad.data_ptr(), K if akc else M, akc, Bd.data_ptr(), K if bkc else N, bkc,
+                                 Cd.data_ptr(), N, M, N, K, bd.data_ptr(), 1, 1, md.data_ptr(), N, 1, split,
+                                 ws.data_ptr(), None))
+    torch.cuda.synchronize()
+    close(Cd.cpu().numpy(), ref.numpy(), 1e-5, 'gemm')
+
+
+def test_gemm_large_skip_shape(lib):
+    """The skip GEMM shape (K = 1600, N = 512) against torch fp64."""
+    M, N, K = 1024, 512, 1600
+    g = torch.Generator().manual_seed(2)
+    A = torch.rand(M, K, generator=g, dtype=torch.float64) * 2 - 1
+    Bm = (torch.rand(K, N, generator=g, dtype=torch.float64) * 2 - 1) * 0.05
+    C = torch.empty(M, N, device=DEV)
+    Ad, Bd = A.float().to(DEV), Bm.float().to(DEV)
+    _lib.check(lib.lbwn_gemm_f32(Ad.data_ptr(), K, 1, Bd.data_ptr(), N, 0, C.data_ptr(), N, M, N, K, None, 0, 0,
+                                 None, 0, 0, 1, None, None))
+    torch.cuda.synchronize()
+    close(C.cpu().numpy(), (A @ Bm).numpy(), 1e-5, 'gemm_skip')
+
+
+# ---- one layer ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize('d,T', [(1, 128), (2, 200), (64, 256), (512, 300), (256, 100), (8, 1024)])
+@pytest.mark.parametrize('C', [32, 5])
+def test_layer_forward(lib, d, T, C):
+    B, H = 2, 512
+    rng = np.random.default_rng(d + T + C)
+    xbuf = rng.uniform(-1, 1, size=(B, H + T, C))
+    Ws = rng.uniform(-0.3, 0.3, size=(2, C, C))
+    Wg = rng.uniform(-0.3, 0.3, size=(2, C, C))
+    bs, bg = rng.uniform(-0.1, 0.1, C), rng.uniform(-0.1, 0.1, C)
+    Wr, br = rng.uniform(-0.3, 0.3, size=(C, C)), rng.uniform(-0.1, 0.1, C)
+    x = xbuf[:, H:]
+    prev = xbuf[:, H - d:H - d + T]
+    z = np.tanh(prev @ Ws[0] + x @ Ws[1] + bs) * R._sigmoid(prev @ Wg[0] + x @ Wg[1] + bg)
+    xo = x + z @ Wr + br
+    t = lambda a: torch.tensor(a, dtype=torch.float32, device=DEV).contiguous()
+    xin, ws_, wg_, bs_, bg_, wr_, br_ = map(t, (xbuf, Ws, Wg, bs, bg, Wr, br))
+    zout = torch.zeros(B * T, C, device=DEV)
+    xout = torch.zeros(B, H + T, C, device=DEV)
+    _lib.check(lib.lbwn_layer_forward(xin.data_ptr(), xout.data_ptr(), zout.data_ptr(), C, ws_.data_ptr(),
+                                      wg_.data_ptr(), bs_.data_ptr(), bg_.data_ptr(), wr_.data_ptr(), br_.data_ptr(),
+                                      None, None, None, 0, B, T, H, d, C, C, None))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(zout.cpu().numpy().reshape(B, T, C), z, rtol=0, atol=1e-5)
+    np.testing.assert_allclose(xout.cpu().numpy()[:, H:], xo, rtol=0, atol=2e-5)
+
+
+# ---- head --------------------------------------------------------------------------------
+
+def test_head_xent(lib):
+    B, T, Q = 3, 257, 256
+    rng = np.random.default_rng(5)
+    lg = rng.normal(size=(B, T, Q)) * 3
+    q, ids = rand_batch(dict(n_quant=Q), B, T, invalid=20)
+    arch = dict(n_quant=Q)
+    st, dlog = R.loss_fcn(arch, {}, lg, q, ids, 0.0)
+    lgd = torch.tensor(lg, dtype=torch.float32, device=DEV).contiguous()
+    qd = torch.tensor(q, device=DEV)
+    idd = torch.tensor(ids, device=DEV)
+    stats = torch.zeros(4, device=DEV)
+    ws = torch.zeros(3 * 2048, device=DEV)
+    _lib.check(lib.lbwn_head_xent(lgd.data_ptr(), qd.data_ptr(), idd.data_ptr(), B, T, Q, 1, stats.data_ptr(),
+                                  ws.data_ptr(), None))
+    s = stats.cpu().numpy()
+    assert int(s[1]) == st['n_valid']
+    np.testing.assert_allclose(s[0], st['sum_xent'], rtol=1e-5)
+    assert int(s[2]) // (B * (T - 1)) == st['avg_diff']
+    np.testing.assert_allclose(lgd.cpu().numpy() / st['n_valid'], dlog, rtol=0, atol=1e-6)
+
+
+# ---- mu-law --------------------------------------------------------------------------------
+
+def test_mulaw_gpu_golden(lib):
+    g = np.load(os.path.join(GOLDEN, 'mulaw.npz'))
+    x = torch.tensor(g['mu_x32'], device=DEV)
+    q = torch.empty(x.numel(), dtype=torch.int32, device=DEV)
+    _lib.check(lib.lbwn_mulaw_encode(x.data_ptr(), q.data_ptr(), x.numel(), 256, 0, None))
+    np.testing.assert_array_equal(q.cpu().numpy(), g['mu_enc32_256'])
+    qs = torch.arange(256, dtype=torch.int32, device=DEV)
+    out = torch.empty(256, device=DEV)
+    _lib.check(lib.lbwn_mulaw_decode(qs.data_ptr(), out.data_ptr(), 256, 256, None))
+    np.testing.assert_allclose(out.cpu().numpy(), R.mu_decode_tf32(np.arange(256), 256), rtol=2e-6, atol=1e-7)
+
+
+# ---- full plan -------------------------------------------------------------------------------
+
+def _run_oracle(arch, net, q, ids):
+    P, S = oracle_params(net)
+    lg, cache, new_save = R.forward(arch, P, q, ids, S)
+    st, dlog = R.loss_fcn(arch, P, lg, q, ids, 0.0)
+    return P, S, lg, cache, new_save, st, dlog
+
+
+@pytest.mark.parametrize('which,B,T', [('small', 2, 256), ('small', 3, 200), ('arch3', 2, 512)])
+def test_plan_forward_backward(which, B, T):
+    arch = arch3() if which == 'arch3' else small_arch()
+    net = make_net(arch, B)
+    q, ids = rand_batch(arch, B, T)
+    P, S, lg, cache, new_save, st, dlog = _run_oracle(arch, net, q, ids)
+    net.forward(q, None, ids, backward=True)
+    torch.cuda.synchronize()
+    L, Cd = R.n_layers(arch), arch['n_dil']
+    # forward activations (z before backward overwrote it is not kept: compare SAVE / stats /
+    # logits-derived quantities, then per-layer z via a fresh forward below)
+    stats = net.stats.cpu().numpy()
+    assert int(stats[1]) == st['n_valid']
+    np.testing.assert_allclose(stats[0] / st['n_valid'], st['mean_xent'], rtol=1e-5)
+    for i, (k, v) in enumerate(new_save.items()):
+        if i == 0:   # layer 0's SAVE is pure data movement of the embedded input: bit-exact
+            np.testing.assert_array_equal(net.save_vars[k].cpu().numpy(), v.astype(np.float32), err_msg=k)
+        else:        # deeper layers hold fp32-computed residual activations
+            close(net.save_vars[k].cpu().numpy(), v, 1e-5, k)
+    # gradients: ours are Σxent-grads (raw); the oracle's are of the mean
+    G = R.backward(arch, P, cache, dlog, 0.0)
+    inv = 1.0 / st['n_valid']
+    for name in net.layout.names():
+        ours = net.grads[name].cpu().double().numpy() * inv
+        close(ours, G[name], 2e-4, name)
+    # fresh forward with the original SAVE: z of every layer, skip sum, logits
+    net2 = make_net(arch, B)
+    net2.forward(q, None, ids, backward=False)
+    torch.cuda.synchronize()
+    M = B * T
+    z = net2.plan_tensor(T, 'z').view(M, L * Cd).cpu().numpy()
+    # (a) north_star bar: conv activations within 1e-5 on IDENTICAL inputs -> feed the
+    #     oracle's layer the GPU's own x_l (halo = SAVE) and compare z_l.
+    H = 2 ** (arch['n_block_layers'] - 1)
+    Cr = arch['n_res']
+    xs = net2.plan_tensor(T, 'x')
+    stride = xs.numel() // L
+    for l, b, bl, d in ((l,) + R.layer_index(arch, l) for l in range(L)):
+        xb = xs[l * stride:l * stride + B * (H + T) * Cr].view(B, H + T, Cr).cpu().double().numpy()
+        sfx = '_%d_%d' % (b, bl)
+        prev, x = xb[:, H - d:H - d + T], xb[:, H:]
+        v = {nm: prev @ P[nm + sfx][0] + x @ P[nm + sfx][1] + P[nm + '_BIAS' + sfx] for nm in ('SIGNAL', 'GATE')}
+        zl = np.tanh(v['SIGNAL']) * R._sigmoid(v['GATE'])
+        np.testing.assert_allclose(z[:, l * Cd:(l + 1) * Cd], zl.reshape(M, Cd), rtol=0, atol=1e-5,
+                                   err_msg='z layer %d (identical inputs)' % l)
+    # (b) end to end through L layers of fp32 residual accumulation vs float64
+    for l in range(L):
+        np.testing.assert_allclose(z[:, l * Cd:(l + 1) * Cd], cache['z'][l].reshape(M, Cd), rtol=0, atol=5e-5,
+                                   err_msg='z layer %d (end to end)' % l)
+    s = net2.plan_tensor(T, 's').view(M, -1).cpu().numpy()
+    close(s, cache['S'].reshape(M, -1), 1e-5, 'skip sum')
+    r2 = net2.plan_tensor(T, 'r2').view(M, -1).cpu().numpy()
+    close(r2, cache['r2'].reshape(M, -1), 2e-5, 'relu2')
+
+
+def test_staged_equals_unstaged_bitwise():
+    """README.md:6-21: processing a stream in stages with the saved D-separation state is
+    the same function as one long slice.  Position-wise kernels make it bit-exact."""
+    arch = small_arch()
+    B, T = 2, 512
+    q, ids = rand_batch(arch, B, T)
+    a = make_net(arch, B)
+    a.forward(q, None, ids, backward=False)
+    full = a.plan_tensor(T, 'r2').view(B, T, -1).clone()
+    save_full = a.save_flat.clone()
+    b = make_net(arch, B)
+    parts = []
+    for lo, hi in ((0, 128), (128, 384), (384, 512)):
+        b.forward(q[:, lo:hi], None, ids[:, lo:hi], backward=False)
+        parts.append(b.plan_tensor(hi - lo, 'r2').view(B, hi - lo, -1).clone())
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(parts, 1), full)
+    assert torch.equal(b.save_flat, save_full)
+
+
+def test_adam_step_matches_oracle():
+    arch = small_arch(nb=1, nbl=3)
+    B, T = 2, 128
+    net = make_net(arch, B, l2=1e-3)
+    q, ids = rand_batch(arch, B, T)
+    P, S = oracle_params(net)
+    opt_o = R.AdamTF1(1e-3)
+    opt = AdamOptimizer(1e-3)
+    for step in range(3):
+        lg, cache, S = R.forward(arch, P, q, ids, S)
+        st, dlog = R.loss_fcn(arch, P, lg, q, ids, 1e-3)
+        G = R.backward(arch, P, cache, dlog, 1e-3)
+        opt_o.step(P, G)
+        gv, loss = net.build(q, None, ids)
+        np.testing.assert_allclose(float(loss), st['total'], rtol=2e-5)
+        opt.apply_gradients(gv)
+    torch.cuda.synchronize()
+    # Adam normalises each element's step (m/√v): elements whose gradient is ~0 can take a
+    # ±lr step on rounding noise, so bound the max by the step size and the bulk tightly.
+    for name in net.layout.names():
+        d = np.abs(net.vars[name].cpu().double().numpy() - P[name])
+        assert d.max() <= 2 * 3 * 1e-3 + 1e-6, name
+        assert np.mean(d) <= 2e-6, (name, np.mean(d))
+    assert net.counters[0].item() == 3 and net.counters[1].item() == 3 * st['n_valid']
