@@ -67,6 +67,13 @@ size_t lbwn_plan_workspace_bytes(const lbwn_plan* plan);
  * "z" [M][L·n_dil] (gate outputs; dZ after backward), "s" [M][n_skip] (skip sum; dS after
  * backward), "r2" [M][n_post], "logits" [M][n_quant] (dlogits after forward).  */
 int lbwn_plan_tensor(const lbwn_plan* plan, const char* name, size_t* offset, size_t* bytes);
+/* One-shot timing probe: the next lbwn_train_forward/backward on this plan records
+ * hipEvent_t ev_start right before and ev_stop right after the named launch(es):
+ * "layer_fwd" (all residual-layer forward launches), "layer_fwd@<l>" (layer l only),
+ * "layer_bwd", "layer_bwd@<l>", "skip_fwd" (S = Zcat·SKIPcat), "post1_fwd", "post2_fwd",
+ * "head", "dskip" (Zcatᵀ·dS), "dz" (dS·SKIPcatᵀ), "dpost1", "dpost2".  Events are the
+ * caller's (e.g. torch.cuda.Event(enable_timing=True).cuda_event). */
+int lbwn_plan_probe(lbwn_plan* plan, const char* launch_name, void* ev_start, void* ev_stop);
 /* receptive field F = n_blocks·Σ2^l (tmodel.py:50-51) */
 int lbwn_recep_field_sz(const lbwn_arch* arch);
 

@@ -23,7 +23,45 @@ struct lbwn_plan {
   long x_layer_stride;  // floats
   int split_post2, split_post1, split_skip, split_pre;
   long split_floats;
+  // one-shot event probe
+  char probe[32];
+  hipEvent_t probe_start, probe_stop;
 };
+
+namespace {
+struct Probe {
+  lbwn_plan* p;
+  hipStream_t st;
+  bool on;
+  // name: launch kind; l: layer index (-1 = not a layer launch); first/last: span of a kind
+  Probe(lbwn_plan* p_, hipStream_t s, const char* name, int l = -1, bool first = true) : p(p_), st(s), on(false) {
+    if (!p->probe[0]) return;
+    char full[40];
+    snprintf(full, sizeof(full), "%s@%d", name, l);
+    if (!strcmp(p->probe, full) || (!strcmp(p->probe, name) && first)) {
+      (void)hipEventRecord(p->probe_start, st);
+    }
+  }
+  static void end(lbwn_plan* p, hipStream_t st, const char* name, int l = -1, bool last = true) {
+    if (!p->probe[0]) return;
+    char full[40];
+    snprintf(full, sizeof(full), "%s@%d", name, l);
+    if (!strcmp(p->probe, full) || (!strcmp(p->probe, name) && last)) {
+      (void)hipEventRecord(p->probe_stop, st);
+      p->probe[0] = 0;
+    }
+  }
+};
+}  // namespace
+
+int lbwn_plan_probe(lbwn_plan* p, const char* name, void* ev_start, void* ev_stop) {
+  LBWN_REQUIRE(p && name && ev_start && ev_stop, "plan_probe: null argument");
+  LBWN_REQUIRE(strlen(name) < sizeof(p->probe), "plan_probe: name too long");
+  strcpy(p->probe, name);
+  p->probe_start = (hipEvent_t)ev_start;
+  p->probe_stop = (hipEvent_t)ev_stop;
+  return 0;
+}
 
 namespace {
 
@@ -169,7 +207,9 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     a.d = 1 << (l % p->nbl);
     a.Cr = Cr;
     a.Cd = Cd;
+    Probe(p, st, "layer_fwd", l, l == 0);
     if ((e = lbwn_layer_fwd_launch(a, st))) return e;
+    Probe::end(p, st, "layer_fwd", l, l == L - 1);
   }
   // SAVE_l <- last d rows of [SAVE ++ x_l]  (tmodel.py:165)
   if ((e = lbwn_dsep_save_launch(X, p->x_layer_stride, save, L, p->nbl, B, T, H, Cr, st))) return e;
@@ -180,23 +220,31 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   }
   g.A = Z; g.lda = ldz; g.B = P->skip; g.ldb = p->Cs; g.C = S; g.ldc = p->Cs;
   g.M = (int)M; g.N = p->Cs; g.K = (int)ldz; g.bias = P->skip_b ? bsum : nullptr;
+  Probe(p, st, "skip_fwd");
   if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
+  Probe::end(p, st, "skip_fwd");
   // relu(relu(S)·POST1 + b1)  (tmodel.py:194-203)
   g = gemm0();
   g.A = S; g.lda = p->Cs; g.B = P->post1; g.ldb = p->Cp; g.C = R2; g.ldc = p->Cp;
   g.M = (int)M; g.N = p->Cp; g.K = p->Cs; g.bias = P->post1_b; g.relu_a = 1; g.relu_out = 1;
+  Probe(p, st, "post1_fwd");
   if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
+  Probe::end(p, st, "post1_fwd");
   // logits = R2·POST2 + b2  (tmodel.py:204-209)
   g = gemm0();
   g.A = R2; g.lda = p->Cp; g.B = P->post2; g.ldb = p->Q; g.C = LOG; g.ldc = p->Q;
   g.M = (int)M; g.N = p->Q; g.K = p->Cp; g.bias = P->post2_b;
+  Probe(p, st, "post2_fwd");
   if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
+  Probe::end(p, st, "post2_fwd");
   // masked softmax-xent (+ unnormalised dlogits in place)  (tmodel.py:228-249)
   lbwn_head_args h;
   h.logits = LOG; h.q = wav_q; h.ids = ids; h.B = B; h.T = T; h.Q = p->Q;
   h.partial = at<float>(ws, p->oHEADP); h.write_grad = 1;
   int nb = 0;
+  Probe(p, st, "head");
   if ((e = lbwn_head_launch(h, &nb, st))) return e;
+  Probe::end(p, st, "head");
   return lbwn_stats_reduce_launch(h.partial, nb, stats, st);
 }
 
@@ -219,7 +267,9 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   // dPOST2 = R2ᵀ·dlogits, db2 = Σ dlogits
   g = gemm0();
   g.A = R2; g.lda = Cp; g.B = LOG; g.ldb = Q; g.C = G->post2; g.ldc = Q; g.M = Cp; g.N = Q; g.K = (int)M;
+  Probe(p, st, "dpost2");
   if ((e = lbwn_gemm_launch(g, 0, 0, p->split_post2, SPL, st))) return e;
+  Probe::end(p, st, "dpost2");
   if (G->post2_b && (e = lbwn_colsum_launch(LOG, Q, (int)M, Q, G->post2_b, 0, COLS, st))) return e;
   // dH1 = dlogits·POST2ᵀ ⊙ (R2 > 0)   (in place over R2)
   g = gemm0();
@@ -230,7 +280,9 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   g = gemm0();
   g.A = S; g.lda = Cs; g.relu_a = 1; g.B = R2; g.ldb = Cp; g.C = G->post1; g.ldc = Cp; g.M = Cs; g.N = Cp;
   g.K = (int)M;
+  Probe(p, st, "dpost1");
   if ((e = lbwn_gemm_launch(g, 0, 0, p->split_post1, SPL, st))) return e;
+  Probe::end(p, st, "dpost1");
   if (G->post1_b && (e = lbwn_colsum_launch(R2, Cp, (int)M, Cp, G->post1_b, 0, COLS, st))) return e;
   // dS = dH1·POST1ᵀ ⊙ (S > 0)   (in place over S)
   g = gemm0();
@@ -240,7 +292,9 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   // dSKIPcat = Zcatᵀ·dS; every layer's SKIP_BIAS gets the same Σ dS
   g = gemm0();
   g.A = Z; g.lda = ldz; g.B = S; g.ldb = Cs; g.C = G->skip; g.ldc = Cs; g.M = (int)ldz; g.N = Cs; g.K = (int)M;
+  Probe(p, st, "dskip");
   if ((e = lbwn_gemm_launch(g, 0, 0, p->split_skip, SPL, st))) return e;
+  Probe::end(p, st, "dskip");
   if (G->skip_b) {
     if ((e = lbwn_colsum_launch(S, Cs, (int)M, Cs, G->skip_b, 0, COLS, st))) return e;
     if ((e = lbwn_bcast_rows_launch(G->skip_b, L, Cs, st))) return e;
@@ -248,7 +302,9 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   // dZ = dS·SKIPcatᵀ  (over Z: z is recomputed by the layer backward)
   g = gemm0();
   g.A = S; g.lda = Cs; g.B = P->skip; g.ldb = Cs; g.C = Z; g.ldc = ldz; g.M = (int)M; g.N = (int)ldz; g.K = Cs;
+  Probe(p, st, "dz");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
+  Probe::end(p, st, "dz");
   // residual stack in reverse; layer l reduces layer l+1's weight-grad partials on the fly
   const int nblk = lbwn_layer_nblocks(B, T);
   for (int l = L - 1; l >= 0; --l) {
@@ -284,7 +340,9 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     a.out_c0 = at<float>(ws, p->oGC0[l & 1]);
     a.slab = at<float>(ws, p->oSLAB[l & 1]);
     a.slab_stride = lbwn_layer_slab_stride();
+    Probe(p, st, "layer_bwd", l, l == L - 1);
     if ((e = lbwn_layer_bwd_launch(a, st))) return e;
+    Probe::end(p, st, "layer_bwd", l, l == 0);
   }
   {  // layer 0's partials
     lbwn_layer_args a;

@@ -43,6 +43,7 @@ _SIGS = {
     'lbwn_plan_create': (c_int, [ctypes.POINTER(Arch), c_int, c_int, ctypes.POINTER(c_void_p)]),
     'lbwn_plan_destroy': (None, [c_void_p]),
     'lbwn_plan_workspace_bytes': (c_size_t, [c_void_p]),
+    'lbwn_plan_probe': (c_int, [c_void_p, ctypes.c_char_p, c_void_p, c_void_p]),
     'lbwn_plan_tensor': (c_int, [c_void_p, ctypes.c_char_p, ctypes.POINTER(c_size_t), ctypes.POINTER(c_size_t)]),
     'lbwn_train_forward': (c_int, [c_void_p, ctypes.POINTER(Params), c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_void_p]),
     'lbwn_train_backward': (c_int, [c_void_p, ctypes.POINTER(Params), ctypes.POINTER(Params), c_fp, c_fp, c_fp,
