@@ -104,6 +104,29 @@ int lbwn_adam_tf1(float* params, const float* grads, float* m, float* v, int64_t
                   float lr, float beta1, float beta2, float eps, float l2_factor, const float* stats,
                   int64_t* counters, void* stream);
 
+/* ---- cached autoregressive generation (imodel.WaveNetGen, imodel.py:7-303) ------------ */
+typedef struct lbwn_gen_plan lbwn_gen_plan;
+/* B streams, outputs for up to max_steps samples, teacher vector up to max_teacher codes. */
+int lbwn_gen_plan_create(const lbwn_arch* arch, int batch_sz, int64_t max_steps, int64_t max_teacher,
+                         lbwn_gen_plan** out);
+void lbwn_gen_plan_destroy(lbwn_gen_plan* plan);
+size_t lbwn_gen_workspace_bytes(const lbwn_gen_plan* plan);
+/* "samples" int32 [B][max_steps] (drawn µ-law codes), "wav" fp32 [B][max_steps]
+ * (mu_decode of the draws, imodel.py:181-182), "logits" [B][Q] (last step), "step" int64,
+ * "rings" (lookback state, SAVE layout), "teacher" int32. */
+int lbwn_gen_tensor(const lbwn_gen_plan* plan, const char* name, size_t* offset, size_t* bytes);
+/* Reset the state (zero lookback rings = imodel's zero-initialised buffers, step 0 input =
+ * zero vector), load the teacher codes (device int32, may be NULL) and GC ids (device
+ * int32 [B], GC archs; imodel.py:53-56).  pre_bias=1 adds PRE_BIAS to the input embedding
+ * (tmodel-consistent); 0 reproduces imodel.py:75-77 literally.  Draws use
+ * u = splitmix64(seed, stream, step) >> 40 / 2^24 and the inverse softmax CDF (the
+ * reference's tf.multinomial, imodel.py:179, is TF-RNG and not reproducible). */
+int lbwn_gen_start(lbwn_gen_plan* plan, const lbwn_params* params, void* workspace, const int* gc_ids,
+                   const int* teacher, int64_t n_teacher, uint64_t seed, int pre_bias, void* stream);
+/* Generate n_steps more samples for every stream (the tf.while_loop body, imodel.py:214-272).
+ * Device-resident step counter: the launches are graph-capturable and replayable. */
+int lbwn_gen_run(lbwn_gen_plan* plan, const lbwn_params* params, void* workspace, int n_steps, void* stream);
+
 /* ---- fine-grained kernels (parity tests, custom drivers) ------------------------------ */
 /* ops.mu_encode_np (ops.py:23-28, tf32=0, float64 math) / ops.mu_encode (ops.py:4-9, tf32=1) */
 int lbwn_mulaw_encode(const float* x, int* q, int64_t n, int n_quanta, int tf32, void* stream);
@@ -121,11 +144,14 @@ int lbwn_gemm_f32(const float* A, int64_t lda, int a_kcontig, const float* B, in
 /* One residual layer forward (tmodel.py:117-184): x_in is the [B][H+T][n_res] halo
  * buffer whose rows [H-d, H) hold SAVE; writes z [M][*] (row stride ldz) and, if x_out,
  * x_out body rows (x + z·RES + b). gc_tab [n_cat+1][2·n_dil] / ids, cond [M][2·n_dil]
- * (row stride ldcond) are optional conditioning adds. */
+ * (row stride ldcond) are optional conditioning adds.  wpack_ws: 16-B aligned scratch of
+ * lbwn_layer_image_floats_abi() floats for the packed weight image. */
+int lbwn_layer_image_floats_abi(void);
 int lbwn_layer_forward(const float* x_in, float* x_out, float* z, int64_t ldz, const float* w_sig,
                        const float* w_gate, const float* b_sig, const float* b_gate, const float* w_res,
                        const float* b_res, const float* gc_tab, const int* ids, const float* cond,
-                       int64_t ldcond, int B, int T, int H, int dilation, int n_res, int n_dil, void* stream);
+                       int64_t ldcond, int B, int T, int H, int dilation, int n_res, int n_dil, float* wpack_ws,
+                       void* stream);
 
 /* D-separation prepend/save for all layers at once (tmodel.py:122-127, :165). */
 int lbwn_dsep_prepend(float* x_all, int64_t x_layer_stride, const float* save, int n_layers, int n_block_layers,

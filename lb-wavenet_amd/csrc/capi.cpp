@@ -57,11 +57,13 @@ int lbwn_gemm_f32(const float* A, int64_t lda, int a_kcontig, const float* B, in
   return lbwn_gemm_launch(g, a_kcontig, b_kcontig, split_k, slab_ws, (hipStream_t)stream);
 }
 
+int lbwn_layer_image_floats_abi(void) { return lbwn_layer_image_floats(); }
+
 int lbwn_layer_forward(const float* x_in, float* x_out, float* z, int64_t ldz, const float* w_sig,
                        const float* w_gate, const float* b_sig, const float* b_gate, const float* w_res,
                        const float* b_res, const float* gc_tab, const int* ids, const float* cond, int64_t ldcond,
-                       int B, int T, int H, int dilation, int n_res, int n_dil, void* stream) {
-  LBWN_REQUIRE(x_in && z && w_sig && w_gate && w_res, "layer_forward: null argument");
+                       int B, int T, int H, int dilation, int n_res, int n_dil, float* wpack_ws, void* stream) {
+  LBWN_REQUIRE(x_in && z && w_sig && w_gate && w_res && wpack_ws, "layer_forward: null argument");
   LBWN_REQUIRE(!gc_tab || ids, "layer_forward: gc_tab needs ids");
   lbwn_layer_args a;
   memset(&a, 0, sizeof(a));
@@ -69,6 +71,10 @@ int lbwn_layer_forward(const float* x_in, float* x_out, float* z, int64_t ldz, c
   a.w_sig = w_sig; a.w_gate = w_gate; a.b_sig = b_sig; a.b_gate = b_gate; a.w_res = w_res; a.b_res = b_res;
   a.gc_tab = gc_tab; a.ids = ids; a.cond = cond; a.ldcond = (long)ldcond;
   a.B = B; a.T = T; a.H = H; a.d = dilation; a.Cr = n_res; a.Cd = n_dil;
+  a.wpack = wpack_ws;
+  if (int e = lbwn_pack_layers_launch(w_sig, w_gate, b_sig, b_gate, w_res, b_res, wpack_ws, 1, n_res, n_dil,
+                                      (hipStream_t)stream))
+    return e;
   return lbwn_layer_fwd_launch(a, (hipStream_t)stream);
 }
 

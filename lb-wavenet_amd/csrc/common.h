@@ -17,9 +17,10 @@ LBWN_DEV floatx16 mfma32(float a, float b, floatx16 c) {
 // Row of accumulator register r for lane half h.
 LBWN_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-// Accurate (ocml) transcendental forms: the gate is MFMA/HBM-bound, not VALU-bound, and
-// parity is 1e-5 against a float64 oracle.
-LBWN_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+// Gate transcendentals on the hardware v_exp_f32 / v_rcp_f32 (≈1 ulp each): σ(x) =
+// 1/(1+e^-x); tanh(x) = 2σ(2x) - 1 (absolute error ≈1e-7, inside the 1e-5 parity bar).
+LBWN_DEV float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+LBWN_DEV float tanhf_(float x) { return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f; }
 
 // Host-side error plumbing (defined in capi.cpp).
 void lbwn_set_error(const char* fmt, ...);

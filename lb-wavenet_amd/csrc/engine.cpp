@@ -18,7 +18,7 @@ struct lbwn_plan {
   int B, T, L, nbl, H, Cr, Cd, Cs, Cp, Q;
   long M;
   // workspace carving (byte offsets)
-  size_t oX, oZ, oS, oR2, oLOG, oGA[2], oGC0[2], oDX0, oSLAB[2], oSPLIT, oCOLS, oHEADP, oBSUM;
+  size_t oX, oZ, oS, oR2, oLOG, oGA[2], oGC0[2], oDX0, oSLAB[2], oSPLIT, oCOLS, oHEADP, oBSUM, oWPK;
   size_t total;
   long x_layer_stride;  // floats
   int split_post2, split_post1, split_skip, split_pre;
@@ -71,11 +71,14 @@ size_t carve(size_t& cur, size_t bytes) {
   return o;
 }
 
+// Split-K for the weight-gradient GEMMs (K = B·T positions).  One 4-wave block per CU
+// leaves the MFMA pipe latency-exposed, so aim for ~4 resident blocks per CU (1024 blocks)
+// with the slab traffic capped at 64 MB.
 int pick_split(int M, int N, long K) {
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  int s = std::max(1, 512 / tiles);
-  s = (int)std::min<long>(s, std::max<long>(1, K / 256));
-  return s;
+  const long slab_cap = std::max<long>(1, (64L << 20) / (4L * M * N));
+  const long s = std::max<long>(1, std::min<long>({1024 / tiles, K / 512, slab_cap}));
+  return (int)s;
 }
 
 template <typename T>
@@ -126,7 +129,7 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->split_pre = pick_split(p->Q, p->Cr, M);
   p->split_floats = std::max({(long)p->split_post2 * p->Cp * p->Q, (long)p->split_post1 * p->Cs * p->Cp,
                               (long)p->split_skip * ldz * p->Cs, (long)p->split_pre * p->Q * p->Cr});
-  const int nblk = lbwn_layer_nblocks(B, T);
+  const int nblk = lbwn_layer_bwd_grid(B, T);
   size_t cur = 0;
   p->oX = carve(cur, sizeof(float) * (size_t)p->x_layer_stride * L);
   p->oZ = carve(cur, sizeof(float) * (size_t)M * ldz);
@@ -143,6 +146,7 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->oCOLS = carve(cur, sizeof(float) * (size_t)lbwn_colsum_ws_floats((int)M, std::max({p->Cs, p->Cp, p->Q, p->Cr})));
   p->oHEADP = carve(cur, sizeof(float) * 3 * 2048);
   p->oBSUM = carve(cur, sizeof(float) * (size_t)p->Cs);
+  p->oWPK = carve(cur, sizeof(float) * (size_t)L * lbwn_layer_image_floats());
   p->total = cur;
   *out = p;
   return 0;
@@ -183,6 +187,10 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   float* LOG = at<float>(ws, p->oLOG);
   float* bsum = at<float>(ws, p->oBSUM);
   int e;
+  // per-layer weights -> padded LDS images (once per step; reused by the backward)
+  float* WPK = at<float>(ws, p->oWPK);
+  if ((e = lbwn_pack_layers_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b, WPK, L, Cr, Cd, st)))
+    return e;
   // one-hot·PRE + PRE_BIAS == row gather (tmodel.py:53-66, :86-102)
   if ((e = lbwn_embed_launch(wav_q, P->pre, P->pre_b, X, B, T, H, Cr, p->Q, st))) return e;
   // D-separation prepend for every layer (tmodel.py:122-127)
@@ -200,6 +208,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     a.b_gate = P->gate_b ? P->gate_b + (long)l * Cd : nullptr;
     a.w_res = P->res + (long)l * Cd * Cr;
     a.b_res = P->res_b ? P->res_b + (long)l * Cr : nullptr;
+    a.wpack = WPK + (long)l * lbwn_layer_image_floats();
     a.ids = ids;
     a.B = B;
     a.T = T;
@@ -306,7 +315,8 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
   Probe::end(p, st, "dz");
   // residual stack in reverse; layer l reduces layer l+1's weight-grad partials on the fly
-  const int nblk = lbwn_layer_nblocks(B, T);
+  const int nblk = lbwn_layer_bwd_grid(B, T);
+  const float* WPK = at<float>(ws, p->oWPK);
   for (int l = L - 1; l >= 0; --l) {
     lbwn_layer_args a;
     memset(&a, 0, sizeof(a));
@@ -317,6 +327,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     a.b_gate = P->gate_b ? P->gate_b + (long)l * Cd : nullptr;
     a.w_res = P->res + (long)l * Cd * Cr;
     a.b_res = P->res_b ? P->res_b + (long)l * Cr : nullptr;
+    a.wpack = WPK + (long)l * lbwn_layer_image_floats();
     a.ids = ids;
     a.B = B; a.T = T; a.H = H; a.d = 1 << (l % p->nbl); a.Cr = Cr; a.Cd = Cd;
     a.dz_skip = Z + (long)l * Cd;

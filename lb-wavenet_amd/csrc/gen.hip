@@ -1,0 +1,467 @@
+// Cached single-step autoregressive generation (imodel.py:61-272).
+//
+// Per generated sample, all state stays on device so a chunk of steps can be captured in a
+// hipGraph and replayed: the step counter, the per-layer lookback rings (the generation
+// form of the D-separation cache: layer l keeps its last d inputs, slot t mod d, replacing
+// imodel's shift-by-chunk buffers imodel.py:88-98, :190-207), the next input code, the
+// teacher vector and a counter-based RNG.  One step =
+//   gen_chain   1 workgroup per 16 streams: PRE row (+bias), 50 × [dilated conv (VALU; B is
+//               ~10 so a 32-wide MFMA tile would be mostly padding), gate, residual], z_cat out
+//   gen_rowvec  × 3: skip = z_cat·SKIPcat + Σb, h = relu(relu(skip)·POST1 + b1),
+//               logits = h·POST2 + b2 (weights L2-resident across steps)
+//   gen_sample  inverse-CDF draw of softmax(logits) with u = hash(seed, stream, step),
+//               µ-law decode, next input = teacher[t] or the draw (imodel.py:167-187, :260-269)
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int GB = 16;                 // streams per chain workgroup
+constexpr int WIMG_G = 64 * 64 + 32 * 32 + 96;  // conv W[k][o] (64×64) | RES[c][o] (32×32) | b_conv[64] | b_res[32]
+
+struct ChainK {
+  const float* pre; const float* pre_b;
+  const float* sig; const float* gate; const float* sig_b; const float* gate_b;
+  const float* res; const float* res_b;
+  const float* gc_proj;   // [L][B][64] or null
+  float* rings;           // packed per layer [B][d][Cr]
+  float* zcat;            // [B][L*Cd]
+  const long long* step;  // current step t
+  int* code;              // [B] input code for this step (-1 = zero vector)
+  int B, L, nbl, Cr, Cd, Q, pre_bias;
+};
+
+LBWN_DEV long ring_offset(int l, int nbl, int B, int Cr) {
+  const long s = (long)(l / nbl) * ((1L << nbl) - 1) + ((1L << (l % nbl)) - 1);
+  return s * B * Cr;
+}
+
+// stage layer l's weights (reference layouts) into registers -> LDS image
+struct WStage {
+  static constexpr int N = (WIMG_G + 1023) / 1024;  // 6 per thread
+  float v[N];
+  LBWN_DEV void load(const ChainK& a, int l, int tid) {
+    const int Cr = a.Cr, Cd = a.Cd;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int e = tid + 1024 * i;
+      float x = 0.f;
+      if (e < 64 * 64) {
+        const int k = e >> 6, o = e & 63, tap = k >> 5, in = k & 31, oc = o & 31;
+        if (in < Cr && oc < Cd) x = (o < 32 ? a.sig : a.gate)[(long)l * 2 * Cr * Cd + (tap * Cr + in) * Cd + oc];
+      } else if (e < 64 * 64 + 32 * 32) {
+        const int f = e - 64 * 64, c = f >> 5, o = f & 31;
+        if (c < Cd && o < Cr) x = a.res[(long)l * Cd * Cr + c * Cr + o];
+      } else if (e < WIMG_G) {
+        const int f = e - 64 * 64 - 32 * 32;
+        if (f < 64) {
+          const float* bb = f < 32 ? a.sig_b : a.gate_b;
+          if (bb && (f & 31) < Cd) x = bb[(long)l * Cd + (f & 31)];
+        } else if (a.res_b && f - 64 < Cr) {
+          x = a.res_b[(long)l * Cr + f - 64];
+        }
+      }
+      v[i] = x;
+    }
+  }
+  LBWN_DEV void store(float* W, int tid) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int e = tid + 1024 * i;
+      if (e < WIMG_G) W[e] = v[i];
+    }
+  }
+};
+
+__global__ __launch_bounds__(1024) void gen_chain_kernel(ChainK a) {
+  __shared__ __attribute__((aligned(16))) float Wb[2][WIMG_G];
+  __shared__ float X[GB][32];       // current layer input
+  __shared__ float PV[2][GB][32];   // prefetched prev tap (double buffer over layers)
+  __shared__ float Z[GB][32];
+  __shared__ float P[4][GB][64];    // conv partials over 4 K-quarters
+  const int tid = threadIdx.x;
+  const int b0 = blockIdx.x * GB;
+  const int nb = min(GB, a.B - b0);
+  const long t = *a.step;
+  const int Cr = a.Cr, Cd = a.Cd;
+
+  WStage ws;
+  ws.load(a, 0, tid);
+  // input z0 = onehot(code)·PRE (+ PRE_BIAS): zero vector at step 0 (imodel.py:61-79)
+  if (tid < GB * 32) {
+    const int b = tid >> 5, c = tid & 31;
+    float v = 0.f;
+    if (b < nb && c < Cr) {
+      const int code = a.code[b0 + b];
+      if (code >= 0) v = a.pre[(long)code * Cr + c];
+      if (a.pre_bias && a.pre_b) v += a.pre_b[c];
+    }
+    X[b][c] = v;
+  }
+  // prev tap of layer 0: input of layer 0 at t - d (ring slot t mod d, zero-initialised)
+  auto load_prev = [&](int l, int buf) {
+    if (tid < GB * 32) {
+      const int b = tid >> 5, c = tid & 31;
+      const int d = 1 << (l % a.nbl);
+      float v = 0.f;
+      if (b < nb && c < Cr) v = a.rings[ring_offset(l, a.nbl, a.B, Cr) + ((long)(b0 + b) * d + (t % d)) * Cr + c];
+      PV[buf][b][c] = v;
+    }
+  };
+  load_prev(0, 0);
+  ws.store(Wb[0], tid);
+  __syncthreads();
+
+  for (int l = 0; l < a.L; ++l) {
+    const int cur = l & 1;
+    const float* W = Wb[cur];
+    if (l + 1 < a.L) ws.load(a, l + 1, tid);   // prefetch next layer's weights (lands during compute)
+    // ring write: this layer's input at slot t mod d (the prev tap was read before)
+    if (tid < GB * 32) {
+      const int b = tid >> 5, c = tid & 31;
+      const int d = 1 << (l % a.nbl);
+      if (b < nb && c < Cr)
+        a.rings[ring_offset(l, a.nbl, a.B, Cr) + ((long)(b0 + b) * d + (t % d)) * Cr + c] = X[b][c];
+    }
+    // conv partials: thread (o, kq, bq): 4 streams × 16 k
+    {
+      const int o = tid & 63, kq = (tid >> 6) & 3, bq = tid >> 8;
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 16; ++kk) {
+        const int k = kq * 16 + kk;
+        const float w = W[k * 64 + o];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int b = bq * 4 + j;
+          const float xv = k < 32 ? PV[cur][b][k] : X[b][k - 32];
+          acc[j] = fmaf(xv, w, acc[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) P[kq][bq * 4 + j][o] = acc[j];
+    }
+    if (l + 1 < a.L) load_prev(l + 1, cur ^ 1);
+    __syncthreads();
+    // gate
+    if (tid < GB * 32) {
+      const int b = tid >> 5, c = tid & 31;
+      const float* bs = W + 64 * 64 + 32 * 32;
+      float vs = bs[c], vg = bs[32 + c];
+#pragma unroll
+      for (int kq = 0; kq < 4; ++kq) { vs += P[kq][b][c]; vg += P[kq][b][32 + c]; }
+      if (a.gc_proj && b < nb) {
+        const float* g = a.gc_proj + ((long)l * a.B + b0 + b) * 64;
+        vs += g[c];
+        vg += g[32 + c];
+      }
+      const float z = (c < Cd && b < nb) ? tanhf_(vs) * sigmoidf_(vg) : 0.f;
+      Z[b][c] = z;
+      if (b < nb && c < Cd) a.zcat[(long)(b0 + b) * a.L * Cd + l * Cd + c] = z;
+    }
+    __syncthreads();
+    // residual: x += z·RES + b   (thread (o, b) for 512 outputs; K = 32)
+    if (tid < GB * 32) {
+      const int b = tid >> 5, o = tid & 31;
+      const float* R = W + 64 * 64;
+      float r = W[64 * 64 + 32 * 32 + 64 + o];   // b_res
+#pragma unroll 8
+      for (int c = 0; c < 32; ++c) r = fmaf(Z[b][c], R[c * 32 + o], r);
+      X[b][o] += r;
+    }
+    if (l + 1 < a.L) ws.store(Wb[cur ^ 1], tid);
+    __syncthreads();
+  }
+}
+
+// out[b][n] = epi( Σ_k act(in[b][k])·W[k][n] + bias ), b < B (≤ 64 per launch row loop),
+// block = 4 columns; thread (c = tid & 3, ks = tid >> 2): K slice, all streams.
+struct RowK {
+  const float* in; long ldin; const float* W; long ldw; float* out; long ldout;
+  const float* bias; int bias_rows;   // bias = Σ_{r<bias_rows} bias[r*N + n]
+  int B, K, N, relu_in, relu_out;
+};
+
+__global__ __launch_bounds__(256) void gen_rowvec_kernel(RowK a) {
+  extern __shared__ __attribute__((aligned(16))) float xin[];   // [16][K] (act applied)
+  __shared__ float red[64][4][17];
+  const int c = threadIdx.x & 3, ks = threadIdx.x >> 2;  // 64 K slices
+  const int n = blockIdx.x * 4 + c;
+  float acc[16];
+  for (int bb0 = 0; bb0 < a.B; bb0 += 16) {
+    const int nbb = min(16, a.B - bb0);
+    for (int e = threadIdx.x; e < 16 * a.K; e += 256) {
+      const int j = e / a.K, k = e % a.K;
+      float x = 0.f;
+      if (j < nbb) {
+        x = a.in[(long)(bb0 + j) * a.ldin + k];
+        if (a.relu_in) x = fmaxf(x, 0.f);
+      }
+      xin[e] = x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+    if (n < a.N) {
+      for (int k = ks; k < a.K; k += 64) {
+        const float w = a.W[(long)k * a.ldw + n];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j] = fmaf(xin[j * a.K + k], w, acc[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) red[ks][c][j] = acc[j];
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const int cc = threadIdx.x & 3, j = threadIdx.x >> 2;
+      const int nn = blockIdx.x * 4 + cc;
+      if (nn < a.N && j < nbb) {
+        float s = 0.f;
+        for (int q = 0; q < 64; ++q) s += red[q][cc][j];
+        if (a.bias)
+          for (int r = 0; r < a.bias_rows; ++r) s += a.bias[(long)r * a.N + nn];
+        if (a.relu_out) s = fmaxf(s, 0.f);
+        a.out[(long)(bb0 + j) * a.ldout + nn] = s;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+LBWN_DEV uint64_t splitmix(uint64_t seed, uint64_t stream, uint64_t step) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ULL + (stream << 32) + step + 0x632BE59BD9B4E019ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+struct SampleK {
+  const float* logits; int Q, B;
+  long long* step; int* code; const int* teacher; long long n_teacher;
+  int* samples; float* wav; long long max_steps; unsigned long long seed;
+};
+
+// one block; wave w handles streams w, w+16, ...: softmax CDF in a fixed order, first k with
+// cumsum(e)[k] > u·Σe (oracle/wavenet_ref.py sample_from_logits restates the same transform).
+__global__ __launch_bounds__(1024) void gen_sample_kernel(SampleK a) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long t = *a.step;
+  for (int b = w; b < a.B; b += 16) {
+    const float* lg = a.logits + (long)b * a.Q;
+    float mx = -INFINITY;
+    for (int c = lane; c < a.Q; c += 64) mx = fmaxf(mx, lg[c]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    // each lane owns a contiguous run of Q/64 codes: local sums, then an exclusive scan
+    const int per = (a.Q + 63) / 64, c0 = lane * per;
+    float loc = 0.f;
+    for (int j = 0; j < per; ++j)
+      if (c0 + j < a.Q) loc += expf(lg[c0 + j] - mx);
+    float incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    const float total = __shfl(incl, 63);
+    const float excl = incl - loc;
+    const uint64_t h = splitmix(a.seed, (uint64_t)b, (uint64_t)t);
+    const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+    const float target = u * total;
+    // lane whose run contains the crossing point
+    int found = a.Q;
+    if (excl <= target && target < incl) {
+      float run = excl;
+      for (int j = 0; j < per; ++j) {
+        if (c0 + j >= a.Q) break;
+        run += expf(lg[c0 + j] - mx);
+        if (run > target) { found = c0 + j; break; }
+      }
+      if (found == a.Q) found = min(c0 + per, a.Q) - 1;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) found = min(found, __shfl_xor(found, o));
+    if (found >= a.Q) found = a.Q - 1;
+    if (lane == 0) {
+      if (t < a.max_steps) {
+        a.samples[(long)b * a.max_steps + t] = found;
+        const float mu = (float)(a.Q - 1), inv = 1.f / mu;               // ops.py:12-20
+        const float aa = (2.f * (float)found - 1.f) * inv - 1.f;
+        const float sg = aa > 0.f ? 1.f : (aa < 0.f ? -1.f : 0.f);
+        a.wav[(long)b * a.max_steps + t] = sg * (powf(1.f + mu, fabsf(aa)) - 1.f) * inv;
+      }
+      a.code[b] = (t < a.n_teacher) ? a.teacher[t] : found;              // imodel.py:260-269
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *a.step = t + 1;
+}
+
+// gc_proj[l][b][o] = GC_EMBED[gc_id[b]] · [GC_SIGNAL_l | GC_GATE_l]  (imodel.py:53-56, :113-118)
+__global__ void gen_gc_proj_kernel(const float* emb, const float* gsig, const float* ggate, const int* ids,
+                                   float* out, int B, int Ge, int Cd) {
+  const int l = blockIdx.x;
+  for (int e = threadIdx.x; e < B * 64; e += blockDim.x) {
+    const int b = e / 64, o = e % 64, oc = o & 31;
+    float s = 0.f;
+    if (oc < Cd) {
+      const float* G = (o < 32 ? gsig : ggate) + (long)l * Ge * Cd;
+      const float* em = emb + (long)ids[b] * Ge;
+      for (int k = 0; k < Ge; ++k) s += em[k] * G[k * Cd + oc];
+    }
+    out[((long)l * B + b) * 64 + o] = s;
+  }
+}
+
+__global__ void gen_reset_kernel(float* rings, long n_ring, int* code, int B, long long* step) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n_ring; e += (long)gridDim.x * blockDim.x)
+    rings[e] = 0.f;
+  if (blockIdx.x == 0) {
+    for (int b = threadIdx.x; b < B; b += blockDim.x) code[b] = -1;
+    if (threadIdx.x == 0) *step = 0;
+  }
+}
+
+}  // namespace
+
+// ---- host side: generation plan ----------------------------------------------------------
+
+#include "../../include/lbwn.h"
+
+struct lbwn_gen_plan {
+  lbwn_arch a;
+  int B, L, nbl, Cr, Cd, Cs, Cp, Q;
+  long long max_steps;
+  size_t oRING, oZCAT, oSKIP, oH, oLOG, oSTEP, oCODE, oTEACH, oSAMP, oWAV, oGCP, total;
+  long n_ring;
+  long long n_teacher, max_teacher;
+  unsigned long long seed;
+  int pre_bias;
+};
+
+static size_t gcarve(size_t& cur, size_t bytes) {
+  size_t o = cur;
+  cur += (bytes + 255) / 256 * 256;
+  return o;
+}
+
+extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps, int64_t max_teacher,
+                                    lbwn_gen_plan** out) {
+  LBWN_REQUIRE(a && out && B >= 1 && max_steps >= 1 && max_teacher >= 0, "gen_plan_create: bad arguments");
+  LBWN_REQUIRE(a->n_res <= 32 && a->n_dil <= 32, "gen: n_res/n_dil must be <= 32");
+  LBWN_REQUIRE((long)a->n_blocks * a->n_block_layers * a->n_dil <= 2000 && a->n_skip <= 2000 && a->n_post <= 2000,
+               "gen: row-vector GEMM K too large for LDS staging");
+  LBWN_REQUIRE(a->n_lc_out == 0, "gen: local conditioning is not supported by the cached generator "
+                                 "(imodel.py has no LC path)");
+  lbwn_gen_plan* p = new lbwn_gen_plan();
+  p->a = *a;
+  p->B = B;
+  p->nbl = a->n_block_layers;
+  p->L = a->n_blocks * a->n_block_layers;
+  p->Cr = a->n_res; p->Cd = a->n_dil; p->Cs = a->n_skip; p->Cp = a->n_post; p->Q = a->n_quant;
+  p->max_steps = max_steps;
+  p->max_teacher = max_teacher;
+  long dsum = (long)a->n_blocks * ((1L << a->n_block_layers) - 1);
+  p->n_ring = dsum * B * p->Cr;
+  size_t cur = 0;
+  p->oRING = gcarve(cur, 4 * (size_t)p->n_ring);
+  p->oZCAT = gcarve(cur, 4 * (size_t)B * p->L * p->Cd);
+  p->oSKIP = gcarve(cur, 4 * (size_t)B * p->Cs);
+  p->oH = gcarve(cur, 4 * (size_t)B * p->Cp);
+  p->oLOG = gcarve(cur, 4 * (size_t)B * p->Q);
+  p->oSTEP = gcarve(cur, 8);
+  p->oCODE = gcarve(cur, 4 * (size_t)B);
+  p->oTEACH = gcarve(cur, 4 * (size_t)std::max<int64_t>(1, max_teacher));
+  p->oSAMP = gcarve(cur, 4 * (size_t)B * max_steps);
+  p->oWAV = gcarve(cur, 4 * (size_t)B * max_steps);
+  p->oGCP = gcarve(cur, 4 * (size_t)p->L * B * 64);
+  p->total = cur;
+  *out = p;
+  return 0;
+}
+
+extern "C" void lbwn_gen_plan_destroy(lbwn_gen_plan* p) { delete p; }
+extern "C" size_t lbwn_gen_workspace_bytes(const lbwn_gen_plan* p) { return p ? p->total : 0; }
+
+extern "C" int lbwn_gen_tensor(const lbwn_gen_plan* p, const char* name, size_t* off, size_t* bytes) {
+  LBWN_REQUIRE(p && name && off && bytes, "gen_tensor: null argument");
+  const size_t B = p->B;
+  if (!strcmp(name, "samples")) { *off = p->oSAMP; *bytes = 4 * B * p->max_steps; }
+  else if (!strcmp(name, "wav")) { *off = p->oWAV; *bytes = 4 * B * p->max_steps; }
+  else if (!strcmp(name, "logits")) { *off = p->oLOG; *bytes = 4 * B * p->Q; }
+  else if (!strcmp(name, "step")) { *off = p->oSTEP; *bytes = 8; }
+  else if (!strcmp(name, "rings")) { *off = p->oRING; *bytes = 4 * (size_t)p->n_ring; }
+  else if (!strcmp(name, "teacher")) { *off = p->oTEACH; *bytes = 4 * (size_t)std::max<long long>(1, p->n_teacher); }
+  else LBWN_REQUIRE(false, "gen_tensor: unknown tensor '%s'", name);
+  return 0;
+}
+
+template <typename T>
+static T* gat(void* ws, size_t off) {
+  return reinterpret_cast<T*>(static_cast<char*>(ws) + off);
+}
+
+extern "C" int lbwn_gen_start(lbwn_gen_plan* p, const lbwn_params* P, void* ws, const int* gc_ids,
+                              const int* teacher, int64_t n_teacher, uint64_t seed, int pre_bias, void* stream) {
+  LBWN_REQUIRE(p && P && ws, "gen_start: null argument");
+  LBWN_REQUIRE(p->a.n_gc_embed == 0 || gc_ids, "gen_start: GC arch needs gc_ids [B]");
+  LBWN_REQUIRE(!teacher || (n_teacher >= 0 && n_teacher <= p->max_teacher),
+               "gen_start: teacher length %lld exceeds plan capacity %lld", (long long)n_teacher, p->max_teacher);
+  hipStream_t st = (hipStream_t)stream;
+  p->n_teacher = teacher ? n_teacher : 0;
+  p->seed = seed;
+  p->pre_bias = pre_bias;
+  gen_reset_kernel<<<256, 256, 0, st>>>(gat<float>(ws, p->oRING), p->n_ring, gat<int>(ws, p->oCODE), p->B,
+                                        gat<long long>(ws, p->oSTEP));
+  LBWN_CHECK_LAUNCH();
+  if (p->n_teacher > 0) {
+    hipError_t e = hipMemcpyAsync(gat<int>(ws, p->oTEACH), teacher, 4 * (size_t)p->n_teacher, hipMemcpyDeviceToDevice,
+                                  st);
+    LBWN_REQUIRE(e == hipSuccess, "gen_start: teacher copy failed: %s", hipGetErrorString(e));
+  }
+  if (p->a.n_gc_embed > 0) {
+    gen_gc_proj_kernel<<<p->L, 256, 0, st>>>(P->gc_embed, P->gc_sig, P->gc_gate, gc_ids, gat<float>(ws, p->oGCP),
+                                             p->B, p->a.n_gc_embed, p->Cd);
+    LBWN_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+extern "C" int lbwn_gen_run(lbwn_gen_plan* p, const lbwn_params* P, void* ws, int n_steps, void* stream) {
+  LBWN_REQUIRE(p && P && ws && n_steps >= 0, "gen_run: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  ChainK c;
+  c.pre = P->pre; c.pre_b = P->pre_b; c.sig = P->sig; c.gate = P->gate; c.sig_b = P->sig_b; c.gate_b = P->gate_b;
+  c.res = P->res; c.res_b = P->res_b;
+  c.gc_proj = p->a.n_gc_embed > 0 ? gat<float>(ws, p->oGCP) : nullptr;
+  c.rings = gat<float>(ws, p->oRING); c.zcat = gat<float>(ws, p->oZCAT);
+  c.step = gat<long long>(ws, p->oSTEP); c.code = gat<int>(ws, p->oCODE);
+  c.B = p->B; c.L = p->L; c.nbl = p->nbl; c.Cr = p->Cr; c.Cd = p->Cd; c.Q = p->Q; c.pre_bias = p->pre_bias;
+  RowK sk, p1, p2;
+  sk.in = c.zcat; sk.ldin = (long)p->L * p->Cd; sk.W = P->skip; sk.ldw = p->Cs; sk.out = gat<float>(ws, p->oSKIP);
+  sk.ldout = p->Cs; sk.bias = P->skip_b; sk.bias_rows = p->L; sk.B = p->B; sk.K = p->L * p->Cd; sk.N = p->Cs;
+  sk.relu_in = 0; sk.relu_out = 0;
+  p1.in = sk.out; p1.ldin = p->Cs; p1.W = P->post1; p1.ldw = p->Cp; p1.out = gat<float>(ws, p->oH); p1.ldout = p->Cp;
+  p1.bias = P->post1_b; p1.bias_rows = 1; p1.B = p->B; p1.K = p->Cs; p1.N = p->Cp; p1.relu_in = 1; p1.relu_out = 1;
+  p2.in = p1.out; p2.ldin = p->Cp; p2.W = P->post2; p2.ldw = p->Q; p2.out = gat<float>(ws, p->oLOG); p2.ldout = p->Q;
+  p2.bias = P->post2_b; p2.bias_rows = 1; p2.B = p->B; p2.K = p->Cp; p2.N = p->Q; p2.relu_in = 0; p2.relu_out = 0;
+  SampleK sm;
+  sm.logits = p2.out; sm.Q = p->Q; sm.B = p->B; sm.step = gat<long long>(ws, p->oSTEP); sm.code = c.code;
+  sm.teacher = gat<int>(ws, p->oTEACH); sm.n_teacher = p->n_teacher; sm.samples = gat<int>(ws, p->oSAMP);
+  sm.wav = gat<float>(ws, p->oWAV); sm.max_steps = p->max_steps; sm.seed = p->seed;
+  const int gchain = (p->B + GB - 1) / GB;
+  for (int i = 0; i < n_steps; ++i) {
+    gen_chain_kernel<<<gchain, 1024, 0, st>>>(c);
+    gen_rowvec_kernel<<<(sk.N + 3) / 4, 256, 64 * sk.K, st>>>(sk);
+    gen_rowvec_kernel<<<(p1.N + 3) / 4, 256, 64 * p1.K, st>>>(p1);
+    gen_rowvec_kernel<<<(p2.N + 3) / 4, 256, 64 * p2.K, st>>>(p2);
+    gen_sample_kernel<<<1, 1024, 0, st>>>(sm);
+    LBWN_CHECK_LAUNCH();
+  }
+  return 0;
+}

@@ -28,6 +28,7 @@ struct lbwn_layer_args {
   const float* w_sig; const float* w_gate;  // [2][Cr][Cd]
   const float* b_sig; const float* b_gate;  // [Cd] nullable
   const float* w_res; const float* b_res;   // [Cd][Cr], [Cr] nullable
+  const float* wpack;       // packed LDS image of this layer (lbwn_pack_layers_launch)
   const float* gc_tab;      // [ncat+1][2*Cd] (sig | gate) nullable
   const int* ids;           // [B][T]
   const float* cond; long ldcond;  // [M][2*Cd] nullable (LC projection)
@@ -49,7 +50,11 @@ constexpr int LBWN_LAYER_POS = 128;   // positions per layer-kernel block
 int lbwn_layer_fwd_launch(const lbwn_layer_args& a, hipStream_t st);
 int lbwn_layer_bwd_launch(const lbwn_layer_args& a, hipStream_t st);
 int lbwn_layer_slab_stride();
+int lbwn_layer_image_floats();
 int lbwn_layer_nblocks(int B, int T);
+int lbwn_layer_bwd_grid(int B, int T);   // = number of slab partials per layer
+int lbwn_pack_layers_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
+                            const float* res, const float* res_b, float* out, int L, int Cr, int Cd, hipStream_t st);
 int lbwn_layer_reduce_launch(const lbwn_layer_args& a, hipStream_t st);  // standalone reduction
 
 // D-separation state transfer for ALL layers at once.

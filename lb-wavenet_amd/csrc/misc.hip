@@ -162,29 +162,54 @@ __global__ void stats_reduce_kernel(const float* partial, int nparts, float* sta
 }
 
 // ---- column sums (bias gradients), deterministic two-pass ------------------------------------
+// pass 1: block = CS_ROWS rows × all N columns (float4 groups × row lanes); pass 2: 1024
+// threads per 64 columns sum the chunk partials.  N % 4 == 0, N <= 1024.
 
-constexpr int CS_ROWS = 256;  // rows per partial
-__global__ void colsum_partial_kernel(const float* __restrict__ X, long ldx, int M, int N, float* part) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  const int r0 = blockIdx.y * CS_ROWS;
-  if (n >= N) return;
-  float s = 0.f;
-  const int r1 = min(M, r0 + CS_ROWS);
-  for (int r = r0; r < r1; ++r) s += X[(long)r * ldx + n];
-  part[(long)blockIdx.y * N + n] = s;
+constexpr int CS_ROWS = 64;
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ X, long ldx, int M, int N,
+                                                             float* part) {
+  __shared__ floatx4 red[256];
+  const int ng = N / 4, RL = max(1, 256 / ng);
+  const int t = threadIdx.x, g = t % ng, rl = t / ng;
+  const int r0 = blockIdx.x * CS_ROWS;
+  floatx4 s = {0.f, 0.f, 0.f, 0.f};
+  if (rl < RL && g < ng) {
+    const int r1 = min(M, r0 + CS_ROWS);
+#pragma unroll 8
+    for (int r = r0 + rl; r < r1; r += RL) s += *(const floatx4*)(X + (long)r * ldx + 4 * g);
+  }
+  red[t] = s;
+  __syncthreads();
+  if (t < ng) {
+    floatx4 tot = red[t];
+    for (int k = 1; k < RL; ++k) tot += red[k * ng + t];
+    *(floatx4*)(part + (long)blockIdx.x * N + 4 * t) = tot;
+  }
 }
-__global__ void colsum_final_kernel(const float* part, int nparts, int N, float* out, int accumulate) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
+__global__ __launch_bounds__(1024) void colsum_final_kernel(const float* part, int nparts, int N, float* out,
+                                                            int accumulate) {
+  __shared__ float red[1024];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), lane = threadIdx.x >> 6;  // 16 part lanes
   float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += part[(long)p * N + n];
-  out[n] = accumulate ? out[n] + s : s;
+  if (c < N) {
+#pragma unroll 8
+    for (int p = lane; p < nparts; p += 16) s += part[(long)p * N + c];
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x < 64 && c < N) {
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) tot += red[k * 64 + threadIdx.x];
+    out[c] = accumulate ? out[c] + tot : tot;
+  }
 }
 
 __global__ void sum_bias_kernel(const float* b, int L, int N, float* out) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
   float s = 0.f;
+#pragma unroll 10
   for (int l = 0; l < L; ++l) s += b[(long)l * N + n];
   out[n] = s;
 }
@@ -309,16 +334,16 @@ int lbwn_colsum_ws_floats(int M, int N) { return ((M + CS_ROWS - 1) / CS_ROWS) *
 
 int lbwn_colsum_launch(const float* X, long ldx, int M, int N, float* out, int accumulate, float* ws,
                        hipStream_t st) {
+  LBWN_REQUIRE(N % 4 == 0 && N <= 1024 && ldx % 4 == 0, "colsum: N %% 4 / N <= 1024 / ldx %% 4 required");
   const int np = (M + CS_ROWS - 1) / CS_ROWS;
-  dim3 g1((N + 255) / 256, np);
-  colsum_partial_kernel<<<g1, 256, 0, st>>>(X, ldx, M, N, ws);
-  colsum_final_kernel<<<(N + 255) / 256, 256, 0, st>>>(ws, np, N, out, accumulate);
+  colsum_partial_kernel<<<np, 256, 0, st>>>(X, ldx, M, N, ws);
+  colsum_final_kernel<<<(N + 63) / 64, 1024, 0, st>>>(ws, np, N, out, accumulate);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
 
 int lbwn_sum_bias_launch(const float* b, int L, int N, float* out, hipStream_t st) {
-  sum_bias_kernel<<<(N + 255) / 256, 256, 0, st>>>(b, L, N, out);
+  sum_bias_kernel<<<(N + 63) / 64, 64, 0, st>>>(b, L, N, out);
   LBWN_CHECK_LAUNCH();
   return 0;
 }

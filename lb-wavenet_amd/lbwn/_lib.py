@@ -50,12 +50,20 @@ _SIGS = {
                                     c_fp, c_void_p]),
     'lbwn_adam_tf1': (c_int, [c_fp, c_fp, c_fp, c_fp, c_int64, c_int64, c_float, c_float, c_float, c_float,
                               c_float, c_fp, c_fp, c_void_p]),
+    'lbwn_gen_plan_create': (c_int, [ctypes.POINTER(Arch), c_int, c_int64, c_int64, ctypes.POINTER(c_void_p)]),
+    'lbwn_gen_plan_destroy': (None, [c_void_p]),
+    'lbwn_gen_workspace_bytes': (c_size_t, [c_void_p]),
+    'lbwn_gen_tensor': (c_int, [c_void_p, ctypes.c_char_p, ctypes.POINTER(c_size_t), ctypes.POINTER(c_size_t)]),
+    'lbwn_gen_start': (c_int, [c_void_p, ctypes.POINTER(Params), c_fp, c_fp, c_fp, c_int64, ctypes.c_uint64, c_int,
+                               c_void_p]),
+    'lbwn_gen_run': (c_int, [c_void_p, ctypes.POINTER(Params), c_fp, c_int, c_void_p]),
     'lbwn_mulaw_encode': (c_int, [c_fp, c_fp, c_int64, c_int, c_int, c_void_p]),
     'lbwn_mulaw_decode': (c_int, [c_fp, c_fp, c_int64, c_int, c_void_p]),
     'lbwn_gemm_f32': (c_int, [c_fp, c_int64, c_int, c_fp, c_int64, c_int, c_fp, c_int64, c_int, c_int, c_int,
                               c_fp, c_int, c_int, c_fp, c_int64, c_int, c_int, c_fp, c_void_p]),
+    'lbwn_layer_image_floats_abi': (c_int, []),
     'lbwn_layer_forward': (c_int, [c_fp, c_fp, c_fp, c_int64, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp,
-                                   c_fp, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
+                                   c_fp, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_void_p]),
     'lbwn_dsep_prepend': (c_int, [c_fp, c_int64, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     'lbwn_dsep_save': (c_int, [c_fp, c_int64, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     'lbwn_head_xent': (c_int, [c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_void_p]),

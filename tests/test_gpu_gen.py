@@ -1,0 +1,76 @@
+"""Cached generation (imodel.py) on the GPU vs the oracle's restatement.  Draws use the
+same counter-based uniforms on both sides, so sample sequences must match exactly (a flip
+needs u·Σe to land within fp32 rounding of a CDF boundary: ~1e-6 per draw)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from lbwn.arch import load_arch, normalize_arch
+from lbwn.imodel import WaveNetGen
+from lbwn.tmodel import WaveNetTrain
+from oracle import wavenet_ref as R
+from tests.conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def small(gc=0):
+    return normalize_arch(dict(n_blocks=2, n_block_layers=4, n_quant=256, n_res=32, n_dil=32, n_skip=64,
+                               n_post=32, n_gc_embed=8 if gc else 0, n_gc_category=gc, use_bias=True))
+
+
+def make_gen(arch, B, chunk, seed=7, teacher=None, pre_bias=True, graph=True):
+    tr = WaveNetTrain(**arch, batch_sz=1, l2_factor=0.0, print_interval=0)
+    tr.init_vars(3, bias_scale=0.2)
+    # sharpen the head so draws are not uniform noise
+    with torch.no_grad():
+        tr.vars['POST2'].mul_(4.0)
+    g = WaveNetGen(arch['n_blocks'], arch['n_block_layers'], arch['n_quant'], arch['n_res'], arch['n_dil'],
+                   arch['n_skip'], arch['n_post'], arch['n_gc_embed'], arch['n_gc_category'], arch['use_bias'],
+                   B, chunk, None, seed=seed, pre_bias=pre_bias, graph=graph)
+    g.load_params(tr)
+    P = {n: v.cpu().double().numpy() for n, v in tr.vars.items()}
+    return g, P
+
+
+@pytest.mark.parametrize('pre_bias', [True, False])
+def test_gen_free_running_matches_oracle(pre_bias):
+    arch = small()
+    B, n = 3, 48
+    g, P = make_gen(arch, B, chunk=16, pre_bias=pre_bias)
+    _, wav, _ = g.run(n)
+    torch.cuda.synchronize()
+    s_ref, w_ref = R.generate(arch, P, B, n, seed=7, pre_bias=pre_bias)
+    np.testing.assert_array_equal(g.samples().cpu().numpy()[:, :n], s_ref)
+    np.testing.assert_allclose(wav.cpu().numpy(), w_ref[:, :wav.shape[1]], rtol=1e-6, atol=1e-6)
+
+
+def test_gen_teacher_forced_and_gc():
+    arch = small(gc=5)
+    B, n = 2, 40
+    teacher_q = np.random.default_rng(1).integers(0, 256, 25).astype(np.int32)
+    g, P = make_gen(arch, B, chunk=10)
+    g.teacher_mu = torch.as_tensor(teacher_q, device='cuda')
+    g.build_graph(n)
+    gc = [2, 5]
+    g.run(n, gc_ids=gc)
+    torch.cuda.synchronize()
+    s_ref, _, lg_ref = R.generate(arch, P, B, n, seed=7, teacher_q=teacher_q, gc_ids=gc, return_logits=True)
+    np.testing.assert_array_equal(g.samples().cpu().numpy()[:, :n], s_ref)
+    np.testing.assert_allclose(g.logits().cpu().numpy(), lg_ref[:, -1], rtol=0, atol=2e-4 * np.abs(lg_ref).max())
+
+
+def test_gen_arch3_b10_graph_replay():
+    arch = load_arch(os.path.join(ROOT, 'par', 'arch3.json'))
+    B, n = 10, 300
+    g, P = make_gen(arch, B, chunk=100)
+    n_out, wav, _ = g.run(n)
+    torch.cuda.synchronize()
+    assert wav.shape == (B, 300)
+    s_ref, w_ref = R.generate(arch, P, B, n, seed=7)
+    got = g.samples().cpu().numpy()[:, :n]
+    mism = int((got != s_ref).sum())
+    assert mism == 0, '%d / %d draws differ' % (mism, got.size)
+    assert int(g.tensor('step', torch.int64).item()) == n

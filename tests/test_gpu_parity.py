@@ -119,9 +119,10 @@ def test_layer_forward(lib, d, T, C):
     xin, ws_, wg_, bs_, bg_, wr_, br_ = map(t, (xbuf, Ws, Wg, bs, bg, Wr, br))
     zout = torch.zeros(B * T, C, device=DEV)
     xout = torch.zeros(B, H + T, C, device=DEV)
+    wpk = torch.empty(lib.lbwn_layer_image_floats_abi(), device=DEV)
     _lib.check(lib.lbwn_layer_forward(xin.data_ptr(), xout.data_ptr(), zout.data_ptr(), C, ws_.data_ptr(),
                                       wg_.data_ptr(), bs_.data_ptr(), bg_.data_ptr(), wr_.data_ptr(), br_.data_ptr(),
-                                      None, None, None, 0, B, T, H, d, C, C, None))
+                                      None, None, None, 0, B, T, H, d, C, C, wpk.data_ptr(), None))
     torch.cuda.synchronize()
     np.testing.assert_allclose(zout.cpu().numpy().reshape(B, T, C), z, rtol=0, atol=1e-5)
     np.testing.assert_allclose(xout.cpu().numpy()[:, H:], xo, rtol=0, atol=2e-5)
