@@ -28,6 +28,7 @@ import torch.distributed as dist  # noqa: E402
 from lbwn import _lib  # noqa: E402
 from lbwn.arch import load_arch, mel_hop_sz, n_layers, recep_field_sz  # noqa: E402
 from lbwn.data import SliceDealer, SyntheticSource  # noqa: E402
+from lbwn.imodel import WaveNetGen  # noqa: E402
 from lbwn.optim import AdamOptimizer  # noqa: E402
 from lbwn.tmodel import WaveNetTrain  # noqa: E402
 
@@ -51,6 +52,46 @@ def kernel_work(name, arch, M):
         # re-read is served from LDS/L2 and counted once.
         return 'hbm', 4.0 * M * (2 * Cr + Cd)
     raise KeyError(name)
+
+
+def gen_bytes_per_step(arch, B):
+    """every weight read once per step (PRE table excluded: one row per stream)
+    + per stream 50 lookback reads/writes of n_res floats + PRE row, skip/head vectors."""
+    from lbwn.arch import ParamLayout
+    lay = ParamLayout(arch)
+    w = sum(e.numel for n, e in lay.entries.items() if n != 'PRE') * 4
+    L, Cr = n_layers(arch), arch['n_res']
+    per_stream = L * 2 * 4 * Cr + 4 * Cr + 4 * (arch['n_skip'] + arch['n_post'] + arch['n_quant']) + 4 * L * arch['n_dil']
+    return w + B * per_stream
+
+
+def bench_gen(net, arch, B=10, seconds=3.0, sr=16000, chunk=1000):
+    """imodel.py cached generation, arch3, B=10, 3 s @ 16 kHz (BASELINE configs[2]), graph
+    replay of chunk-sized step sequences; weights = the benchmark net's."""
+    g = WaveNetGen(arch['n_blocks'], arch['n_block_layers'], arch['n_quant'], arch['n_res'], arch['n_dil'],
+                   arch['n_skip'], arch['n_post'], arch['n_gc_embed'], arch['n_gc_category'], arch['use_bias'],
+                   B, chunk, None, seed=1, graph=True)
+    g.load_params(net)
+    n = int(seconds * sr)
+    g.build_graph(n)
+    gc = list(range(1, B + 1)) if arch['n_gc_embed'] else None
+    g.init_buffers(gc)
+    g.step(chunk)   # capture + warm
+    torch.cuda.synchronize()
+    g.init_buffers(gc)
+    t0 = time.perf_counter()
+    g.step(n)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    bps = gen_bytes_per_step(arch, B)
+    return {'metric': 'cached autoregressive gen audio samples/s (B streams x steps / wall)',
+            'value': B * n / dt, 'unit': 'audio samples/s', 'steps': n, 'batch': B, 'wall_s': dt,
+            'us_per_step': dt / n * 1e6, 'config': 'imodel.py cached gen, par/arch3.json, B=%d, %.0f s @ %d Hz, '
+                                                   'chunk %d, hipGraph replay' % (B, seconds, sr, chunk),
+            'roofline': {'bound': 'hbm', 'bytes_per_step': bps, 'achieved': bps * n / dt / 1e9, 'peak': HBM_PEAK / 1e9,
+                         'unit': 'GB/s', 'frac': bps * n / dt / HBM_PEAK,
+                         'note': 'weights are L2/MALL-resident across steps; the step is a 55-stage dependent '
+                                 'chain, latency- not bandwidth-bound'}}
 
 
 def cpu_baseline(arch, seconds):
@@ -100,6 +141,8 @@ def main():
     ap.add_argument('--cpu-seconds', type=float, default=15.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--gc', type=int, default=None, help='--num-global-cond for GC archs')
+    ap.add_argument('--no-gen', action='store_true')
+    ap.add_argument('--gen-seconds', type=float, default=3.0)
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -209,6 +252,8 @@ def main():
         'roofline_dilconv': roof('layer_fwd', samples['layer_fwd']),
         'warmup_probe_ms': warm_t,
     }
+    if world == 1 and not args.no_gen and arch['n_lc_out'] == 0:
+        out['gen'] = bench_gen(net, arch, B=10, seconds=args.gen_seconds)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(arch, args.cpu_seconds)
     if rank == 0:

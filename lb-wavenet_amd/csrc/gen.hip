@@ -22,6 +22,7 @@
 namespace {
 
 constexpr int GB = 16;                 // streams per chain workgroup
+constexpr int RV_MAXI = 32;            // row-vector GEMM: K <= 64·32 = 2048
 constexpr int WIMG_G = 64 * 64 + 32 * 32 + 96;  // conv W[k][o] (64×64) | RES[c][o] (32×32) | b_conv[64] | b_res[32]
 
 struct ChainK {
@@ -78,22 +79,47 @@ struct WStage {
   }
 };
 
+// LDS: all L layers' lookback taps (read once, up front), 2 weight images, x/z rows,
+// conv partials over 2 K-halves.  GBS streams per workgroup (16, or 8 for deep stacks).
+template <int GBS>
 __global__ __launch_bounds__(1024) void gen_chain_kernel(ChainK a) {
-  __shared__ __attribute__((aligned(16))) float Wb[2][WIMG_G];
-  __shared__ float X[GB][32];       // current layer input
-  __shared__ float PV[2][GB][32];   // prefetched prev tap (double buffer over layers)
-  __shared__ float Z[GB][32];
-  __shared__ float P[4][GB][64];    // conv partials over 4 K-quarters
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* Wb0 = sm;
+  float* Wb1 = sm + WIMG_G;
+  float* X = Wb1 + WIMG_G;          // [GBS][32]
+  float* Z = X + GBS * 32;          // [GBS][32]
+  float* P = Z + GBS * 32;          // [2][GBS][64]
+  float* PV = P + 2 * GBS * 64;     // [L][GBS][32]
   const int tid = threadIdx.x;
-  const int b0 = blockIdx.x * GB;
-  const int nb = min(GB, a.B - b0);
+  const int b0 = blockIdx.x * GBS;
+  const int nb = min(GBS, a.B - b0);
   const long t = *a.step;
-  const int Cr = a.Cr, Cd = a.Cd;
+  const int Cr = a.Cr, Cd = a.Cd, L = a.L;
 
   WStage ws;
   ws.load(a, 0, tid);
+  // every layer's prev tap: input of layer l at t - d_l (ring slot t mod d_l, zero-initialised)
+  {
+    const int n = L * GBS * 32;
+    for (int base = tid; base < n; base += 1024 * 8) {
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int e = base + 1024 * i;
+        v[i] = 0.f;
+        if (e < n) {
+          const int l = e / (GBS * 32), r = e % (GBS * 32), b = r >> 5, c = r & 31;
+          const int d = 1 << (l % a.nbl);
+          if (b < nb && c < Cr) v[i] = a.rings[ring_offset(l, a.nbl, a.B, Cr) + ((long)(b0 + b) * d + (t % d)) * Cr + c];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (base + 1024 * i < n) PV[base + 1024 * i] = v[i];
+    }
+  }
   // input z0 = onehot(code)·PRE (+ PRE_BIAS): zero vector at step 0 (imodel.py:61-79)
-  if (tid < GB * 32) {
+  if (tid < GBS * 32) {
     const int b = tid >> 5, c = tid & 31;
     float v = 0.f;
     if (b < nb && c < Cr) {
@@ -101,89 +127,78 @@ __global__ __launch_bounds__(1024) void gen_chain_kernel(ChainK a) {
       if (code >= 0) v = a.pre[(long)code * Cr + c];
       if (a.pre_bias && a.pre_b) v += a.pre_b[c];
     }
-    X[b][c] = v;
+    X[tid] = v;
   }
-  // prev tap of layer 0: input of layer 0 at t - d (ring slot t mod d, zero-initialised)
-  auto load_prev = [&](int l, int buf) {
-    if (tid < GB * 32) {
-      const int b = tid >> 5, c = tid & 31;
-      const int d = 1 << (l % a.nbl);
-      float v = 0.f;
-      if (b < nb && c < Cr) v = a.rings[ring_offset(l, a.nbl, a.B, Cr) + ((long)(b0 + b) * d + (t % d)) * Cr + c];
-      PV[buf][b][c] = v;
-    }
-  };
-  load_prev(0, 0);
-  ws.store(Wb[0], tid);
+  ws.store(Wb0, tid);
   __syncthreads();
 
-  for (int l = 0; l < a.L; ++l) {
-    const int cur = l & 1;
-    const float* W = Wb[cur];
-    if (l + 1 < a.L) ws.load(a, l + 1, tid);   // prefetch next layer's weights (lands during compute)
-    // ring write: this layer's input at slot t mod d (the prev tap was read before)
-    if (tid < GB * 32) {
+  constexpr int SPG = GBS / 8;   // streams per conv thread
+  for (int l = 0; l < L; ++l) {
+    const float* W = (l & 1) ? Wb1 : Wb0;
+    float* Wn = (l & 1) ? Wb0 : Wb1;
+    const float* pv = PV + l * GBS * 32;
+    if (l + 1 < L) ws.load(a, l + 1, tid);   // next layer's weights land during this layer
+    // ring write: this layer's input becomes the tap of step t + d (slot t mod d)
+    if (tid < GBS * 32) {
       const int b = tid >> 5, c = tid & 31;
       const int d = 1 << (l % a.nbl);
       if (b < nb && c < Cr)
-        a.rings[ring_offset(l, a.nbl, a.B, Cr) + ((long)(b0 + b) * d + (t % d)) * Cr + c] = X[b][c];
+        a.rings[ring_offset(l, a.nbl, a.B, Cr) + ((long)(b0 + b) * d + (t % d)) * Cr + c] = X[tid];
     }
-    // conv partials: thread (o, kq, bq): 4 streams × 16 k
+    // conv partials: thread (o, K-half kh, stream group bg): SPG streams × 32 k
     {
-      const int o = tid & 63, kq = (tid >> 6) & 3, bq = tid >> 8;
-      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      const int o = tid & 63, kh = (tid >> 6) & 1, bg = tid >> 7;
+      const float* xin = kh ? X : pv;
+      float acc[SPG];
 #pragma unroll
-      for (int kk = 0; kk < 16; ++kk) {
-        const int k = kq * 16 + kk;
-        const float w = W[k * 64 + o];
+      for (int j = 0; j < SPG; ++j) acc[j] = 0.f;
+#pragma unroll 8
+      for (int k = 0; k < 32; ++k) {
+        const float w = W[(kh * 32 + k) * 64 + o];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int b = bq * 4 + j;
-          const float xv = k < 32 ? PV[cur][b][k] : X[b][k - 32];
-          acc[j] = fmaf(xv, w, acc[j]);
-        }
+        for (int j = 0; j < SPG; ++j) acc[j] = fmaf(xin[(bg * SPG + j) * 32 + k], w, acc[j]);
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) P[kq][bq * 4 + j][o] = acc[j];
+      for (int j = 0; j < SPG; ++j) P[(kh * GBS + bg * SPG + j) * 64 + o] = acc[j];
     }
-    if (l + 1 < a.L) load_prev(l + 1, cur ^ 1);
     __syncthreads();
     // gate
-    if (tid < GB * 32) {
+    if (tid < GBS * 32) {
       const int b = tid >> 5, c = tid & 31;
       const float* bs = W + 64 * 64 + 32 * 32;
-      float vs = bs[c], vg = bs[32 + c];
-#pragma unroll
-      for (int kq = 0; kq < 4; ++kq) { vs += P[kq][b][c]; vg += P[kq][b][32 + c]; }
+      float vs = bs[c] + P[b * 64 + c] + P[(GBS + b) * 64 + c];
+      float vg = bs[32 + c] + P[b * 64 + 32 + c] + P[(GBS + b) * 64 + 32 + c];
       if (a.gc_proj && b < nb) {
         const float* g = a.gc_proj + ((long)l * a.B + b0 + b) * 64;
         vs += g[c];
         vg += g[32 + c];
       }
       const float z = (c < Cd && b < nb) ? tanhf_(vs) * sigmoidf_(vg) : 0.f;
-      Z[b][c] = z;
-      if (b < nb && c < Cd) a.zcat[(long)(b0 + b) * a.L * Cd + l * Cd + c] = z;
+      Z[tid] = z;
+      if (b < nb && c < Cd) a.zcat[(long)(b0 + b) * L * Cd + l * Cd + c] = z;
     }
     __syncthreads();
-    // residual: x += z·RES + b   (thread (o, b) for 512 outputs; K = 32)
-    if (tid < GB * 32) {
+    // residual: x += z·RES + b
+    if (tid < GBS * 32) {
       const int b = tid >> 5, o = tid & 31;
       const float* R = W + 64 * 64;
       float r = W[64 * 64 + 32 * 32 + 64 + o];   // b_res
 #pragma unroll 8
-      for (int c = 0; c < 32; ++c) r = fmaf(Z[b][c], R[c * 32 + o], r);
-      X[b][o] += r;
+      for (int c = 0; c < 32; ++c) r = fmaf(Z[b * 32 + c], R[c * 32 + o], r);
+      X[tid] += r;
     }
-    if (l + 1 < a.L) ws.store(Wb[cur ^ 1], tid);
+    if (l + 1 < L) ws.store(Wn, tid);
     __syncthreads();
   }
 }
+
+size_t chain_lds_bytes(int gbs, int L) { return 4 * (size_t)(2 * WIMG_G + 2 * gbs * 32 + 2 * gbs * 64 + (size_t)L * gbs * 32); }
 
 // out[b][n] = epi( Σ_k act(in[b][k])·W[k][n] + bias ), b < B (≤ 64 per launch row loop),
 // block = 4 columns; thread (c = tid & 3, ks = tid >> 2): K slice, all streams.
 struct RowK {
   const float* in; long ldin; const float* W; long ldw; float* out; long ldout;
-  const float* bias; int bias_rows;   // bias = Σ_{r<bias_rows} bias[r*N + n]
+  const float* bias;                  // [N] nullable
   int B, K, N, relu_in, relu_out;
 };
 
@@ -193,25 +208,51 @@ __global__ __launch_bounds__(256) void gen_rowvec_kernel(RowK a) {
   const int c = threadIdx.x & 3, ks = threadIdx.x >> 2;  // 64 K slices
   const int n = blockIdx.x * 4 + c;
   float acc[16];
+  // every weight of this thread's K slice is issued first (K <= 64·RV_MAXI); it lands while
+  // the activations are staged
+  float wr[RV_MAXI];
+#pragma unroll
+  for (int i = 0; i < RV_MAXI; ++i) {
+    const int k = ks + 64 * i;
+    wr[i] = (n < a.N && k < a.K) ? a.W[(long)k * a.ldw + n] : 0.f;
+  }
   for (int bb0 = 0; bb0 < a.B; bb0 += 16) {
     const int nbb = min(16, a.B - bb0);
-    for (int e = threadIdx.x; e < 16 * a.K; e += 256) {
-      const int j = e / a.K, k = e % a.K;
-      float x = 0.f;
-      if (j < nbb) {
-        x = a.in[(long)(bb0 + j) * a.ldin + k];
-        if (a.relu_in) x = fmaxf(x, 0.f);
+    {
+      const int nf4 = 16 * a.K / 4;   // K % 4 == 0, ldin % 4 == 0
+      for (int base = threadIdx.x; base < nf4; base += 256 * 8) {
+        floatx4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int e = base + 256 * i;
+          v[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+          if (e < nf4) {
+            const int j = (4 * e) / a.K, k = (4 * e) % a.K;
+            if (j < nbb) {
+              v[i] = *(const floatx4*)(a.in + (long)(bb0 + j) * a.ldin + k);
+              if (a.relu_in) {
+                v[i][0] = fmaxf(v[i][0], 0.f); v[i][1] = fmaxf(v[i][1], 0.f);
+                v[i][2] = fmaxf(v[i][2], 0.f); v[i][3] = fmaxf(v[i][3], 0.f);
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (base + 256 * i < nf4) *(floatx4*)(xin + 4 * (base + 256 * i)) = v[i];
       }
-      xin[e] = x;
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = 0.f;
     if (n < a.N) {
-      for (int k = ks; k < a.K; k += 64) {
-        const float w = a.W[(long)k * a.ldw + n];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) acc[j] = fmaf(xin[j * a.K + k], w, acc[j]);
+      for (int i = 0; i < RV_MAXI; ++i) {
+        const int k = ks + 64 * i;
+        if (k < a.K) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) acc[j] = fmaf(xin[j * a.K + k], wr[i], acc[j]);
+        }
       }
     }
 #pragma unroll
@@ -221,10 +262,8 @@ __global__ __launch_bounds__(256) void gen_rowvec_kernel(RowK a) {
       const int cc = threadIdx.x & 3, j = threadIdx.x >> 2;
       const int nn = blockIdx.x * 4 + cc;
       if (nn < a.N && j < nbb) {
-        float s = 0.f;
+        float s = a.bias ? a.bias[nn] : 0.f;
         for (int q = 0; q < 64; ++q) s += red[q][cc][j];
-        if (a.bias)
-          for (int r = 0; r < a.bias_rows; ++r) s += a.bias[(long)r * a.N + nn];
         if (a.relu_out) s = fmaxf(s, 0.f);
         a.out[(long)(bb0 + j) * a.ldout + nn] = s;
       }
@@ -337,7 +376,7 @@ struct lbwn_gen_plan {
   lbwn_arch a;
   int B, L, nbl, Cr, Cd, Cs, Cp, Q;
   long long max_steps;
-  size_t oRING, oZCAT, oSKIP, oH, oLOG, oSTEP, oCODE, oTEACH, oSAMP, oWAV, oGCP, total;
+  size_t oRING, oZCAT, oSKIP, oH, oLOG, oSTEP, oCODE, oTEACH, oSAMP, oWAV, oGCP, oBSUM, total;
   long n_ring;
   long long n_teacher, max_teacher;
   unsigned long long seed;
@@ -354,7 +393,9 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
                                     lbwn_gen_plan** out) {
   LBWN_REQUIRE(a && out && B >= 1 && max_steps >= 1 && max_teacher >= 0, "gen_plan_create: bad arguments");
   LBWN_REQUIRE(a->n_res <= 32 && a->n_dil <= 32, "gen: n_res/n_dil must be <= 32");
-  LBWN_REQUIRE((long)a->n_blocks * a->n_block_layers * a->n_dil <= 2000 && a->n_skip <= 2000 && a->n_post <= 2000,
+  LBWN_REQUIRE(a->n_skip % 4 == 0 && a->n_post % 4 == 0 && ((long)a->n_blocks * a->n_block_layers * a->n_dil) % 4 == 0,
+               "gen: row-vector GEMM needs K %% 4 == 0");
+  LBWN_REQUIRE((long)a->n_blocks * a->n_block_layers * a->n_dil <= 2048 && a->n_skip <= 2048 && a->n_post <= 2048,
                "gen: row-vector GEMM K too large for LDS staging");
   LBWN_REQUIRE(a->n_lc_out == 0, "gen: local conditioning is not supported by the cached generator "
                                  "(imodel.py has no LC path)");
@@ -380,6 +421,7 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
   p->oSAMP = gcarve(cur, 4 * (size_t)B * max_steps);
   p->oWAV = gcarve(cur, 4 * (size_t)B * max_steps);
   p->oGCP = gcarve(cur, 4 * (size_t)p->L * B * 64);
+  p->oBSUM = gcarve(cur, 4 * (size_t)p->Cs);
   p->total = cur;
   *out = p;
   return 0;
@@ -424,6 +466,9 @@ extern "C" int lbwn_gen_start(lbwn_gen_plan* p, const lbwn_params* P, void* ws, 
                                   st);
     LBWN_REQUIRE(e == hipSuccess, "gen_start: teacher copy failed: %s", hipGetErrorString(e));
   }
+  if (P->skip_b) {
+    if (int e = lbwn_sum_bias_launch(P->skip_b, p->L, p->Cs, gat<float>(ws, p->oBSUM), st)) return e;
+  }
   if (p->a.n_gc_embed > 0) {
     gen_gc_proj_kernel<<<p->L, 256, 0, st>>>(P->gc_embed, P->gc_sig, P->gc_gate, gc_ids, gat<float>(ws, p->oGCP),
                                              p->B, p->a.n_gc_embed, p->Cd);
@@ -444,19 +489,24 @@ extern "C" int lbwn_gen_run(lbwn_gen_plan* p, const lbwn_params* P, void* ws, in
   c.B = p->B; c.L = p->L; c.nbl = p->nbl; c.Cr = p->Cr; c.Cd = p->Cd; c.Q = p->Q; c.pre_bias = p->pre_bias;
   RowK sk, p1, p2;
   sk.in = c.zcat; sk.ldin = (long)p->L * p->Cd; sk.W = P->skip; sk.ldw = p->Cs; sk.out = gat<float>(ws, p->oSKIP);
-  sk.ldout = p->Cs; sk.bias = P->skip_b; sk.bias_rows = p->L; sk.B = p->B; sk.K = p->L * p->Cd; sk.N = p->Cs;
+  sk.ldout = p->Cs; sk.bias = P->skip_b ? gat<float>(ws, p->oBSUM) : nullptr; sk.B = p->B; sk.K = p->L * p->Cd; sk.N = p->Cs;
   sk.relu_in = 0; sk.relu_out = 0;
   p1.in = sk.out; p1.ldin = p->Cs; p1.W = P->post1; p1.ldw = p->Cp; p1.out = gat<float>(ws, p->oH); p1.ldout = p->Cp;
-  p1.bias = P->post1_b; p1.bias_rows = 1; p1.B = p->B; p1.K = p->Cs; p1.N = p->Cp; p1.relu_in = 1; p1.relu_out = 1;
+  p1.bias = P->post1_b; p1.B = p->B; p1.K = p->Cs; p1.N = p->Cp; p1.relu_in = 1; p1.relu_out = 1;
   p2.in = p1.out; p2.ldin = p->Cp; p2.W = P->post2; p2.ldw = p->Q; p2.out = gat<float>(ws, p->oLOG); p2.ldout = p->Q;
-  p2.bias = P->post2_b; p2.bias_rows = 1; p2.B = p->B; p2.K = p->Cp; p2.N = p->Q; p2.relu_in = 0; p2.relu_out = 0;
+  p2.bias = P->post2_b; p2.B = p->B; p2.K = p->Cp; p2.N = p->Q; p2.relu_in = 0; p2.relu_out = 0;
   SampleK sm;
   sm.logits = p2.out; sm.Q = p->Q; sm.B = p->B; sm.step = gat<long long>(ws, p->oSTEP); sm.code = c.code;
   sm.teacher = gat<int>(ws, p->oTEACH); sm.n_teacher = p->n_teacher; sm.samples = gat<int>(ws, p->oSAMP);
   sm.wav = gat<float>(ws, p->oWAV); sm.max_steps = p->max_steps; sm.seed = p->seed;
-  const int gchain = (p->B + GB - 1) / GB;
+  const bool wide = chain_lds_bytes(16, p->L) <= 160 * 1024;
+  const int gbs = wide ? 16 : 8;
+  LBWN_REQUIRE(chain_lds_bytes(gbs, p->L) <= 160 * 1024, "gen: too many layers for the LDS tap cache");
+  const int gchain = (p->B + gbs - 1) / gbs;
+  const size_t lds = chain_lds_bytes(gbs, p->L);
   for (int i = 0; i < n_steps; ++i) {
-    gen_chain_kernel<<<gchain, 1024, 0, st>>>(c);
+    if (wide) gen_chain_kernel<16><<<gchain, 1024, lds, st>>>(c);
+    else gen_chain_kernel<8><<<gchain, 1024, lds, st>>>(c);
     gen_rowvec_kernel<<<(sk.N + 3) / 4, 256, 64 * sk.K, st>>>(sk);
     gen_rowvec_kernel<<<(p1.N + 3) / 4, 256, 64 * p1.K, st>>>(p1);
     gen_rowvec_kernel<<<(p2.N + 3) / 4, 256, 64 * p2.K, st>>>(p2);

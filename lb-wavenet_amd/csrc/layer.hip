@@ -24,6 +24,10 @@ constexpr int DS = 68;              // dv tile row [pos][64]
 constexpr int WIMG = 64 * WS + 32 * XS + 96;  // packed per-layer image (floats), multiple of 4
 constexpr int SLAB = 2048 + 2048 + 1024 + 96;
 constexpr int RED_PARTS = 32;       // deferred reduction: parts prefetched per thread (8 lanes × 32)
+// Timing-only ablation switches (tools/ablate.sh); 0 in every real build.
+#ifndef LBWN_ABL
+#define LBWN_ABL 0
+#endif
 
 // Compact kernel arguments (the full lbwn_layer_args by value spilled ~100 SGPRs).
 struct FwdK {
@@ -174,15 +178,28 @@ LBWN_DEV void conv_tile(const float* Xp, const float* Xc, const float* Ws, const
   }
   const float* xp = Xp + (32 * w + pi) * XS;
   const float* xc = Xc + (32 * w + pi) * XS;
-#pragma unroll
-  for (int g = 0; g < 8; ++g) {
+  // operands of group g (8 k values: k = 8g+4h+j) are fetched while group g-1's MFMAs issue
+  floatx4 bx[2];
+  float ws_[2][4], wg_[2][4];
+  auto load = [&](int g, int buf) {
     const float* src = g < 4 ? xp : xc;
-    const floatx4 bx = *(const floatx4*)(src + 8 * (g & 3) + 4 * h);
+    bx[buf] = *(const floatx4*)(src + 8 * (g & 3) + 4 * h);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int k = 8 * g + 4 * h + j;
-      acc_s = mfma32(Ws[k * WS + pi], bx[j], acc_s);
-      acc_g = mfma32(Ws[k * WS + 32 + pi], bx[j], acc_g);
+      ws_[buf][j] = Ws[k * WS + pi];
+      wg_[buf][j] = Ws[k * WS + 32 + pi];
+    }
+  };
+  load(0, 0);
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    const int cb = g & 1;
+    if (g + 1 < 8) load(g + 1, cb ^ 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc_s = mfma32(ws_[cb][j], bx[cb][j], acc_s);
+      acc_g = mfma32(wg_[cb][j], bx[cb][j], acc_g);
     }
   }
 }
@@ -224,7 +241,12 @@ __global__ __launch_bounds__(256) void layer_fwd_kernel(FwdK a) {
     const bool valid = t < a.T;
     const long m = (long)b * a.T + t;
     floatx16 acc_s, acc_g;
-    conv_tile(Xp, Xc, Ws, bs, a, m, valid, w, lane, acc_s, acc_g);
+    if (LBWN_ABL & 32) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { acc_s[r] = Xc[r * 8 + lane]; acc_g[r] = Xp[r * 8 + lane]; }
+    } else {
+      conv_tile(Xp, Xc, Ws, bs, a, m, valid, w, lane, acc_s, acc_g);
+    }
     floatx16 z;
 #pragma unroll
     for (int r = 0; r < 16; ++r) z[r] = tanhf_(acc_s[r]) * sigmoidf_(acc_g[r]);
@@ -238,11 +260,16 @@ __global__ __launch_bounds__(256) void layer_fwd_kernel(FwdK a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc_r[4 * q + j] = xv[j] + bv[j];
       }
+      float ra[16];
 #pragma unroll
-      for (int s = 0; s < 16; ++s) acc_r = mfma32(Rs[acc_row(s, h) * XS + pi], z[s], acc_r);
-      if (valid) store_rows16(a.x_out + ((long)b * (a.H + a.T) + a.H + t) * a.Cr, acc_r, a.Cr, h);
+      for (int s = 0; s < 16; ++s) ra[s] = Rs[acc_row(s, h) * XS + pi];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) acc_r = mfma32(ra[s], z[s], acc_r);
+      if (valid && !(LBWN_ABL & 64)) store_rows16(a.x_out + ((long)b * (a.H + a.T) + a.H + t) * a.Cr, acc_r, a.Cr, h);
+      if (LBWN_ABL & 64) asm volatile("" ::"v"(acc_r[0]), "v"(acc_r[15]));
     }
-    if (valid) store_rows16(a.z + m * a.ldz, z, a.Cd, h);
+    if (valid && !(LBWN_ABL & 64)) store_rows16(a.z + m * a.ldz, z, a.Cd, h);
+    if (LBWN_ABL & 64) asm volatile("" ::"v"(z[0]), "v"(z[15]));
   }
 }
 
@@ -317,7 +344,7 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(BwdK a) {
 
   // deferred reduction of the deeper layer's partials: issue the loads now, sum at the end
   float pre[RED_PARTS];
-  const bool red = a.red_slab && (int)blockIdx.x < ngroups;
+  const bool red = !(LBWN_ABL & 1) && a.red_slab && (int)blockIdx.x < ngroups;
   if (red) slab_group_prefetch(a, blockIdx.x, pre, tid);
 
   stage_image(Ws, a.wpack, tid);
@@ -358,7 +385,12 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(BwdK a) {
 
     // 1. recompute the gate
     floatx16 acc_s, acc_g;
-    conv_tile(Xp, Xc, Ws, bs, a, m, valid, w, lane, acc_s, acc_g);
+    if (LBWN_ABL & 4) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { acc_s[r] = Xc[r]; acc_g[r] = Xp[r]; }
+    } else {
+      conv_tile(Xp, Xc, Ws, bs, a, m, valid, w, lane, acc_s, acc_g);
+    }
     floatx16 th, sg;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -367,12 +399,17 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(BwdK a) {
     }
     // 2. dzᵀ += RES·gᵀ   (dz[pos][c] = dZ[pos][c] + Σ_o g[pos][o]·RES[c][o])
     const float* gp = G + (32 * w + pi) * XS;
+    {
+      floatx4 gx[4], rx[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const floatx4 gx = *(const floatx4*)(gp + 8 * g + 4 * h);
-      const floatx4 rx = *(const floatx4*)(Rs + pi * XS + 8 * g + 4 * h);
+      for (int g = 0; g < 4; ++g) {
+        gx[g] = *(const floatx4*)(gp + 8 * g + 4 * h);
+        rx[g] = *(const floatx4*)(Rs + pi * XS + 8 * g + 4 * h);
+      }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) dz = mfma32(rx[j], gx[j], dz);
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dz = mfma32(rx[g][j], gx[g][j], dz);
     }
     // 3. dvᵀ, parked position-major with z for the weight-grad products
     floatx16 dvs, dvg, z;
@@ -398,43 +435,70 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(BwdK a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) { acc_a[4 * q + j] = gv[j]; acc_c[4 * q + j] = 0.f; }
     }
+    {
+      floatx4 wv[2][4];  // [buf][w0s, w0g, w1s, w1g]
+      auto loadw = [&](int q, int buf) {
+        const int ko = 8 * q + 4 * h;
+        wv[buf][0] = *(const floatx4*)(Ws + pi * WS + ko);
+        wv[buf][1] = *(const floatx4*)(Ws + pi * WS + 32 + ko);
+        wv[buf][2] = *(const floatx4*)(Ws + (32 + pi) * WS + ko);
+        wv[buf][3] = *(const floatx4*)(Ws + (32 + pi) * WS + 32 + ko);
+      };
+      loadw(0, 0);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int ko = 8 * q + 4 * h;
-      const floatx4 w0s = *(const floatx4*)(Ws + pi * WS + ko);
-      const floatx4 w0g = *(const floatx4*)(Ws + pi * WS + 32 + ko);
-      const floatx4 w1s = *(const floatx4*)(Ws + (32 + pi) * WS + ko);
-      const floatx4 w1g = *(const floatx4*)(Ws + (32 + pi) * WS + 32 + ko);
+      for (int q = 0; q < ((LBWN_ABL & 8) ? 0 : 4); ++q) {
+        const int cb = q & 1;
+        if (q + 1 < 4) loadw(q + 1, cb ^ 1);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int s = 4 * q + j;
-        acc_a = mfma32(w1s[j], dvs[s], acc_a);
-        acc_c = mfma32(w0s[j], dvs[s], acc_c);
-        acc_a = mfma32(w1g[j], dvg[s], acc_a);
-        acc_c = mfma32(w0g[j], dvg[s], acc_c);
+        for (int j = 0; j < 4; ++j) {
+          const int s2 = 4 * q + j;
+          acc_a = mfma32(wv[cb][2][j], dvs[s2], acc_a);
+          acc_c = mfma32(wv[cb][0][j], dvs[s2], acc_c);
+          acc_a = mfma32(wv[cb][3][j], dvg[s2], acc_a);
+          acc_c = mfma32(wv[cb][1][j], dvg[s2], acc_c);
+        }
       }
     }
-    if (valid) {
+    if (valid && !(LBWN_ABL & 16)) {
       store_rows16(a.out_a + m * a.Cr, acc_a, a.Cr, h);
       store_rows16(a.out_c0 + m * a.Cr, acc_c, a.Cr, h);
     }
+    if (LBWN_ABL & 16) asm volatile("" ::"v"(acc_a[0]), "v"(acc_c[0]), "v"(acc_a[15]), "v"(acc_c[15]));
     __syncthreads();  // DV / ZT of every wave visible
 
     // 5. dSIG/dGATE tile w over all LP positions: A[i=in][k=pos] = X[pos][in], B[k][j=o] = DV[pos][o]
     {
       const float* X = (w & 1) ? Xc : Xp;
       const int oc = (w >> 1) * 32 + pi;
-#pragma unroll 8
-      for (int s = 0; s < LP / 2; ++s) {
-        const int p = 2 * s + h;
-        accW = mfma32(X[p * XS + pi], DV[p * DS + oc], accW);
+      float xa[2][8], da[2][8];
+      auto loadb = [&](int bt, int buf) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int p = 2 * (8 * bt + i) + h;
+          xa[buf][i] = X[p * XS + pi];
+          da[buf][i] = DV[p * DS + oc];
+        }
+      };
+      loadb(0, 0);
+#pragma unroll
+      for (int bt = 0; bt < ((LBWN_ABL & 2) ? 0 : LP / 16); ++bt) {
+        const int cb = bt & 1;
+        if (bt + 1 < LP / 16) loadb(bt + 1, cb ^ 1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) accW = mfma32(xa[cb][i], da[cb][i], accW);
       }
     }
     // 6. dRES part over this wave's 32 positions: A[i=c][k=pos] = z[pos][c], B[k][j=o] = g[pos][o]
+    {
+      float za[16], ga[16];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int p = 32 * w + 2 * s + h;
-      accR = mfma32(ZT[p * XS + pi], G[p * XS + pi], accR);
+      for (int s2 = 0; s2 < 16; ++s2) {
+        const int p = 32 * w + 2 * s2 + h;
+        za[s2] = ZT[p * XS + pi];
+        ga[s2] = G[p * XS + pi];
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) accR = mfma32(za[s2], ga[s2], accR);
     }
     // bias partials: column sums of DV (64) and G (32) over the tile, 8 position chunks
     {
@@ -503,7 +567,7 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(BwdK a) {
   if (tid < 96) slab[5120 + tid] = bsum;
   // 9. finish the deferred reduction (remaining groups when the grid is small)
   if (red) slab_group_finish(a, blockIdx.x, pre, RED, tid);
-  if (a.red_slab) {
+  if (!(LBWN_ABL & 1) && a.red_slab) {
     float none[RED_PARTS];
     for (int grp = blockIdx.x + gridDim.x; grp < ngroups; grp += gridDim.x) {
       slab_group_prefetch(a, grp, none, tid);
