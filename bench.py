@@ -41,16 +41,17 @@ def kernel_work(name, arch, M):
     L, Cr, Cd, Cs, Cp, Q = (n_layers(arch), arch['n_res'], arch['n_dil'], arch['n_skip'], arch['n_post'],
                             arch['n_quant'])
     flops = {
-        'skip_fwd': 2.0 * M * L * Cd * Cs, 'dskip': 2.0 * M * L * Cd * Cs, 'dz': 2.0 * M * L * Cd * Cs,
-        'post1_fwd': 2.0 * M * Cs * Cp, 'dpost1': 2.0 * M * Cs * Cp,
-        'post2_fwd': 2.0 * M * Cp * Q, 'dpost2': 2.0 * M * Cp * Q,
+        'dskip': 2.0 * M * L * Cd * Cs,
+        'post1_fwd': 2.0 * M * Cs * Cp, 'dpost1': 2.0 * M * Cs * Cp, 'ds': 2.0 * M * Cs * Cp,
+        'post2_fwd': 2.0 * M * Cp * Q, 'dpost2': 2.0 * M * Cp * Q, 'dh': 2.0 * M * Cp * Q,
     }
     if name in flops:
         return 'mfma', flops[name]
-    if name.startswith('layer_fwd'):
-        # x_l in (Cr), x_{l+1} out (Cr), z out (Cd) per position; the dilated tap x[t-d]
-        # re-read is served from LDS/L2 and counted once.
-        return 'hbm', 4.0 * M * (2 * Cr + Cd)
+    if name == 'layer_fwd':
+        # the whole residual stack (persistent chain launch, or the span of the L per-layer
+        # launches): per layer and position x_l in (Cr), x_{l+1} out (Cr), z out (Cd); the
+        # dilated tap x[t-d] is re-read from LDS / the neighbour tile and counted once.
+        return 'hbm', 4.0 * M * (2 * Cr + Cd) * L
     raise KeyError(name)
 
 
@@ -191,7 +192,8 @@ def main():
         return s, e
 
     M = B * T
-    cands = ['skip_fwd', 'dskip', 'dz', 'post1_fwd', 'dpost1', 'post2_fwd', 'dpost2']
+    # single-launch GEMMs (the skip GEMM / dZ run as per-block chunks overlapping the layer chain)
+    cands = ['dskip', 'post1_fwd', 'dpost1', 'ds', 'post2_fwd', 'dpost2', 'dh']
     warm_t = {}
     for i in range(args.warmup):
         pr = None
@@ -201,7 +203,7 @@ def main():
         if pr:
             torch.cuda.synchronize()
             warm_t[pr[0]] = pr[1][0].elapsed_time(pr[1][1])
-    dom = args.probe if args.probe != 'auto' else (max(warm_t, key=warm_t.get) if warm_t else 'skip_fwd')
+    dom = args.probe if args.probe != 'auto' else (max(warm_t, key=warm_t.get) if warm_t else 'dskip')
 
     # ---- timed region ----
     samples = {dom: [], 'layer_fwd': []}
@@ -214,7 +216,7 @@ def main():
         if i % 2 == 0:
             pending.append((dom, probe(dom)))
         else:
-            pending.append(('layer_fwd', probe('layer_fwd@%d' % ((7 * i) % n_layers(arch)))))
+            pending.append(('layer_fwd', probe('layer_fwd')))
         step(args.warmup + i)
     torch.cuda.synchronize()
     if world > 1:

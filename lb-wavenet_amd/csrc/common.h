@@ -41,3 +41,12 @@ void lbwn_set_error(const char* fmt, ...);
       return 22; /* EINVAL */         \
     }                                 \
   } while (0)
+
+#define LBWN_HIP(call)                                                          \
+  do {                                                                          \
+    hipError_t e__ = (call);                                                    \
+    if (e__ != hipSuccess) {                                                    \
+      lbwn_set_error("%s:%d: %s", __FILE__, __LINE__, hipGetErrorString(e__));  \
+      return (int)e__;                                                          \
+    }                                                                           \
+  } while (0)

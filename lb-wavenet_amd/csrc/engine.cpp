@@ -4,6 +4,7 @@
 // native loop here, every buffer is carved once at plan creation, and nothing allocates
 // or synchronises inside forward/backward (so a caller may capture them in a hipGraph).
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -18,11 +19,15 @@ struct lbwn_plan {
   int B, T, L, nbl, H, Cr, Cd, Cs, Cp, Q;
   long M;
   // workspace carving (byte offsets)
-  size_t oX, oZ, oS, oR2, oLOG, oGA[2], oGC0[2], oDX0, oSLAB[2], oSPLIT, oCOLS, oHEADP, oBSUM, oWPK;
+  size_t oX, oZ, oS, oR2, oLOG, oDH, oDS, oDZ, oGA[2], oGC0[2], oDX0, oSLAB, oSPLIT, oSPLIT2, oCOLS, oCOLS2,
+      oHEADP, oBSUM, oWPK, oFLAGS, oSTATUS, oOCG;
   size_t total;
   long x_layer_stride;  // floats
   int split_post2, split_post1, split_skip, split_pre;
   long split_floats;
+  int nblk;                      // layer-bwd blocks = slab partials per layer
+  bool chain = false;            // persistent layer-chain kernels (n_res = n_dil = 32)
+  int chain_grid = 0;            // resident blocks for the chain (set on first use)
   // one-shot event probe
   char probe[32];
   hipEvent_t probe_start, probe_stop;
@@ -130,20 +135,33 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->split_floats = std::max({(long)p->split_post2 * p->Cp * p->Q, (long)p->split_post1 * p->Cs * p->Cp,
                               (long)p->split_skip * ldz * p->Cs, (long)p->split_pre * p->Q * p->Cr});
   const int nblk = lbwn_layer_bwd_grid(B, T);
+  p->nblk = nblk;
   size_t cur = 0;
   p->oX = carve(cur, sizeof(float) * (size_t)p->x_layer_stride * L);
   p->oZ = carve(cur, sizeof(float) * (size_t)M * ldz);
   p->oS = carve(cur, sizeof(float) * (size_t)M * p->Cs);
   p->oR2 = carve(cur, sizeof(float) * (size_t)M * p->Cp);
   p->oLOG = carve(cur, sizeof(float) * (size_t)M * p->Q);
+  p->oDH = carve(cur, sizeof(float) * (size_t)M * p->Cp);
+  p->oDS = carve(cur, sizeof(float) * (size_t)M * p->Cs);
+  p->oDZ = carve(cur, sizeof(float) * (size_t)M * ldz);
   for (int i = 0; i < 2; ++i) {
     p->oGA[i] = carve(cur, sizeof(float) * (size_t)M * p->Cr);
     p->oGC0[i] = carve(cur, sizeof(float) * (size_t)M * p->Cr);
-    p->oSLAB[i] = carve(cur, sizeof(float) * (size_t)nblk * lbwn_layer_slab_stride());
   }
+  const int ntiles = B * ((T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS);
+  p->oSLAB = carve(cur, sizeof(float) * (size_t)L * std::max(nblk, ntiles) * lbwn_layer_slab_stride());
   p->oDX0 = carve(cur, sizeof(float) * (size_t)M * p->Cr);
   p->oSPLIT = carve(cur, sizeof(float) * (size_t)p->split_floats);
+  p->oSPLIT2 = carve(cur, sizeof(float) * (size_t)p->split_pre * p->Q * p->Cr);
   p->oCOLS = carve(cur, sizeof(float) * (size_t)lbwn_colsum_ws_floats((int)M, std::max({p->Cs, p->Cp, p->Q, p->Cr})));
+  p->oCOLS2 = carve(cur, sizeof(float) * (size_t)lbwn_colsum_ws_floats((int)M, p->Cr));
+  // [status (16 B) | hand-off flags], zeroed together before every chain launch
+  p->oSTATUS = carve(cur, 16 + sizeof(unsigned) * (size_t)B * ((T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS));
+  p->oFLAGS = p->oSTATUS + 16;
+  const char* nc = getenv("LBWN_NO_CHAIN");
+  p->chain = p->Cr == 32 && p->Cd == 32 && !(nc && nc[0] == '1');
+  p->oOCG = p->chain ? carve(cur, sizeof(float) * (size_t)L * M * 32) : 0;
   p->oHEADP = carve(cur, sizeof(float) * 3 * 2048);
   p->oBSUM = carve(cur, sizeof(float) * (size_t)p->Cs);
   p->oWPK = carve(cur, sizeof(float) * (size_t)L * lbwn_layer_image_floats());
@@ -162,6 +180,10 @@ int lbwn_plan_tensor(const lbwn_plan* p, const char* name, size_t* off, size_t* 
   else if (!strcmp(name, "s")) { *off = p->oS; *bytes = f * M * p->Cs; }
   else if (!strcmp(name, "r2")) { *off = p->oR2; *bytes = f * M * p->Cp; }
   else if (!strcmp(name, "logits")) { *off = p->oLOG; *bytes = f * M * p->Q; }
+  else if (!strcmp(name, "status")) { *off = p->oSTATUS; *bytes = 16; }
+  else if (!strcmp(name, "dh")) { *off = p->oDH; *bytes = f * M * p->Cp; }
+  else if (!strcmp(name, "ds")) { *off = p->oDS; *bytes = f * M * p->Cs; }
+  else if (!strcmp(name, "dz")) { *off = p->oDZ; *bytes = f * M * p->L * p->Cd; }
   else LBWN_REQUIRE(false, "plan_tensor: unknown tensor '%s'", name);
   return 0;
 }
@@ -173,11 +195,45 @@ static lbwn_gemm_args gemm0() {
   return g;
 }
 
+namespace {
+
+// Device facts needed at first launch (not at plan creation, which must work without a GPU).
+int ensure_device(lbwn_plan* p) {
+  if (p->chain_grid) return 0;
+  // chain grid: at most one block per CU, so every block of a round is resident
+  int dev = 0, ncu = 0;
+  LBWN_HIP(hipGetDevice(&dev));
+  LBWN_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  const int ntiles = p->B * ((p->T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS);
+  p->chain_grid = std::max(1, std::min(ntiles, ncu));
+  return 0;
+}
+
+lbwn_layer_args layer_base(const lbwn_plan* p, const lbwn_params* P, const float* WPK, const int* ids, int l) {
+  const int Cr = p->Cr, Cd = p->Cd;
+  lbwn_layer_args a;
+  memset(&a, 0, sizeof(a));
+  a.w_sig = P->sig + (long)l * 2 * Cr * Cd;
+  a.w_gate = P->gate + (long)l * 2 * Cr * Cd;
+  a.b_sig = P->sig_b ? P->sig_b + (long)l * Cd : nullptr;
+  a.b_gate = P->gate_b ? P->gate_b + (long)l * Cd : nullptr;
+  a.w_res = P->res + (long)l * Cd * Cr;
+  a.b_res = P->res_b ? P->res_b + (long)l * Cr : nullptr;
+  a.wpack = WPK + (long)l * lbwn_layer_image_floats();
+  a.ids = ids;
+  a.B = p->B; a.T = p->T; a.H = p->H; a.d = 1 << (l % p->nbl); a.Cr = Cr; a.Cd = Cd;
+  return a;
+}
+
+}  // namespace
+
 int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* wav_q, const int* ids,
                        const float* mel, float* save, float* stats, void* stream) {
   LBWN_REQUIRE(p && P && ws && wav_q && ids && save && stats, "train_forward: null argument");
   (void)mel;
   hipStream_t st = (hipStream_t)stream;
+  int e;
+  if ((e = ensure_device(p))) return e;
   const int L = p->L, B = p->B, T = p->T, H = p->H, Cr = p->Cr, Cd = p->Cd;
   const long M = p->M, ldz = (long)L * Cd;
   float* X = at<float>(ws, p->oX);
@@ -186,7 +242,6 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   float* R2 = at<float>(ws, p->oR2);
   float* LOG = at<float>(ws, p->oLOG);
   float* bsum = at<float>(ws, p->oBSUM);
-  int e;
   // per-layer weights -> padded LDS images (once per step; reused by the backward)
   float* WPK = at<float>(ws, p->oWPK);
   if ((e = lbwn_pack_layers_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b, WPK, L, Cr, Cd, st)))
@@ -195,45 +250,42 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   if ((e = lbwn_embed_launch(wav_q, P->pre, P->pre_b, X, B, T, H, Cr, p->Q, st))) return e;
   // D-separation prepend for every layer (tmodel.py:122-127)
   if ((e = lbwn_dsep_prepend_launch(X, p->x_layer_stride, save, L, p->nbl, B, T, H, Cr, st))) return e;
-  for (int l = 0; l < L; ++l) {
-    lbwn_layer_args a;
-    memset(&a, 0, sizeof(a));
-    a.x_in = X + l * p->x_layer_stride;
-    a.x_out = (l + 1 < L) ? X + (l + 1) * p->x_layer_stride : nullptr;
-    a.z = Z + (long)l * Cd;
-    a.ldz = ldz;
-    a.w_sig = P->sig + (long)l * 2 * Cr * Cd;
-    a.w_gate = P->gate + (long)l * 2 * Cr * Cd;
-    a.b_sig = P->sig_b ? P->sig_b + (long)l * Cd : nullptr;
-    a.b_gate = P->gate_b ? P->gate_b + (long)l * Cd : nullptr;
-    a.w_res = P->res + (long)l * Cd * Cr;
-    a.b_res = P->res_b ? P->res_b + (long)l * Cr : nullptr;
-    a.wpack = WPK + (long)l * lbwn_layer_image_floats();
-    a.ids = ids;
-    a.B = B;
-    a.T = T;
-    a.H = H;
-    a.d = 1 << (l % p->nbl);
-    a.Cr = Cr;
-    a.Cd = Cd;
-    Probe(p, st, "layer_fwd", l, l == 0);
-    if ((e = lbwn_layer_fwd_launch(a, st))) return e;
-    Probe::end(p, st, "layer_fwd", l, l == L - 1);
+  if (p->chain) {
+    // all layers in one persistent launch (tmodel.py:313-325)
+    lbwn_chain_args c;
+    memset(&c, 0, sizeof(c));
+    c.X = X; c.xls = p->x_layer_stride; c.Z = Z; c.ldz = ldz; c.wpack = WPK; c.ids = ids;
+    c.flags = at<unsigned>(ws, p->oFLAGS); c.status = at<unsigned>(ws, p->oSTATUS);
+    c.B = B; c.T = T; c.H = H; c.L = L; c.nbl = p->nbl; c.Cr = Cr; c.Cd = Cd; c.grid = p->chain_grid;
+    Probe(p, st, "layer_fwd");
+    if ((e = lbwn_chain_fwd_launch(c, st))) return e;
+    Probe::end(p, st, "layer_fwd");
+  } else {
+    for (int l = 0; l < L; ++l) {
+      lbwn_layer_args a = layer_base(p, P, WPK, ids, l);
+      a.x_in = X + l * p->x_layer_stride;
+      a.x_out = (l + 1 < L) ? X + (l + 1) * p->x_layer_stride : nullptr;
+      a.z = Z + (long)l * Cd;
+      a.ldz = ldz;
+      Probe(p, st, "layer_fwd", l, l == 0);
+      if ((e = lbwn_layer_fwd_launch(a, st))) return e;
+      Probe::end(p, st, "layer_fwd", l, l == L - 1);
+    }
   }
   // SAVE_l <- last d rows of [SAVE ++ x_l]  (tmodel.py:165)
   if ((e = lbwn_dsep_save_launch(X, p->x_layer_stride, save, L, p->nbl, B, T, H, Cr, st))) return e;
   // S = Σ_l (z_l·SKIP_l + b) as ONE GEMM over Zcat (tmodel.py:171-184, :316-320)
-  lbwn_gemm_args g = gemm0();
-  if (P->skip_b) {
-    if ((e = lbwn_sum_bias_launch(P->skip_b, L, p->Cs, bsum, st))) return e;
+  if (P->skip_b && (e = lbwn_sum_bias_launch(P->skip_b, L, p->Cs, bsum, st))) return e;
+  {
+    lbwn_gemm_args g = gemm0();
+    g.A = Z; g.lda = ldz; g.B = P->skip; g.ldb = p->Cs; g.C = S; g.ldc = p->Cs;
+    g.M = (int)M; g.N = p->Cs; g.K = (int)ldz; g.bias = P->skip_b ? bsum : nullptr;
+    Probe(p, st, "skip_fwd");
+    if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
+    Probe::end(p, st, "skip_fwd");
   }
-  g.A = Z; g.lda = ldz; g.B = P->skip; g.ldb = p->Cs; g.C = S; g.ldc = p->Cs;
-  g.M = (int)M; g.N = p->Cs; g.K = (int)ldz; g.bias = P->skip_b ? bsum : nullptr;
-  Probe(p, st, "skip_fwd");
-  if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
-  Probe::end(p, st, "skip_fwd");
   // relu(relu(S)·POST1 + b1)  (tmodel.py:194-203)
-  g = gemm0();
+  lbwn_gemm_args g = gemm0();
   g.A = S; g.lda = p->Cs; g.B = P->post1; g.ldb = p->Cp; g.C = R2; g.ldc = p->Cp;
   g.M = (int)M; g.N = p->Cp; g.K = p->Cs; g.bias = P->post1_b; g.relu_a = 1; g.relu_out = 1;
   Probe(p, st, "post1_fwd");
@@ -257,21 +309,28 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   return lbwn_stats_reduce_launch(h.partial, nb, stats, st);
 }
 
+// Backward (tmodel.py:338-340, TF autodiff of the graph above): head/skip GEMMs, then the
+// residual stack in reverse (one persistent chain launch, or one launch per layer), then
+// one batched reduction of every layer's weight-gradient partials, then dPRE.
 int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G, void* ws, const int* wav_q,
                         const int* ids, const float* mel, void* stream) {
   LBWN_REQUIRE(p && P && G && ws && wav_q && ids, "train_backward: null argument");
   (void)mel;
   hipStream_t st = (hipStream_t)stream;
-  const int L = p->L, B = p->B, T = p->T, H = p->H, Cr = p->Cr, Cd = p->Cd, Cs = p->Cs, Cp = p->Cp, Q = p->Q;
+  int e;
+  if ((e = ensure_device(p))) return e;
+  const int L = p->L, B = p->B, T = p->T, Cr = p->Cr, Cd = p->Cd, Cs = p->Cs, Cp = p->Cp, Q = p->Q;
   const long M = p->M, ldz = (long)L * Cd;
   float* X = at<float>(ws, p->oX);
   float* Z = at<float>(ws, p->oZ);
   float* S = at<float>(ws, p->oS);
   float* R2 = at<float>(ws, p->oR2);
   float* LOG = at<float>(ws, p->oLOG);
+  float* DH = at<float>(ws, p->oDH);
+  float* DS = at<float>(ws, p->oDS);
+  float* DZ = at<float>(ws, p->oDZ);
   float* SPL = at<float>(ws, p->oSPLIT);
   float* COLS = at<float>(ws, p->oCOLS);
-  int e;
   lbwn_gemm_args g;
   // dPOST2 = R2ᵀ·dlogits, db2 = Σ dlogits
   g = gemm0();
@@ -280,91 +339,91 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   if ((e = lbwn_gemm_launch(g, 0, 0, p->split_post2, SPL, st))) return e;
   Probe::end(p, st, "dpost2");
   if (G->post2_b && (e = lbwn_colsum_launch(LOG, Q, (int)M, Q, G->post2_b, 0, COLS, st))) return e;
-  // dH1 = dlogits·POST2ᵀ ⊙ (R2 > 0)   (in place over R2)
+  // dH1 = dlogits·POST2ᵀ ⊙ (R2 > 0)
   g = gemm0();
-  g.A = LOG; g.lda = Q; g.B = P->post2; g.ldb = Q; g.C = R2; g.ldc = Cp; g.M = (int)M; g.N = Cp; g.K = Q;
+  g.A = LOG; g.lda = Q; g.B = P->post2; g.ldb = Q; g.C = DH; g.ldc = Cp; g.M = (int)M; g.N = Cp; g.K = Q;
   g.mask = R2; g.ldm = Cp;
+  Probe(p, st, "dh");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
+  Probe::end(p, st, "dh");
   // dPOST1 = relu(S)ᵀ·dH1, db1 = Σ dH1
   g = gemm0();
-  g.A = S; g.lda = Cs; g.relu_a = 1; g.B = R2; g.ldb = Cp; g.C = G->post1; g.ldc = Cp; g.M = Cs; g.N = Cp;
+  g.A = S; g.lda = Cs; g.relu_a = 1; g.B = DH; g.ldb = Cp; g.C = G->post1; g.ldc = Cp; g.M = Cs; g.N = Cp;
   g.K = (int)M;
   Probe(p, st, "dpost1");
   if ((e = lbwn_gemm_launch(g, 0, 0, p->split_post1, SPL, st))) return e;
   Probe::end(p, st, "dpost1");
-  if (G->post1_b && (e = lbwn_colsum_launch(R2, Cp, (int)M, Cp, G->post1_b, 0, COLS, st))) return e;
-  // dS = dH1·POST1ᵀ ⊙ (S > 0)   (in place over S)
+  if (G->post1_b && (e = lbwn_colsum_launch(DH, Cp, (int)M, Cp, G->post1_b, 0, COLS, st))) return e;
+  // dS = dH1·POST1ᵀ ⊙ (S > 0)
   g = gemm0();
-  g.A = R2; g.lda = Cp; g.B = P->post1; g.ldb = Cp; g.C = S; g.ldc = Cs; g.M = (int)M; g.N = Cs; g.K = Cp;
+  g.A = DH; g.lda = Cp; g.B = P->post1; g.ldb = Cp; g.C = DS; g.ldc = Cs; g.M = (int)M; g.N = Cs; g.K = Cp;
   g.mask = S; g.ldm = Cs;
+  Probe(p, st, "ds");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
+  Probe::end(p, st, "ds");
   // dSKIPcat = Zcatᵀ·dS; every layer's SKIP_BIAS gets the same Σ dS
   g = gemm0();
-  g.A = Z; g.lda = ldz; g.B = S; g.ldb = Cs; g.C = G->skip; g.ldc = Cs; g.M = (int)ldz; g.N = Cs; g.K = (int)M;
+  g.A = Z; g.lda = ldz; g.B = DS; g.ldb = Cs; g.C = G->skip; g.ldc = Cs; g.M = (int)ldz; g.N = Cs; g.K = (int)M;
   Probe(p, st, "dskip");
   if ((e = lbwn_gemm_launch(g, 0, 0, p->split_skip, SPL, st))) return e;
   Probe::end(p, st, "dskip");
   if (G->skip_b) {
-    if ((e = lbwn_colsum_launch(S, Cs, (int)M, Cs, G->skip_b, 0, COLS, st))) return e;
+    if ((e = lbwn_colsum_launch(DS, Cs, (int)M, Cs, G->skip_b, 0, COLS, st))) return e;
     if ((e = lbwn_bcast_rows_launch(G->skip_b, L, Cs, st))) return e;
   }
-  // dZ = dS·SKIPcatᵀ  (over Z: z is recomputed by the layer backward)
+  // dZ = dS·SKIPcatᵀ
   g = gemm0();
-  g.A = S; g.lda = Cs; g.B = P->skip; g.ldb = Cs; g.C = Z; g.ldc = ldz; g.M = (int)M; g.N = (int)ldz; g.K = Cs;
+  g.A = DS; g.lda = Cs; g.B = P->skip; g.ldb = Cs; g.C = DZ; g.ldc = ldz; g.M = (int)M; g.N = (int)ldz; g.K = Cs;
   Probe(p, st, "dz");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
   Probe::end(p, st, "dz");
-  // residual stack in reverse; layer l reduces layer l+1's weight-grad partials on the fly
-  const int nblk = lbwn_layer_bwd_grid(B, T);
+  // residual stack in reverse
   const float* WPK = at<float>(ws, p->oWPK);
-  for (int l = L - 1; l >= 0; --l) {
-    lbwn_layer_args a;
-    memset(&a, 0, sizeof(a));
-    a.x_in = X + l * p->x_layer_stride;
-    a.w_sig = P->sig + (long)l * 2 * Cr * Cd;
-    a.w_gate = P->gate + (long)l * 2 * Cr * Cd;
-    a.b_sig = P->sig_b ? P->sig_b + (long)l * Cd : nullptr;
-    a.b_gate = P->gate_b ? P->gate_b + (long)l * Cd : nullptr;
-    a.w_res = P->res + (long)l * Cd * Cr;
-    a.b_res = P->res_b ? P->res_b + (long)l * Cr : nullptr;
-    a.wpack = WPK + (long)l * lbwn_layer_image_floats();
-    a.ids = ids;
-    a.B = B; a.T = T; a.H = H; a.d = 1 << (l % p->nbl); a.Cr = Cr; a.Cd = Cd;
-    a.dz_skip = Z + (long)l * Cd;
-    a.lddz = ldz;
-    if (l + 1 < L) {
-      a.g_a = at<float>(ws, p->oGA[(l + 1) & 1]);
-      a.g_c0 = at<float>(ws, p->oGC0[(l + 1) & 1]);
-      a.g_d = 1 << ((l + 1) % p->nbl);
-      const int lp = l + 1;
-      a.red_slab = at<float>(ws, p->oSLAB[lp & 1]);
-      a.red_nparts = nblk;
-      a.red_stride = lbwn_layer_slab_stride();
-      a.red_dsig = G->sig + (long)lp * 2 * Cr * Cd;
-      a.red_dgate = G->gate + (long)lp * 2 * Cr * Cd;
-      a.red_dres = G->res + (long)lp * Cd * Cr;
-      a.red_dbsig = G->sig_b ? G->sig_b + (long)lp * Cd : nullptr;
-      a.red_dbgate = G->gate_b ? G->gate_b + (long)lp * Cd : nullptr;
-      a.red_dbres = G->res_b ? G->res_b + (long)lp * Cr : nullptr;
+  const int sstr = lbwn_layer_slab_stride();
+  float* SLABS = at<float>(ws, p->oSLAB);
+  if (p->chain) {
+    const int ntiles = B * ((T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS);
+    lbwn_chain_args c;
+    memset(&c, 0, sizeof(c));
+    c.X = X; c.xls = p->x_layer_stride; c.DZ = DZ; c.ldz = ldz; c.wpack = WPK; c.ids = ids;
+    c.slab = SLABS; c.ocg = at<float>(ws, p->oOCG); c.ocls = M * 32;
+    c.dx0_a = at<float>(ws, p->oGA[0]); c.dx0_c = at<float>(ws, p->oGC0[0]);
+    c.flags = at<unsigned>(ws, p->oFLAGS); c.status = at<unsigned>(ws, p->oSTATUS);
+    c.B = B; c.T = T; c.H = p->H; c.L = L; c.nbl = p->nbl; c.Cr = Cr; c.Cd = Cd; c.grid = p->chain_grid;
+    Probe(p, st, "layer_bwd");
+    if ((e = lbwn_chain_bwd_launch(c, st))) return e;
+    Probe::end(p, st, "layer_bwd");
+    lbwn_layer_red_args r;
+    r.slab = SLABS; r.nparts = ntiles; r.stride = sstr; r.Cr = Cr; r.Cd = Cd;
+    r.dsig = G->sig; r.dgate = G->gate; r.dres = G->res;
+    r.dbsig = G->sig_b; r.dbgate = G->gate_b; r.dbres = G->res_b;
+    Probe(p, st, "layer_reduce");
+    if ((e = lbwn_layer_reduce_all_launch(r, L, (long)ntiles * sstr, st))) return e;
+    Probe::end(p, st, "layer_reduce");
+  } else {
+      for (int l = L - 1; l >= 0; --l) {
+      lbwn_layer_args a = layer_base(p, P, WPK, ids, l);
+      a.x_in = X + l * p->x_layer_stride;
+      a.dz_skip = DZ + (long)l * Cd;
+      a.lddz = ldz;
+      if (l + 1 < L) {
+        a.g_a = at<float>(ws, p->oGA[(l + 1) & 1]);
+        a.g_c0 = at<float>(ws, p->oGC0[(l + 1) & 1]);
+        a.g_d = 1 << ((l + 1) % p->nbl);
+      }
+      a.out_a = at<float>(ws, p->oGA[l & 1]);
+      a.out_c0 = at<float>(ws, p->oGC0[l & 1]);
+      a.slab = SLABS + (long)l * p->nblk * sstr;
+      a.slab_stride = sstr;
+      Probe(p, st, "layer_bwd", l, l == L - 1);
+      if ((e = lbwn_layer_bwd_launch(a, st))) return e;
+      Probe::end(p, st, "layer_bwd", l, l == 0);
     }
-    a.out_a = at<float>(ws, p->oGA[l & 1]);
-    a.out_c0 = at<float>(ws, p->oGC0[l & 1]);
-    a.slab = at<float>(ws, p->oSLAB[l & 1]);
-    a.slab_stride = lbwn_layer_slab_stride();
-    Probe(p, st, "layer_bwd", l, l == L - 1);
-    if ((e = lbwn_layer_bwd_launch(a, st))) return e;
-    Probe::end(p, st, "layer_bwd", l, l == 0);
-  }
-  {  // layer 0's partials
-    lbwn_layer_args a;
-    memset(&a, 0, sizeof(a));
-    a.Cr = Cr; a.Cd = Cd;
-    a.red_slab = at<float>(ws, p->oSLAB[0]);
-    a.red_nparts = nblk;
-    a.red_stride = lbwn_layer_slab_stride();
-    a.red_dsig = G->sig; a.red_dgate = G->gate; a.red_dres = G->res;
-    a.red_dbsig = G->sig_b; a.red_dbgate = G->gate_b; a.red_dbres = G->res_b;
-    if ((e = lbwn_layer_reduce_launch(a, st))) return e;
+    lbwn_layer_red_args r;
+    r.slab = SLABS; r.nparts = p->nblk; r.stride = sstr; r.Cr = Cr; r.Cd = Cd;
+    r.dsig = G->sig; r.dgate = G->gate; r.dres = G->res;
+    r.dbsig = G->sig_b; r.dbgate = G->gate_b; r.dbres = G->res_b;
+    if ((e = lbwn_layer_reduce_all_launch(r, L, (long)p->nblk * sstr, st))) return e;
   }
   // dx_0 = (g + dcur) + shift(dprev); dPRE = onehot(q)ᵀ·dx_0, dPRE_BIAS = Σ dx_0
   float* DX0 = at<float>(ws, p->oDX0);
@@ -373,11 +432,9 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   g = gemm0();
   g.a_codes = wav_q; g.B = DX0; g.ldb = Cr; g.C = G->pre; g.ldc = Cr; g.M = Q; g.N = Cr; g.K = (int)M;
   g.lda = 4;  // unused (one-hot A)
-  if (Cr % 4 == 0) {
-    if ((e = lbwn_gemm_launch(g, 0, 0, p->split_pre, SPL, st))) return e;
-  } else {
-    LBWN_REQUIRE(false, "train_backward: n_res %% 4 != 0 not supported for the PRE gradient yet");
-  }
-  if (G->pre_b && (e = lbwn_colsum_launch(DX0, Cr, (int)M, Cr, G->pre_b, 0, COLS, st))) return e;
+  LBWN_REQUIRE(Cr % 4 == 0, "train_backward: n_res %% 4 != 0 not supported for the PRE gradient yet");
+  if ((e = lbwn_gemm_launch(g, 0, 0, p->split_pre, at<float>(ws, p->oSPLIT2), st))) return e;
+  if (G->pre_b && (e = lbwn_colsum_launch(DX0, Cr, (int)M, Cr, G->pre_b, 0, at<float>(ws, p->oCOLS2), st)))
+    return e;
   return 0;
 }

@@ -41,10 +41,13 @@ struct lbwn_layer_args {
   int slab_stride;
   float* dv_out; long lddv; // [M][2Cd] nullable (needed for LC grads)
   float* gc_dtab;           // [ncat+1][2Cd] atomically accumulated (nullable)
-  // ---- deferred reduction of the previous (deeper) layer's slab ----
-  const float* red_slab; int red_nparts; int red_stride;
-  float* red_dsig; float* red_dgate; float* red_dres;
-  float* red_dbsig; float* red_dbgate; float* red_dbres;
+};
+// Sum a layer's per-block weight-grad partials into the reference-layout gradients.
+struct lbwn_layer_red_args {
+  const float* slab; int nparts; int stride;
+  float* dsig; float* dgate; float* dres;      // [2][Cr][Cd], [2][Cr][Cd], [Cd][Cr]
+  float* dbsig; float* dbgate; float* dbres;   // nullable
+  int Cr, Cd;
 };
 constexpr int LBWN_LAYER_POS = 128;   // positions per layer-kernel block
 int lbwn_layer_fwd_launch(const lbwn_layer_args& a, hipStream_t st);
@@ -55,7 +58,28 @@ int lbwn_layer_nblocks(int B, int T);
 int lbwn_layer_bwd_grid(int B, int T);   // = number of slab partials per layer
 int lbwn_pack_layers_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                             const float* res, const float* res_b, float* out, int L, int Cr, int Cd, hipStream_t st);
-int lbwn_layer_reduce_launch(const lbwn_layer_args& a, hipStream_t st);  // standalone reduction
+int lbwn_layer_reduce_launch(const lbwn_layer_red_args& r, hipStream_t st);
+
+// Persistent layer chain (all L layers in one launch, tile hand-offs through flags).
+struct lbwn_chain_args {
+  float* X; long xls;          // x_l buffers of all layers, layer stride in floats
+  float* Z; long ldz;
+  const float* wpack;
+  const float* gc_tab; const int* ids;
+  unsigned* flags;             // [B·ceil(T/128)] (zeroed by the launcher)
+  unsigned* status;            // sticky error word (spin timeout)
+  int B, T, H, L, nbl, Cr, Cd;
+  int grid;                    // ≤ blocks resident at once (rounds of tiles)
+  // backward only
+  const float* DZ;             // dZ (row stride ldz)
+  float* slab;                 // [L][ntiles][slab_stride]
+  float* ocg; long ocls;       // out_c0 hand-off rows per layer [L][B·T][32]
+  float* dx0_a; float* dx0_c;  // layer 0's dx parts [B·T][32]
+};
+int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st);
+int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st);
+int lbwn_layer_reduce_all_launch(const lbwn_layer_red_args& r, int L, long slab_layer, hipStream_t st);
+int lbwn_chain_fwd_lds_bytes();
 
 // D-separation state transfer for ALL layers at once.
 int lbwn_dsep_prepend_launch(float* xall, long xlayer_stride, const float* save, int L, int nbl,

@@ -42,10 +42,11 @@ struct BwdK {
   const float* gc_tab; const int* ids; const float* cond; float* dv_out; float* gc_dtab;
   long lddz, ldcond, lddv;
   int B, T, H, d, Cr, Cd, g_d, slab_stride;
-  // deferred reduction
-  const float* red_slab; float* red_dsig; float* red_dgate; float* red_dres;
-  float* red_dbsig; float* red_dbgate; float* red_dbres;
-  int red_nparts, red_stride;
+};
+// Standalone slab reduction (runs on an auxiliary stream, off the layer chain).
+struct RedK {
+  const float* slab; float* dsig; float* dgate; float* dres; float* dbsig; float* dbgate; float* dbres;
+  int nparts, stride, Cr, Cd;
 };
 
 // ---- weight packing ---------------------------------------------------------------------
@@ -273,36 +274,242 @@ __global__ __launch_bounds__(256) void layer_fwd_kernel(FwdK a) {
   }
 }
 
+// ---- persistent forward chain -------------------------------------------------------------
+// The 50 dependent layers as ONE launch.  A block owns a 128-position tile of one stream for
+// every layer; its own rows stay in LDS (double-buffered x_l / x_{l+1}), and only the dilated
+// tap's halo (rows t0-d .. t0-1: min(d,128) rows of ONE producer tile of the same stream, or
+// SAVE) crosses blocks.  Hand-off (cdna_hip_programming §6 G16, R1 form): the producer stores
+// x_{l+1} write-through (sc1), every wave drains (s_waitcnt vmcnt(0)), block barrier, one
+// lane stores flag[tile] = l+1 (relaxed, agent); the consumer polls that word relaxed from one
+// lane, barriers, and reads the halo ONLY with sc1 loads (no acquire fence needed).  The own
+// tap (W1·x[t]) is computed before the poll so the hand-off latency hides behind it.
+// Deadlock freedom: tiles run in rounds of gridDim.x ≤ resident blocks, in increasing tile
+// order; a producer tile is always in the same round (resident) or an earlier one (done).
+// Every spin is bounded (SPIN_TIMEOUT) and reports through the status word.
+typedef __attribute__((address_space(1))) unsigned gu32;
+constexpr long long SPIN_TIMEOUT = 400000000LL;  // wall_clock64 ticks (100 MHz) = 4 s
+constexpr int BUF_DW3 = 0x00020000;
+
+struct ChainFK {
+  float* X; long xls;        // x_l for all layers: layer stride (floats); each [B][H+T][32]
+  float* Z; long ldz;
+  const float* wpack;        // L packed images
+  const float* gc_tab; const int* ids; const float* cond; long ldcond;  // (conv_init)
+  unsigned* flags; unsigned* status;
+  int B, T, H, L, nbl, Cd;
+};
+
+LBWN_DEV bool wait_flag_ge(unsigned* f, unsigned want, unsigned* status, unsigned code) {
+  const long long t0 = wall_clock64();
+  for (;;) {
+    if (__hip_atomic_load((gu32*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) return true;
+    if (wall_clock64() - t0 > SPIN_TIMEOUT) {
+      __hip_atomic_store((gu32*)status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+LBWN_DEV void publish_flag(unsigned* f, unsigned v) {
+  __hip_atomic_store((gu32*)f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// bias (+ GC / LC conditioning) into the accumulators (acc layout rows = out channel)
+template <typename K>
+LBWN_DEV void conv_init(const float* bs, const K& a, long m, bool valid, int h, floatx16& acc_s, floatx16& acc_g) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    acc_s[r] = bs[acc_row(r, h)];
+    acc_g[r] = bs[32 + acc_row(r, h)];
+  }
+  if (valid && (a.gc_tab || a.cond)) {
+    const float* cs = a.gc_tab ? a.gc_tab + (long)a.ids[m] * 2 * a.Cd : nullptr;
+    const float* cl = a.cond ? a.cond + m * a.ldcond : nullptr;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = acc_row(r, h);
+      if (o < a.Cd) {
+        if (cs) { acc_s[r] += cs[o]; acc_g[r] += cs[a.Cd + o]; }
+        if (cl) { acc_s[r] += cl[o]; acc_g[r] += cl[a.Cd + o]; }
+      }
+    }
+  }
+}
+
+// acc += Wkᵀ·x over one tap: Wk = the 32 weight-image rows of that tap, xrow = this lane's
+// 32-channel input row (LDS)
+LBWN_DEV void conv_half(const float* xrow, const float* Wk, int pi, int h, floatx16& acc_s, floatx16& acc_g) {
+  floatx4 bx[2];
+  float ws_[2][4], wg_[2][4];
+  auto load = [&](int g, int buf) {
+    bx[buf] = *(const floatx4*)(xrow + 8 * g + 4 * h);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = 8 * g + 4 * h + j;
+      ws_[buf][j] = Wk[k * WS + pi];
+      wg_[buf][j] = Wk[k * WS + 32 + pi];
+    }
+  };
+  load(0, 0);
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int cb = g & 1;
+    if (g + 1 < 4) load(g + 1, cb ^ 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc_s = mfma32(ws_[cb][j], bx[cb][j], acc_s);
+      acc_g = mfma32(wg_[cb][j], bx[cb][j], acc_g);
+    }
+  }
+}
+
+static_assert(4096 + 768 <= 2 * LP * XS, "RED + bias partials must fit in Xp and Xc");
+constexpr int CF_LDS = 3 * LP * XS + WIMG;          // Xc[2] | HALO | IMG  (77.7 KB)
+constexpr int IMG_PF = (WIMG / 4 + 255) / 256;      // float4 per thread to prefetch an image
+
+__global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
+  __shared__ __attribute__((aligned(16))) float sm[CF_LDS];
+  __shared__ int s_fail;
+  float* HALO = sm + 2 * LP * XS;
+  float* Ws = HALO + LP * XS;
+  float* Rs = Ws + 64 * WS;
+  float* bs = Rs + 32 * XS;
+  float* br = bs + 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int pi = lane & 31, h = lane >> 5;
+  const int r = 32 * w + pi;  // this lane's row of the tile
+  const int tps = (a.T + LP - 1) / LP, ntiles = a.B * tps;
+  if (tid == 0) s_fail = 0;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int b = tile / tps, tt = tile % tps, t0 = tt * LP;
+    const int t = t0 + r;
+    const bool valid = t < a.T;
+    const long m = (long)b * a.T + t;
+    const long sb = (long)b * (a.H + a.T) * 32;  // stream base inside a layer buffer
+    __syncthreads();  // previous tile's LDS use done
+    stage_image(Ws, a.wpack, tid);
+    stage_rows(sm, a.X + sb, t0, 0, a.T, a.H, 32, tid);  // x_0 (embed output, pre-launch)
+    __syncthreads();
+    for (int l = 0; l < a.L; ++l) {
+      const int d = 1 << (l % a.nbl);
+      float* cur = sm + (l & 1) * LP * XS;
+      float* nxt = sm + ((l + 1) & 1) * LP * XS;
+      float* xl = a.X + (long)l * a.xls + sb;
+      // 1. prefetch the next layer's weight image (pre-launch data: plain loads)
+      floatx4 pf[IMG_PF];
+      if (l + 1 < a.L) {
+        const floatx4* src = (const floatx4*)(a.wpack + (long)(l + 1) * WIMG);
+#pragma unroll
+        for (int i = 0; i < IMG_PF; ++i) {
+          const int e = tid + 256 * i;
+          if (e < WIMG / 4) pf[i] = src[e];
+        }
+      }
+      // 2. own tap first: W1·x[t]
+      floatx16 acc_s, acc_g;
+      conv_init(bs, a, m, valid, h, acc_s, acc_g);
+      conv_half(cur + r * XS, Ws + 32 * WS, pi, h, acc_s, acc_g);
+      // 3. wait for the producer of the halo rows (x_l is layer l-1's output)
+      const int ptt = tt - max(1, d / LP);
+      if (l > 0 && ptt >= 0) {
+        if (tid == 0 && !s_fail) {
+          if (!wait_flag_ge(a.flags + (long)b * tps + ptt, (unsigned)l, a.status, 1u)) s_fail = 1;
+        }
+        __syncthreads();
+      }
+      // 4. halo rows [0, min(d,LP)): x_l rows t0-d+row (SAVE rows when < 0), sc1 loads
+      {
+        const int nh = min(d, LP);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(xl, (short)0, (int)((long)(a.H + a.T) * 32 * 4), BUF_DW3);
+        for (int e = tid; e < nh * 8; e += 256) {
+          const int row = e >> 3, c4 = (e & 7) * 4;
+          const int off = ((a.H + t0 + row - d) * 32 + c4) * 4;
+          *(floatx4*)(HALO + row * XS + c4) = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+        }
+      }
+      __syncthreads();
+      // 5. dilated tap W0·x[t-d], gate, residual
+      const float* xp = (r >= d) ? cur + (r - d) * XS : HALO + r * XS;
+      conv_half(xp, Ws, pi, h, acc_s, acc_g);
+      floatx16 z;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) z[q] = tanhf_(acc_s[q]) * sigmoidf_(acc_g[q]);
+      if (l + 1 < a.L) {
+        floatx16 acc_r;
+        const float* xc = cur + r * XS;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const floatx4 xv = *(const floatx4*)(xc + 8 * q + 4 * h);
+          const floatx4 bv = *(const floatx4*)(br + 8 * q + 4 * h);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc_r[4 * q + j] = xv[j] + bv[j];
+        }
+        float ra[16];
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) ra[s2] = Rs[acc_row(s2, h) * XS + pi];
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) acc_r = mfma32(ra[s2], z[s2], acc_r);
+        float* xn = a.X + (long)(l + 1) * a.xls + sb;
+        const __amdgpu_buffer_rsrc_t rn =
+            __builtin_amdgcn_make_buffer_rsrc(xn, (short)0, (int)((long)(a.H + a.T) * 32 * 4), BUF_DW3);
+        float* nrow = nxt + r * XS;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const floatx4 v = floatx4{acc_r[4 * q], acc_r[4 * q + 1], acc_r[4 * q + 2], acc_r[4 * q + 3]};
+          *(floatx4*)(nrow + 8 * q + 4 * h) = v;
+          if (valid) __builtin_amdgcn_raw_buffer_store_b128(v, rn, ((a.H + t) * 32 + 8 * q + 4 * h) * 4, 0, 16);
+        }
+      }
+      // 6. publish x_{l+1}: every wave drains its sc1 stores, barrier, one lane signals
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0 && l + 1 < a.L) publish_flag(a.flags + tile, (unsigned)(l + 1));
+      if (valid) store_rows16(a.Z + m * a.ldz + (long)l * a.Cd, z, a.Cd, h);  // skip GEMM input
+      // 7. next weight image (everyone is past this layer's reads of IMG)
+      if (l + 1 < a.L) {
+#pragma unroll
+        for (int i = 0; i < IMG_PF; ++i) {
+          const int e = tid + 256 * i;
+          if (e < WIMG / 4) *(floatx4*)(Ws + 4 * e) = pf[i];
+        }
+        __syncthreads();
+      }
+    }
+  }
+}
+
 // ---- deferred slab reduction -------------------------------------------------------------
 
 // Destination of slab column c (padded 32-channel layout) in reference layout.
-LBWN_DEV void slab_store(const BwdK& a, int c, float tot) {
+LBWN_DEV void slab_store(const RedK& a, int c, float tot) {
   const int Cr = a.Cr, Cd = a.Cd;
   if (c < 4096) {
     const int cc = c & 2047, tap = cc >> 10, in = (cc >> 5) & 31, o = cc & 31;
-    float* dst = c < 2048 ? a.red_dsig : a.red_dgate;
+    float* dst = c < 2048 ? a.dsig : a.dgate;
     if (in < Cr && o < Cd) dst[(tap * Cr + in) * Cd + o] = tot;
   } else if (c < 5120) {
     const int cc = c - 4096, zc = cc >> 5, o = cc & 31;
-    if (zc < Cd && o < Cr) a.red_dres[zc * Cr + o] = tot;
+    if (zc < Cd && o < Cr) a.dres[zc * Cr + o] = tot;
   } else {
     const int cc = c - 5120, seg = cc >> 5, o = cc & 31;
-    if (seg == 0 && a.red_dbsig && o < Cd) a.red_dbsig[o] = tot;
-    if (seg == 1 && a.red_dbgate && o < Cd) a.red_dbgate[o] = tot;
-    if (seg == 2 && a.red_dbres && o < Cr) a.red_dbres[o] = tot;
+    if (seg == 0 && a.dbsig && o < Cd) a.dbsig[o] = tot;
+    if (seg == 1 && a.dbgate && o < Cd) a.dbgate[o] = tot;
+    if (seg == 2 && a.dbres && o < Cr) a.dbres[o] = tot;
   }
 }
 
 // Column group `grp` (32 columns) summed over all parts: thread = (part lane p8, column);
 // `pre` holds parts p8, p8+8, ... (up to RED_PARTS) loaded earlier.
-LBWN_DEV void slab_group_finish(const BwdK& a, int grp, const float (&pre)[RED_PARTS], float* scratch,
+LBWN_DEV void slab_group_finish(const RedK& a, int grp, const float (&pre)[RED_PARTS], float* scratch,
                                 int tid) {
   const int c = grp * 32 + (tid & 31), p8 = tid >> 5;
   float s = 0.f;
   if (c < SLAB) {
 #pragma unroll
     for (int j = 0; j < RED_PARTS; ++j) s += pre[j];
-    for (int p = p8 + 8 * RED_PARTS; p < a.red_nparts; p += 8) s += a.red_slab[(long)p * a.red_stride + c];
+    for (int p = p8 + 8 * RED_PARTS; p < a.nparts; p += 8) s += a.slab[(long)p * a.stride + c];
   }
   scratch[tid] = s;
   __syncthreads();
@@ -315,39 +522,345 @@ LBWN_DEV void slab_group_finish(const BwdK& a, int grp, const float (&pre)[RED_P
   __syncthreads();
 }
 
-LBWN_DEV void slab_group_prefetch(const BwdK& a, int grp, float (&pre)[RED_PARTS], int tid) {
+LBWN_DEV void slab_group_prefetch(const RedK& a, int grp, float (&pre)[RED_PARTS], int tid) {
   const int c = grp * 32 + (tid & 31), p8 = tid >> 5;
 #pragma unroll
   for (int j = 0; j < RED_PARTS; ++j) {
     const int p = p8 + 8 * j;
-    pre[j] = (c < SLAB && p < a.red_nparts) ? a.red_slab[(long)p * a.red_stride + c] : 0.f;
+    pre[j] = (c < SLAB && p < a.nparts) ? a.slab[(long)p * a.stride + c] : 0.f;
   }
 }
 
+// ---- persistent backward chain -------------------------------------------------------------
+// Layers L-1 .. 0 in one launch; tiles in DECREASING order (layer l's tile needs dx_{l+1} at
+// rows t + d_{l+1}, i.e. from the same or LATER tiles).  dx_{l+1}[t] = out_a[t] + out_c0[t+d']
+// (tmodel.py:122-127 autodiff): out_a never leaves the block (registers, acc layout = the B
+// operand of the next dz product); out_c0 stays in LDS for the block's own rows and only its
+// first min(d,128) rows are published (sc1) to the per-layer hand-off buffer for the tile
+// below.  The gate recompute runs before the hand-off wait and the weight-gradient products
+// after the publish, so the cross-tile critical path per layer is G-build → dz → dx.
+// Weight-gradient partials go to slab[l][tile] (summed by layer_reduce_all_kernel).
+struct ChainBK {
+  const float* X; long xls;
+  const float* DZ; long lddz;
+  const float* wpack;
+  float* slab;                 // [L][ntiles][SLAB]
+  float* ocg; long ocls;       // out_c0 hand-off rows: [L][B·T][32], layer stride ocls floats
+  float* dx0_a; float* dx0_c;  // layer 0's out_a / out_c0 [B·T][32]
+  const float* gc_tab; const int* ids; const float* cond; long ldcond;
+  unsigned* flags; unsigned* status;
+  int B, T, H, L, nbl, Cd;
+};
+
+constexpr int CB_LDS = 2 * LP * XS + WIMG + LP * DS + 2 * LP * XS;  // Xp Xc | IMG | DV | G | OC (131 KB)
+
+__global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
+  __shared__ __attribute__((aligned(16))) float sm[CB_LDS];
+  __shared__ int s_fail;
+  float* Xp = sm;
+  float* Xc = Xp + LP * XS;
+  float* Ws = Xc + LP * XS;
+  float* Rs = Ws + 64 * WS;
+  float* bs = Rs + 32 * XS;
+  float* DV = Ws + WIMG;
+  float* G = DV + LP * DS;
+  float* OC = G + LP * XS;
+  float* ZT = Ws;   // after dx
+  float* RED = Xp;  // after dSIG
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int pi = lane & 31, h = lane >> 5;
+  const int r = 32 * w + pi;
+  const int tps = (a.T + LP - 1) / LP, ntiles = a.B * tps;
+  const int oc_bytes = (int)std::min<long>(a.ocls * 4, 0x7fffffffL);
+  if (tid == 0) s_fail = 0;
+  for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
+    const int tile = ntiles - 1 - it;
+    const int b = tile / tps, tt = tile % tps, t0 = tt * LP;
+    const int t = t0 + r;
+    const bool valid = t < a.T;
+    const long mb = (long)b * a.T, m = mb + t;
+    const long sb = (long)b * (a.H + a.T) * 32;
+    __syncthreads();
+    stage_image(Ws, a.wpack + (long)(a.L - 1) * WIMG, tid);
+    floatx16 oa;  // out_a of layer l+1, own row
+#pragma unroll
+    for (int q = 0; q < 16; ++q) oa[q] = 0.f;
+    for (int l = a.L - 1; l >= 0; --l) {
+      const int d = 1 << (l % a.nbl);
+      const int dn = (l + 1 < a.L) ? 1 << ((l + 1) % a.nbl) : 0;
+      const float* xl = a.X + (long)l * a.xls + sb;
+      // 0. this layer's inputs (pre-launch data): x_l taps, dZ rows; next image prefetch
+      stage_rows(Xp, xl, t0, -d, a.T, a.H, 32, tid);
+      stage_rows(Xc, xl, t0, 0, a.T, a.H, 32, tid);
+      floatx16 dz;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        floatx4 v = {0.f, 0.f, 0.f, 0.f};
+        if (valid) v = *(const floatx4*)(a.DZ + m * a.lddz + (long)l * a.Cd + 8 * q + 4 * h);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dz[4 * q + j] = v[j];
+      }
+      floatx4 pf[IMG_PF];
+      if (l > 0) {
+        const floatx4* src = (const floatx4*)(a.wpack + (long)(l - 1) * WIMG);
+#pragma unroll
+        for (int i = 0; i < IMG_PF; ++i) {
+          const int e = tid + 256 * i;
+          if (e < WIMG / 4) pf[i] = src[e];
+        }
+      }
+      __syncthreads();
+      // 1. recompute the gate (no cross-tile dependency)
+      floatx16 acc_s, acc_g;
+      conv_init(bs, a, m, valid, h, acc_s, acc_g);
+      conv_half(Xc + r * XS, Ws + 32 * WS, pi, h, acc_s, acc_g);
+      conv_half(Xp + r * XS, Ws, pi, h, acc_s, acc_g);
+      floatx16 th, sg;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        th[q] = tanhf_(acc_s[q]);
+        sg[q] = sigmoidf_(acc_g[q]);
+      }
+      // 2. G = dx_{l+1} rows of this tile: out_c0_{l+1}[t + dn] (own LDS / published rows) + out_a
+      if (dn) {
+        const int ptt = tt + max(1, dn / LP);
+        if (ptt < tps) {
+          if (tid == 0 && !s_fail) {
+            if (!wait_flag_ge(a.flags + (long)b * tps + ptt, (unsigned)(a.L - l - 1), a.status, 2u)) s_fail = 1;
+          }
+          __syncthreads();
+        }
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)(l + 1) * a.ocls, (short)0, oc_bytes, BUF_DW3);
+        for (int e = tid; e < LP * 8; e += 256) {
+          const int row = e >> 3, c4 = (e & 7) * 4, sr = row + dn, ts = t0 + sr;
+          floatx4 v = {0.f, 0.f, 0.f, 0.f};
+          if (ts < a.T) {
+            if (sr < LP) v = *(const floatx4*)(OC + sr * XS + c4);
+            else v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
+          }
+          *(floatx4*)(G + row * XS + c4) = v;
+        }
+        __syncthreads();
+      } else {
+        for (int e = tid; e < LP * 8; e += 256) *(floatx4*)(G + (e >> 3) * XS + (e & 7) * 4) = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+      floatx16 gv;
+      {
+        float* grow = G + r * XS;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          floatx4 v = *(const floatx4*)(grow + 8 * q + 4 * h);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { v[j] += oa[4 * q + j]; gv[4 * q + j] = v[j]; }
+          *(floatx4*)(grow + 8 * q + 4 * h) = v;
+        }
+      }
+      // 3. dz += RES·g; dv
+      {
+        floatx4 rx[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rx[q] = *(const floatx4*)(Rs + pi * XS + 8 * q + 4 * h);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dz = mfma32(rx[q][j], gv[4 * q + j], dz);
+      }
+      floatx16 dvs, dvg;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        dvs[q] = dz[q] * sg[q] * (1.f - th[q] * th[q]);
+        dvg[q] = dz[q] * th[q] * sg[q] * (1.f - sg[q]);
+      }
+      {
+        float* dvrow = DV + r * DS;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          *(floatx4*)(dvrow + 8 * q + 4 * h) = floatx4{dvs[4 * q], dvs[4 * q + 1], dvs[4 * q + 2], dvs[4 * q + 3]};
+          *(floatx4*)(dvrow + 32 + 8 * q + 4 * h) = floatx4{dvg[4 * q], dvg[4 * q + 1], dvg[4 * q + 2], dvg[4 * q + 3]};
+        }
+      }
+      // 4. dx: out_a = g + W1·dv, out_c0 = W0·dv
+      floatx16 acc_a = gv, acc_c;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc_c[q] = 0.f;
+      {
+        floatx4 wv[2][4];
+        auto loadw = [&](int q, int buf) {
+          const int ko = 8 * q + 4 * h;
+          wv[buf][0] = *(const floatx4*)(Ws + pi * WS + ko);
+          wv[buf][1] = *(const floatx4*)(Ws + pi * WS + 32 + ko);
+          wv[buf][2] = *(const floatx4*)(Ws + (32 + pi) * WS + ko);
+          wv[buf][3] = *(const floatx4*)(Ws + (32 + pi) * WS + 32 + ko);
+        };
+        loadw(0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int cb = q & 1;
+          if (q + 1 < 4) loadw(q + 1, cb ^ 1);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int s2 = 4 * q + j;
+            acc_a = mfma32(wv[cb][2][j], dvs[s2], acc_a);
+            acc_c = mfma32(wv[cb][0][j], dvs[s2], acc_c);
+            acc_a = mfma32(wv[cb][3][j], dvg[s2], acc_a);
+            acc_c = mfma32(wv[cb][1][j], dvg[s2], acc_c);
+          }
+        }
+      }
+      {
+        float* ocrow = OC + r * XS;
+        const __amdgpu_buffer_rsrc_t rw =
+            __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)l * a.ocls, (short)0, oc_bytes, BUF_DW3);
+        const bool pub = l > 0 && valid && r < min(d, LP);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const floatx4 v = floatx4{acc_c[4 * q], acc_c[4 * q + 1], acc_c[4 * q + 2], acc_c[4 * q + 3]};
+          *(floatx4*)(ocrow + 8 * q + 4 * h) = v;
+          if (pub) __builtin_amdgcn_raw_buffer_store_b128(v, rw, (int)((m * 32 + 8 * q + 4 * h) * 4), 0, 16);
+        }
+      }
+      if (l == 0 && valid) {
+        store_rows16(a.dx0_a + m * 32, acc_a, 32, h);
+        store_rows16(a.dx0_c + m * 32, acc_c, 32, h);
+      }
+      oa = acc_a;
+      // publish out_c0_l (every wave drains its sc1 stores, barrier, one lane signals)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // also: DV complete, the weight image is dead
+      if (tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
+      // 5. weight gradients of layer l over this tile
+      {
+        float* zrow = ZT + r * XS;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          floatx4 zv;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) zv[j] = th[4 * q + j] * sg[4 * q + j];
+          *(floatx4*)(zrow + 8 * q + 4 * h) = zv;
+        }
+      }
+      floatx16 accW, accR;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) { accW[q] = 0.f; accR[q] = 0.f; }
+      {  // dSIG/dGATE tile w: A[i=in][k=pos] = X[pos][in], B[k][j=o] = DV[pos][o]
+        const float* X = (w & 1) ? Xc : Xp;
+        const int oc = (w >> 1) * 32 + pi;
+        float xa[2][8], da[2][8];
+        auto loadb = [&](int bt, int buf) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int p = 2 * (8 * bt + i) + h;
+            xa[buf][i] = X[p * XS + pi];
+            da[buf][i] = DV[p * DS + oc];
+          }
+        };
+        loadb(0, 0);
+#pragma unroll
+        for (int bt = 0; bt < LP / 16; ++bt) {
+          const int cb = bt & 1;
+          if (bt + 1 < LP / 16) loadb(bt + 1, cb ^ 1);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) accW = mfma32(xa[cb][i], da[cb][i], accW);
+        }
+      }
+      __syncthreads();  // ZT visible; Xp/Xc free for RED
+      {  // dRES part over this wave's 32 positions
+        float za[16], ga[16];
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) {
+          const int p = 32 * w + 2 * s2 + h;
+          za[s2] = ZT[p * XS + pi];
+          ga[s2] = G[p * XS + pi];
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) accR = mfma32(za[s2], ga[s2], accR);
+      }
+      float* slab = a.slab + ((long)l * ntiles + tile) * SLAB;
+      {  // bias partials: column sums of DV (64) and G (32)
+        float* part = RED + 4096;  // [8][96] after the dRES exchange area
+        if (tid < 128) {
+          const int c4 = (tid & 15) * 4, pc = tid >> 4;
+          floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int p = 0; p < 16; ++p) s4 += *(const floatx4*)(DV + (pc * 16 + p) * DS + c4);
+          *(floatx4*)(part + pc * 96 + c4) = s4;
+        } else if (tid < 192) {
+          const int c4 = ((tid - 128) & 7) * 4, pc = (tid - 128) >> 3;
+          floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int p = 0; p < 16; ++p) s4 += *(const floatx4*)(G + (pc * 16 + p) * XS + c4);
+          *(floatx4*)(part + pc * 96 + 64 + c4) = s4;
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          slab[w * 1024 + acc_row(q, h) * 32 + pi] = accW[q];
+          RED[w * 1024 + acc_row(q, h) * 32 + pi] = accR[q];
+        }
+        __syncthreads();
+        if (tid < 96) {
+          float s1 = 0.f;
+#pragma unroll
+          for (int pc = 0; pc < 8; ++pc) s1 += part[pc * 96 + tid];
+          slab[5120 + tid] = s1;
+        }
+        for (int e = tid; e < 1024; e += 256)
+          slab[4096 + e] = ((RED[e] + RED[1024 + e]) + RED[2048 + e]) + RED[3072 + e];
+      }
+      // 6. next layer's weight image (ZT is dead: every wave passed the barrier after dRES)
+      if (l > 0) {
+#pragma unroll
+        for (int i = 0; i < IMG_PF; ++i) {
+          const int e = tid + 256 * i;
+          if (e < WIMG / 4) *(floatx4*)(Ws + 4 * e) = pf[i];
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Sum every layer's slab partials: grid (column groups, L).
+__global__ __launch_bounds__(256) void layer_reduce_all_kernel(RedK a, long slab_layer, long dsig_l, long dres_l,
+                                                               long db_l) {
+  __shared__ float scratch[256];
+  float pre[RED_PARTS];
+  const int l = blockIdx.y;
+  RedK k = a;
+  k.slab = a.slab + l * slab_layer;
+  k.dsig = a.dsig + l * dsig_l;
+  k.dgate = a.dgate + l * dsig_l;
+  k.dres = a.dres + l * dres_l;
+  k.dbsig = a.dbsig ? a.dbsig + l * db_l : nullptr;
+  k.dbgate = a.dbgate ? a.dbgate + l * db_l : nullptr;
+  k.dbres = a.dbres ? a.dbres + l * (long)a.Cr : nullptr;
+  slab_group_prefetch(k, blockIdx.x, pre, threadIdx.x);
+  slab_group_finish(k, blockIdx.x, pre, scratch, threadIdx.x);
+}
+
 // ---- backward ----------------------------------------------------------------------------
+// LDS (112.5 KB, so that one GEMM block of the concurrent weight-gradient stream fits
+// beside it on the CU): Xp | Xc | G | IMG | DV.  After the dx step the weight image is dead
+// and holds zᵀ (ZT); RED (dRES cross-wave sum, bias partials) reuses Xp once step 5 is done.
+constexpr int BWD_LDS = 3 * LP * XS + WIMG + LP * DS;
+static_assert(LP * XS <= WIMG, "ZT must fit in the weight image");
+static_assert(4 * 1024 <= LP * XS, "RED must fit in Xp");
 
 __global__ __launch_bounds__(256) void layer_bwd_kernel(BwdK a) {
-  __shared__ __attribute__((aligned(16))) float sm[3 * LP * XS + WIMG + LP * DS + LP * XS + 4 * 1024];
+  __shared__ __attribute__((aligned(16))) float sm[BWD_LDS];
   float* Xp = sm;
   float* Xc = Xp + LP * XS;
   float* G = Xc + LP * XS;
   float* Ws = G + LP * XS;
   float* Rs = Ws + 64 * WS;
   float* bs = Rs + 32 * XS;
-  float* DV = bs + 96;               // [LP][DS]   dv (sig | gate), position-major
-  float* ZT = DV + LP * DS;          // [LP][XS]   z, position-major
-  float* RED = ZT + LP * XS;         // 4 × 1024
+  float* DV = Ws + WIMG;             // [LP][DS]   dv (sig | gate), position-major
+  float* ZT = Ws;                    // [LP][XS]   z, position-major (after step 4)
+  float* RED = Xp;                   // 4 × 1024 / [8][96] (after step 5)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int pi = lane & 31, h = lane >> 5;
   const int tps = (a.T + LP - 1) / LP, ntiles = a.B * tps;
-  const int ngroups = (SLAB + 31) / 32;
 
-  // deferred reduction of the deeper layer's partials: issue the loads now, sum at the end
-  float pre[RED_PARTS];
-  const bool red = !(LBWN_ABL & 1) && a.red_slab && (int)blockIdx.x < ngroups;
-  if (red) slab_group_prefetch(a, blockIdx.x, pre, tid);
-
-  stage_image(Ws, a.wpack, tid);
   floatx16 accW, accR;  // tile w of dSIG/dGATE (w: 0 sig·prev, 1 sig·cur, 2 gate·prev, 3 gate·cur), dRES part
 #pragma unroll
   for (int r = 0; r < 16; ++r) { accW[r] = 0.f; accR[r] = 0.f; }
@@ -357,7 +870,8 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(BwdK a) {
     const int b = tile / tps, t0 = (tile % tps) * LP;
     const long mb = (long)b * a.T;
     const float* xb = a.x_in + (long)b * (a.H + a.T) * a.Cr;
-    if (tile != (int)blockIdx.x) __syncthreads();
+    if (tile != (int)blockIdx.x) __syncthreads();  // previous tile's LDS reads done
+    stage_image(Ws, a.wpack, tid);
     stage_rows(Xp, xb, t0, -a.d, a.T, a.H, a.Cr, tid);
     stage_rows(Xc, xb, t0, 0, a.T, a.H, a.Cr, tid);
     stage_g(G, a.g_a, a.g_c0, a.g_d, mb, t0, a.T, a.Cr, tid);
@@ -411,21 +925,18 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(BwdK a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) dz = mfma32(rx[g][j], gx[g][j], dz);
     }
-    // 3. dvᵀ, parked position-major with z for the weight-grad products
-    floatx16 dvs, dvg, z;
+    // 3. dvᵀ, parked position-major for the weight-grad products
+    floatx16 dvs, dvg;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      z[r] = th[r] * sg[r];
       dvs[r] = dz[r] * sg[r] * (1.f - th[r] * th[r]);
       dvg[r] = dz[r] * th[r] * sg[r] * (1.f - sg[r]);
     }
     float* dvrow = DV + (32 * w + pi) * DS;
-    float* zrow = ZT + (32 * w + pi) * XS;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       *(floatx4*)(dvrow + 8 * q + 4 * h) = floatx4{dvs[4 * q], dvs[4 * q + 1], dvs[4 * q + 2], dvs[4 * q + 3]};
       *(floatx4*)(dvrow + 32 + 8 * q + 4 * h) = floatx4{dvg[4 * q], dvg[4 * q + 1], dvg[4 * q + 2], dvg[4 * q + 3]};
-      *(floatx4*)(zrow + 8 * q + 4 * h) = floatx4{z[4 * q], z[4 * q + 1], z[4 * q + 2], z[4 * q + 3]};
     }
     // 4. dx: dcurᵀ = W1·dvᵀ (+ g), dprevᵀ = W0·dvᵀ   (rows = in channel)
     floatx16 acc_a, acc_c;
@@ -464,7 +975,17 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(BwdK a) {
       store_rows16(a.out_c0 + m * a.Cr, acc_c, a.Cr, h);
     }
     if (LBWN_ABL & 16) asm volatile("" ::"v"(acc_a[0]), "v"(acc_c[0]), "v"(acc_a[15]), "v"(acc_c[15]));
-    __syncthreads();  // DV / ZT of every wave visible
+    __syncthreads();  // DV of every wave visible; nobody reads the weight image any more
+    {
+      float* zrow = ZT + (32 * w + pi) * XS;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        floatx4 zv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) zv[j] = th[4 * q + j] * sg[4 * q + j];
+        *(floatx4*)(zrow + 8 * q + 4 * h) = zv;
+      }
+    }
 
     // 5. dSIG/dGATE tile w over all LP positions: A[i=in][k=pos] = X[pos][in], B[k][j=o] = DV[pos][o]
     {
@@ -488,6 +1009,7 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(BwdK a) {
         for (int i = 0; i < 8; ++i) accW = mfma32(xa[cb][i], da[cb][i], accW);
       }
     }
+    __syncthreads();  // ZT visible; Xp/Xc free for RED
     // 6. dRES part over this wave's 32 positions: A[i=c][k=pos] = z[pos][c], B[k][j=o] = g[pos][o]
     {
       float za[16], ga[16];
@@ -556,6 +1078,7 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(BwdK a) {
   }
 
   // 8. block partial -> slab: tiles 0..3 straight from their wave, dRES summed over waves
+  __syncthreads();  // bias partial reads of RED done
   float* slab = a.slab + (long)blockIdx.x * a.slab_stride;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -565,18 +1088,9 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(BwdK a) {
   __syncthreads();
   for (int e = tid; e < 1024; e += 256) slab[4096 + e] = ((RED[e] + RED[1024 + e]) + RED[2048 + e]) + RED[3072 + e];
   if (tid < 96) slab[5120 + tid] = bsum;
-  // 9. finish the deferred reduction (remaining groups when the grid is small)
-  if (red) slab_group_finish(a, blockIdx.x, pre, RED, tid);
-  if (!(LBWN_ABL & 1) && a.red_slab) {
-    float none[RED_PARTS];
-    for (int grp = blockIdx.x + gridDim.x; grp < ngroups; grp += gridDim.x) {
-      slab_group_prefetch(a, grp, none, tid);
-      slab_group_finish(a, grp, none, RED, tid);
-    }
-  }
 }
 
-__global__ __launch_bounds__(256) void layer_reduce_kernel(BwdK a) {
+__global__ __launch_bounds__(256) void layer_reduce_kernel(RedK a) {
   __shared__ float scratch[256];
   float pre[RED_PARTS];
   const int ngroups = (SLAB + 31) / 32;
@@ -602,9 +1116,6 @@ BwdK to_bwd(const lbwn_layer_args& a) {
   k.out_a = a.out_a; k.out_c0 = a.out_c0; k.slab = a.slab; k.gc_tab = a.gc_tab; k.ids = a.ids; k.cond = a.cond;
   k.dv_out = a.dv_out; k.gc_dtab = a.gc_dtab; k.lddz = a.lddz; k.ldcond = a.ldcond; k.lddv = a.lddv;
   k.B = a.B; k.T = a.T; k.H = a.H; k.d = a.d; k.Cr = a.Cr; k.Cd = a.Cd; k.g_d = a.g_d; k.slab_stride = a.slab_stride;
-  k.red_slab = a.red_slab; k.red_dsig = a.red_dsig; k.red_dgate = a.red_dgate; k.red_dres = a.red_dres;
-  k.red_dbsig = a.red_dbsig; k.red_dbgate = a.red_dbgate; k.red_dbres = a.red_dbres;
-  k.red_nparts = a.red_nparts; k.red_stride = a.red_stride;
   return k;
 }
 
@@ -641,14 +1152,69 @@ int lbwn_layer_fwd_launch(const lbwn_layer_args& a, hipStream_t st) {
 int lbwn_layer_bwd_launch(const lbwn_layer_args& a, hipStream_t st) {
   if (int e = check_layer(a)) return e;
   LBWN_REQUIRE(a.slab && a.slab_stride >= SLAB, "layer bwd: slab missing");
-  LBWN_REQUIRE(!a.red_slab || a.red_nparts <= 8 * RED_PARTS || true, "unreachable");
   layer_bwd_kernel<<<grid_bwd(a), 256, 0, st>>>(to_bwd(a));
   LBWN_CHECK_LAUNCH();
   return 0;
 }
 
-int lbwn_layer_reduce_launch(const lbwn_layer_args& a, hipStream_t st) {
-  layer_reduce_kernel<<<(SLAB + 31) / 32, 256, 0, st>>>(to_bwd(a));
+int lbwn_layer_reduce_launch(const lbwn_layer_red_args& r, hipStream_t st) {
+  LBWN_REQUIRE(r.slab && r.nparts >= 1 && r.stride >= SLAB, "layer reduce: bad slab");
+  RedK k;
+  k.slab = r.slab; k.dsig = r.dsig; k.dgate = r.dgate; k.dres = r.dres;
+  k.dbsig = r.dbsig; k.dbgate = r.dbgate; k.dbres = r.dbres;
+  k.nparts = r.nparts; k.stride = r.stride; k.Cr = r.Cr; k.Cd = r.Cd;
+  layer_reduce_kernel<<<(SLAB + 31) / 32, 256, 0, st>>>(k);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
+
+int lbwn_chain_fwd_lds_bytes() { return CF_LDS * 4; }
+
+int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
+  LBWN_REQUIRE(c.Cr == 32 && c.Cd == 32, "chain fwd: n_res = n_dil = 32 only");
+  LBWN_REQUIRE(c.grid >= 1 && c.flags && c.status, "chain fwd: bad launch state");
+  LBWN_REQUIRE((((uintptr_t)c.X) & 15) == 0 && (c.xls & 3) == 0, "chain fwd: x not 16-B aligned");
+  ChainFK k;
+  k.X = c.X; k.xls = c.xls; k.Z = c.Z; k.ldz = c.ldz; k.wpack = c.wpack;
+  k.gc_tab = c.gc_tab; k.ids = c.ids; k.cond = nullptr; k.ldcond = 0;
+  k.flags = c.flags; k.status = c.status;
+  k.B = c.B; k.T = c.T; k.H = c.H; k.L = c.L; k.nbl = c.nbl; k.Cd = c.Cd;
+  const int tps = (c.T + LP - 1) / LP;
+  LBWN_REQUIRE((unsigned*)c.status + 4 == c.flags, "chain: status word must head the flag block");
+  LBWN_HIP(hipMemsetAsync(c.status, 0, (16 + (size_t)c.B * tps * 4 + 15) / 16 * 16, st));
+  chain_fwd_kernel<<<c.grid, 256, 0, st>>>(k);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
+  LBWN_REQUIRE(c.Cr == 32 && c.Cd == 32, "chain bwd: n_res = n_dil = 32 only");
+  LBWN_REQUIRE(c.grid >= 1 && c.flags && c.status && c.slab && c.ocg && c.dx0_a && c.dx0_c && c.DZ,
+               "chain bwd: bad launch state");
+  ChainBK k;
+  k.X = c.X; k.xls = c.xls; k.DZ = c.DZ; k.lddz = c.ldz; k.wpack = c.wpack; k.slab = c.slab;
+  k.ocg = c.ocg; k.ocls = c.ocls; k.dx0_a = c.dx0_a; k.dx0_c = c.dx0_c;
+  k.gc_tab = c.gc_tab; k.ids = c.ids; k.cond = nullptr; k.ldcond = 0;
+  k.flags = c.flags; k.status = c.status;
+  k.B = c.B; k.T = c.T; k.H = c.H; k.L = c.L; k.nbl = c.nbl; k.Cd = c.Cd;
+  const int tps = (c.T + LP - 1) / LP;
+  LBWN_REQUIRE((unsigned*)c.status + 4 == c.flags, "chain: status word must head the flag block");
+  LBWN_HIP(hipMemsetAsync(c.status, 0, (16 + (size_t)c.B * tps * 4 + 15) / 16 * 16, st));
+  chain_bwd_kernel<<<c.grid, 256, 0, st>>>(k);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_layer_reduce_all_launch(const lbwn_layer_red_args& r, int L, long slab_layer, hipStream_t st) {
+  LBWN_REQUIRE(r.slab && r.nparts >= 1 && r.stride >= SLAB && L >= 1, "layer reduce: bad slab");
+  RedK k;
+  k.slab = r.slab; k.dsig = r.dsig; k.dgate = r.dgate; k.dres = r.dres;
+  k.dbsig = r.dbsig; k.dbgate = r.dbgate; k.dbres = r.dbres;
+  k.nparts = r.nparts; k.stride = r.stride; k.Cr = r.Cr; k.Cd = r.Cd;
+  layer_reduce_all_kernel<<<dim3((SLAB + 31) / 32, L), 256, 0, st>>>(k, slab_layer, 2L * r.Cr * r.Cd,
+                                                                    (long)r.Cd * r.Cr, r.Cd);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_slab_floats() { return SLAB; }
