@@ -17,10 +17,13 @@
 struct lbwn_plan {
   lbwn_arch a;
   int B, T, L, nbl, H, Cr, Cd, Cs, Cp, Q;
+  int Ge, ncat1, Li, Lo, nup, hop, up[8];   // conditioning (Ge = 0: no GC, Lo = 0: no LC)
   long M;
   // workspace carving (byte offsets)
   size_t oX, oZ, oS, oR2, oLOG, oDH, oDS, oDZ, oGA[2], oGC0[2], oDX0, oSLAB, oSPLIT, oSPLIT2, oCOLS, oCOLS2,
       oHEADP, oBSUM, oWPK, oFLAGS, oSTATUS, oOCG;
+  size_t oGCTAB, oGCD, oLCACT[8], oCOND, oDVALL, oLCCAT, oDLCCAT, oDLC[2];
+  int split_dlc, split_up[8];
   size_t total;
   long x_layer_stride;  // floats
   int split_post2, split_post1, split_skip, split_pre;
@@ -107,7 +110,19 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   LBWN_REQUIRE(a->n_skip % 4 == 0 && a->n_post % 4 == 0 && a->n_quant % 4 == 0,
                "plan: n_skip/n_post/n_quant must be multiples of 4");
   LBWN_REQUIRE(B >= 1 && T >= 2, "plan: batch_sz >= 1 and slice_sz >= 2 required");
-  LBWN_REQUIRE(a->n_gc_embed == 0 && a->n_lc_out == 0, "plan: GC/LC conditioning not yet supported by this build");
+  LBWN_REQUIRE(a->n_res % 4 == 0 && a->n_dil % 4 == 0, "plan: n_res/n_dil must be multiples of 4");
+  LBWN_REQUIRE(a->n_gc_embed >= 0 && (a->n_gc_embed == 0 || a->n_gc_category >= 1),
+               "plan: GC needs n_gc_category >= 1");
+  int hop = 1;
+  if (a->n_lc_out > 0) {
+    LBWN_REQUIRE(a->n_lc_upsample >= 1 && a->n_lc_upsample <= 8, "plan: LC needs 1..8 upsample stages");
+    for (int i = 0; i < a->n_lc_upsample; ++i) {
+      LBWN_REQUIRE(a->lc_upsample[i] >= 1, "plan: bad lc_upsample stride");
+      hop *= a->lc_upsample[i];
+    }
+    LBWN_REQUIRE(T % hop == 0, "plan: slice_sz %d is not a multiple of the mel hop %d", T, hop);
+    LBWN_REQUIRE(a->n_lc_in % 4 == 0 && a->n_lc_out % 4 == 0, "plan: n_lc_in/n_lc_out must be multiples of 4");
+  }
   lbwn_plan* p = new (std::nothrow) lbwn_plan();
   LBWN_REQUIRE(p, "plan: out of host memory");
   p->a = *a;
@@ -122,6 +137,13 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->Cp = a->n_post;
   p->Q = a->n_quant;
   p->M = (long)B * T;
+  p->Ge = a->n_gc_embed;
+  p->ncat1 = a->n_gc_embed > 0 ? a->n_gc_category + 1 : 0;
+  p->Lo = a->n_lc_out;
+  p->Li = a->n_lc_in;
+  p->nup = a->n_lc_out > 0 ? a->n_lc_upsample : 0;
+  p->hop = hop;
+  for (int i = 0; i < 8; ++i) p->up[i] = i < p->nup ? a->lc_upsample[i] : 1;
   const long M = p->M;
   const int L = p->L;
   p->x_layer_stride = (long)B * (p->H + T) * p->Cr;
@@ -134,6 +156,17 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->split_pre = pick_split(p->Q, p->Cr, M);
   p->split_floats = std::max({(long)p->split_post2 * p->Cp * p->Q, (long)p->split_post1 * p->Cs * p->Cp,
                               (long)p->split_skip * ldz * p->Cs, (long)p->split_pre * p->Q * p->Cr});
+  if (p->Lo > 0) {
+    p->split_dlc = pick_split(p->Lo, 2 * L * p->Cd, M);
+    p->split_floats = std::max(p->split_floats, (long)p->split_dlc * p->Lo * 2 * L * p->Cd);
+    long rows = (long)B * (T / hop);
+    for (int i = 0; i < p->nup; ++i) {
+      const int I = i == 0 ? p->Li : p->Lo;
+      p->split_up[i] = pick_split(p->up[i] * p->Lo, I, rows);
+      p->split_floats = std::max(p->split_floats, (long)p->split_up[i] * p->up[i] * p->Lo * I);
+      rows *= p->up[i];
+    }
+  }
   const int nblk = lbwn_layer_bwd_grid(B, T);
   p->nblk = nblk;
   size_t cur = 0;
@@ -162,6 +195,25 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   const char* nc = getenv("LBWN_NO_CHAIN");
   p->chain = p->Cr == 32 && p->Cd == 32 && !(nc && nc[0] == '1');
   p->oOCG = p->chain ? carve(cur, sizeof(float) * (size_t)L * M * 32) : 0;
+  {  // conditioning
+    const size_t f = sizeof(float);
+    const long ncond = 2L * L * p->Cd;
+    p->oGCTAB = p->Ge ? carve(cur, f * (size_t)L * p->ncat1 * 2 * p->Cd) : 0;
+    p->oGCD = p->Ge ? carve(cur, f * (size_t)L * p->ncat1 * 2 * p->Cd) : 0;
+    long rows = (long)B * (T / hop);
+    for (int i = 0; i < 8; ++i) {
+      p->oLCACT[i] = 0;
+      if (i < p->nup) {
+        rows *= p->up[i];
+        p->oLCACT[i] = carve(cur, f * (size_t)rows * p->Lo);
+      }
+    }
+    p->oCOND = p->Lo ? carve(cur, f * (size_t)M * ncond) : 0;
+    p->oDVALL = p->Lo ? carve(cur, f * (size_t)M * ncond) : 0;
+    p->oLCCAT = p->Lo ? carve(cur, f * (size_t)p->Lo * ncond) : 0;
+    p->oDLCCAT = p->Lo ? carve(cur, f * (size_t)p->Lo * ncond) : 0;
+    for (int i = 0; i < 2; ++i) p->oDLC[i] = p->Lo ? carve(cur, f * (size_t)M * std::max(p->Lo, p->Li)) : 0;
+  }
   p->oHEADP = carve(cur, sizeof(float) * 3 * 2048);
   p->oBSUM = carve(cur, sizeof(float) * (size_t)p->Cs);
   p->oWPK = carve(cur, sizeof(float) * (size_t)L * lbwn_layer_image_floats());
@@ -227,13 +279,127 @@ lbwn_layer_args layer_base(const lbwn_plan* p, const lbwn_params* P, const float
 
 }  // namespace
 
+namespace {
+
+// Conditioning operands of the layer stack (tmodel.py:105-114, :150-160)
+struct Cond {
+  const float* gc_tab = nullptr; long gc_ls = 0;   // GCTAB [L][ncat+1][2Cd]
+  const float* cond = nullptr; long ldcond = 0;     // COND [M][L·2Cd]
+  float* gc_dtab = nullptr;                         // backward: GCD
+  float* dv_out = nullptr;                          // backward: DVALL
+  void apply(lbwn_layer_args& a, int l) const {
+    a.gc_tab = gc_tab ? gc_tab + l * gc_ls : nullptr;
+    a.gc_dtab = gc_dtab ? gc_dtab + l * gc_ls : nullptr;
+    a.cond = cond ? cond + (long)l * 2 * a.Cd : nullptr;
+    a.ldcond = ldcond;
+    a.dv_out = dv_out ? dv_out + (long)l * 2 * a.Cd : nullptr;
+    a.lddv = ldcond;
+  }
+};
+
+// GC table and the LC term: upsample (4× conv1d_transpose k = s, tmodel.py:68-83, each a GEMM
+// against the [s][O][I] filter read as k-contiguous), then COND = lc·LCcat.
+int cond_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const float* mel, Cond& c, hipStream_t st) {
+  int e;
+  const int L = p->L, Cd = p->Cd;
+  if (p->Ge > 0) {
+    float* tab = at<float>(ws, p->oGCTAB);
+    if ((e = lbwn_gc_table_launch(P->gc_embed, P->gc_sig, P->gc_gate, tab, L, p->ncat1, p->Ge, Cd, st))) return e;
+    c.gc_tab = tab;
+    c.gc_ls = (long)p->ncat1 * 2 * Cd;
+  }
+  if (p->Lo > 0) {
+    const float* in = mel;
+    long rows = (long)p->B * (p->T / p->hop);
+    int I = p->Li;
+    for (int i = 0; i < p->nup; ++i) {
+      const int s = p->up[i];
+      float* out = at<float>(ws, p->oLCACT[i]);
+      lbwn_gemm_args g = gemm0();
+      g.A = in; g.lda = I; g.B = P->lc_up[i]; g.ldb = I; g.C = out; g.ldc = (long)s * p->Lo;
+      g.M = (int)rows; g.N = s * p->Lo; g.K = I;
+      if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
+      in = out;
+      rows *= s;
+      I = p->Lo;
+    }
+    const long ncond = 2L * L * Cd;
+    float* cat = at<float>(ws, p->oLCCAT);
+    if ((e = lbwn_lc_pack_launch(cat, P->lc_sig, P->lc_gate, L, p->Lo, Cd, 1, st))) return e;
+    lbwn_gemm_args g = gemm0();
+    g.A = in; g.lda = p->Lo; g.B = cat; g.ldb = ncond; g.C = at<float>(ws, p->oCOND); g.ldc = ncond;
+    g.M = (int)p->M; g.N = (int)ncond; g.K = p->Lo;
+    Probe(p, st, "lc_cond");
+    if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
+    Probe::end(p, st, "lc_cond");
+    c.cond = at<float>(ws, p->oCOND);
+    c.ldcond = ncond;
+  }
+  return 0;
+}
+
+// After the layer stack: GC weight/table grads from GCD; LC grads from DVALL through
+// LCcat and the upsample stages (reverse), each a (split-K) GEMM.
+int cond_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G, void* ws, const float* mel,
+                  hipStream_t st) {
+  int e;
+  const int L = p->L, Cd = p->Cd;
+  float* SPL = at<float>(ws, p->oSPLIT);
+  if (p->Ge > 0) {
+    if ((e = lbwn_gc_grad_launch(P->gc_embed, P->gc_sig, P->gc_gate, at<float>(ws, p->oGCD), G->gc_embed, G->gc_sig,
+                                 G->gc_gate, L, p->ncat1, p->Ge, Cd, st)))
+      return e;
+  }
+  if (p->Lo > 0) {
+    const long ncond = 2L * L * Cd;
+    const float* lc = at<float>(ws, p->oLCACT[p->nup - 1]);
+    float* dv = at<float>(ws, p->oDVALL);
+    // dLCcat = lcᵀ·DV  -> LC_SIGNAL_l / LC_GATE_l grads
+    lbwn_gemm_args g = gemm0();
+    g.A = lc; g.lda = p->Lo; g.B = dv; g.ldb = ncond; g.C = at<float>(ws, p->oDLCCAT); g.ldc = ncond;
+    g.M = p->Lo; g.N = (int)ncond; g.K = (int)p->M;
+    if ((e = lbwn_gemm_launch(g, 0, 0, p->split_dlc, SPL, st))) return e;
+    if ((e = lbwn_lc_pack_launch(at<float>(ws, p->oDLCCAT), G->lc_sig, G->lc_gate, L, p->Lo, Cd, 0, st))) return e;
+    // dlc = DV·LCcatᵀ
+    float* dout = at<float>(ws, p->oDLC[0]);
+    g = gemm0();
+    g.A = dv; g.lda = ncond; g.B = at<float>(ws, p->oLCCAT); g.ldb = ncond; g.C = dout; g.ldc = p->Lo;
+    g.M = (int)p->M; g.N = p->Lo; g.K = (int)ncond;
+    if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
+    // upsample stages in reverse
+    long rows = p->M;
+    int buf = 0;
+    for (int i = p->nup - 1; i >= 0; --i) {
+      const int s = p->up[i], I = i == 0 ? p->Li : p->Lo;
+      rows /= s;  // stage input rows
+      const float* in = i == 0 ? mel : at<float>(ws, p->oLCACT[i - 1]);
+      // dF_i[(j,o)][i'] = Σ_bt dout[bt][(j,o)] · in[bt][i']
+      g = gemm0();
+      g.A = dout; g.lda = (long)s * p->Lo; g.B = in; g.ldb = I; g.C = G->lc_up[i]; g.ldc = I;
+      g.M = s * p->Lo; g.N = I; g.K = (int)rows;
+      if ((e = lbwn_gemm_launch(g, 0, 0, p->split_up[i], SPL, st))) return e;
+      if (i == 0) break;  // no gradient into the mel input
+      float* din = at<float>(ws, p->oDLC[buf ^ 1]);
+      g = gemm0();
+      g.A = dout; g.lda = (long)s * p->Lo; g.B = P->lc_up[i]; g.ldb = I; g.C = din; g.ldc = I;
+      g.M = (int)rows; g.N = I; g.K = s * p->Lo;
+      if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
+      dout = din;
+      buf ^= 1;
+    }
+  }
+  return 0;
+}
+
+}  // namespace
+
 int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* wav_q, const int* ids,
                        const float* mel, float* save, float* stats, void* stream) {
   LBWN_REQUIRE(p && P && ws && wav_q && ids && save && stats, "train_forward: null argument");
-  (void)mel;
   hipStream_t st = (hipStream_t)stream;
   int e;
   if ((e = ensure_device(p))) return e;
+  LBWN_REQUIRE(p->Lo == 0 || mel, "train_forward: LC arch needs the mel input");
   const int L = p->L, B = p->B, T = p->T, H = p->H, Cr = p->Cr, Cd = p->Cd;
   const long M = p->M, ldz = (long)L * Cd;
   float* X = at<float>(ws, p->oX);
@@ -248,6 +414,8 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     return e;
   // one-hot·PRE + PRE_BIAS == row gather (tmodel.py:53-66, :86-102)
   if ((e = lbwn_embed_launch(wav_q, P->pre, P->pre_b, X, B, T, H, Cr, p->Q, st))) return e;
+  Cond cd;
+  if ((e = cond_forward(p, P, ws, mel, cd, st))) return e;
   // D-separation prepend for every layer (tmodel.py:122-127)
   if ((e = lbwn_dsep_prepend_launch(X, p->x_layer_stride, save, L, p->nbl, B, T, H, Cr, st))) return e;
   if (p->chain) {
@@ -255,6 +423,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     lbwn_chain_args c;
     memset(&c, 0, sizeof(c));
     c.X = X; c.xls = p->x_layer_stride; c.Z = Z; c.ldz = ldz; c.wpack = WPK; c.ids = ids;
+    c.gc_tab = cd.gc_tab; c.gc_ls = cd.gc_ls; c.cond = cd.cond; c.ldcond = cd.ldcond;
     c.flags = at<unsigned>(ws, p->oFLAGS); c.status = at<unsigned>(ws, p->oSTATUS);
     c.B = B; c.T = T; c.H = H; c.L = L; c.nbl = p->nbl; c.Cr = Cr; c.Cd = Cd; c.grid = p->chain_grid;
     Probe(p, st, "layer_fwd");
@@ -263,6 +432,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   } else {
     for (int l = 0; l < L; ++l) {
       lbwn_layer_args a = layer_base(p, P, WPK, ids, l);
+      cd.apply(a, l);
       a.x_in = X + l * p->x_layer_stride;
       a.x_out = (l + 1 < L) ? X + (l + 1) * p->x_layer_stride : nullptr;
       a.z = Z + (long)l * Cd;
@@ -315,7 +485,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
 int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G, void* ws, const int* wav_q,
                         const int* ids, const float* mel, void* stream) {
   LBWN_REQUIRE(p && P && G && ws && wav_q && ids, "train_backward: null argument");
-  (void)mel;
+  LBWN_REQUIRE(p->Lo == 0 || mel, "train_backward: LC arch needs the mel input");
   hipStream_t st = (hipStream_t)stream;
   int e;
   if ((e = ensure_device(p))) return e;
@@ -377,7 +547,19 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   Probe(p, st, "dz");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
   Probe::end(p, st, "dz");
-  // residual stack in reverse
+  // residual stack in reverse (conditioning recomputed from the forward's GCTAB / COND)
+  Cond cd;
+  if (p->Ge > 0) {
+    cd.gc_tab = at<float>(ws, p->oGCTAB);
+    cd.gc_ls = (long)p->ncat1 * 2 * Cd;
+    cd.gc_dtab = at<float>(ws, p->oGCD);
+    LBWN_HIP(hipMemsetAsync(cd.gc_dtab, 0, sizeof(float) * (size_t)L * p->ncat1 * 2 * Cd, st));
+  }
+  if (p->Lo > 0) {
+    cd.cond = at<float>(ws, p->oCOND);
+    cd.ldcond = 2L * L * Cd;
+    cd.dv_out = at<float>(ws, p->oDVALL);
+  }
   const float* WPK = at<float>(ws, p->oWPK);
   const int sstr = lbwn_layer_slab_stride();
   float* SLABS = at<float>(ws, p->oSLAB);
@@ -387,6 +569,8 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     memset(&c, 0, sizeof(c));
     c.X = X; c.xls = p->x_layer_stride; c.DZ = DZ; c.ldz = ldz; c.wpack = WPK; c.ids = ids;
     c.slab = SLABS; c.ocg = at<float>(ws, p->oOCG); c.ocls = M * 32;
+    c.gc_tab = cd.gc_tab; c.gc_ls = cd.gc_ls; c.cond = cd.cond; c.ldcond = cd.ldcond;
+    c.gc_dtab = cd.gc_dtab; c.dv_out = cd.dv_out; c.lddv = cd.ldcond;
     c.dx0_a = at<float>(ws, p->oGA[0]); c.dx0_c = at<float>(ws, p->oGC0[0]);
     c.flags = at<unsigned>(ws, p->oFLAGS); c.status = at<unsigned>(ws, p->oSTATUS);
     c.B = B; c.T = T; c.H = p->H; c.L = L; c.nbl = p->nbl; c.Cr = Cr; c.Cd = Cd; c.grid = p->chain_grid;
@@ -403,6 +587,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   } else {
       for (int l = L - 1; l >= 0; --l) {
       lbwn_layer_args a = layer_base(p, P, WPK, ids, l);
+      cd.apply(a, l);
       a.x_in = X + l * p->x_layer_stride;
       a.dz_skip = DZ + (long)l * Cd;
       a.lddz = ldz;
@@ -425,6 +610,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     r.dbsig = G->sig_b; r.dbgate = G->gate_b; r.dbres = G->res_b;
     if ((e = lbwn_layer_reduce_all_launch(r, L, (long)p->nblk * sstr, st))) return e;
   }
+  if ((e = cond_backward(p, P, G, ws, mel, st))) return e;
   // dx_0 = (g + dcur) + shift(dprev); dPRE = onehot(q)ᵀ·dx_0, dPRE_BIAS = Σ dx_0
   float* DX0 = at<float>(ws, p->oDX0);
   if ((e = lbwn_shift_add_launch(DX0, at<float>(ws, p->oGA[0]), at<float>(ws, p->oGC0[0]), 1, B, T, Cr, st)))

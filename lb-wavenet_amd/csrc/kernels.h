@@ -65,7 +65,9 @@ struct lbwn_chain_args {
   float* X; long xls;          // x_l buffers of all layers, layer stride in floats
   float* Z; long ldz;
   const float* wpack;
-  const float* gc_tab; const int* ids;
+  const float* gc_tab; long gc_ls; const int* ids;   // GC table [L][ncat+1][2Cd] or null
+  const float* cond; long ldcond;                     // LC term [M][L·2Cd] or null
+  float* dv_out; long lddv; float* gc_dtab;           // backward: LC dv export, GC grad table
   unsigned* flags;             // [B·ceil(T/128)] (zeroed by the launcher)
   unsigned* status;            // sticky error word (spin timeout)
   int B, T, H, L, nbl, Cr, Cd;
@@ -120,3 +122,10 @@ int lbwn_head_nblocks(long M);
 int lbwn_mulaw_encode_launch(const float* x, int* q, long n, int n_quanta, int tf32, hipStream_t st);
 int lbwn_mulaw_decode_launch(const int* q, float* x, long n, int n_quanta, hipStream_t st);
 int lbwn_bcast_rows_launch(float* dst, int L, int N, hipStream_t st);
+
+// Conditioning (cond.hip)
+int lbwn_gc_table_launch(const float* emb, const float* wsig, const float* wgate, float* out, int L, int ncat1,
+                         int Ge, int Cd, hipStream_t st);
+int lbwn_gc_grad_launch(const float* emb, const float* wsig, const float* wgate, const float* gcd, float* demb,
+                        float* dsig, float* dgate, int L, int ncat1, int Ge, int Cd, hipStream_t st);
+int lbwn_lc_pack_launch(float* cat, float* wsig, float* wgate, int L, int Clc, int Cd, int pack, hipStream_t st);

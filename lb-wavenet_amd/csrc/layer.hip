@@ -294,10 +294,21 @@ struct ChainFK {
   float* X; long xls;        // x_l for all layers: layer stride (floats); each [B][H+T][32]
   float* Z; long ldz;
   const float* wpack;        // L packed images
-  const float* gc_tab; const int* ids; const float* cond; long ldcond;  // (conv_init)
+  const float* gc_tab; long gc_ls;              // GC table [L][ncat+1][2Cd] (layer stride gc_ls) or null
+  const int* ids; const float* cond; long ldcond; // LC term COND [M][L·2Cd] (layer l at column l·2Cd) or null
   unsigned* flags; unsigned* status;
   int B, T, H, L, nbl, Cd;
 };
+
+// conditioning operands of one layer, in the shape conv_init reads
+struct CondRef {
+  const float* gc_tab; const int* ids; const float* cond; long ldcond; int Cd;
+};
+template <typename K>
+LBWN_DEV CondRef cond_of(const K& a, int l) {
+  return CondRef{a.gc_tab ? a.gc_tab + (long)l * a.gc_ls : nullptr, a.ids,
+                 a.cond ? a.cond + (long)l * 2 * a.Cd : nullptr, a.ldcond, a.Cd};
+}
 
 LBWN_DEV bool wait_flag_ge(unsigned* f, unsigned want, unsigned* status, unsigned code) {
   const long long t0 = wall_clock64();
@@ -408,7 +419,7 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
       }
       // 2. own tap first: W1·x[t]
       floatx16 acc_s, acc_g;
-      conv_init(bs, a, m, valid, h, acc_s, acc_g);
+      conv_init(bs, cond_of(a, l), m, valid, h, acc_s, acc_g);
       conv_half(cur + r * XS, Ws + 32 * WS, pi, h, acc_s, acc_g);
       // 3. wait for the producer of the halo rows (x_l is layer l-1's output)
       const int ptt = tt - max(1, d / LP);
@@ -547,10 +558,35 @@ struct ChainBK {
   float* slab;                 // [L][ntiles][SLAB]
   float* ocg; long ocls;       // out_c0 hand-off rows: [L][B·T][32], layer stride ocls floats
   float* dx0_a; float* dx0_c;  // layer 0's out_a / out_c0 [B·T][32]
-  const float* gc_tab; const int* ids; const float* cond; long ldcond;
+  const float* gc_tab; long gc_ls; const int* ids; const float* cond; long ldcond;
+  float* dv_out; long lddv;    // dv export for the LC gradients: [M][L·2Cd] (layer l at column l·2Cd) or null
+  float* gc_dtab;              // GC gradient table [L][ncat+1][2Cd] (layer stride gc_ls), atomics, or null
   unsigned* flags; unsigned* status;
   int B, T, H, L, nbl, Cd;
 };
+
+// dv rows of wave w's 32 positions (DV, position-major) scatter-added into the GC gradient
+// table row of each position's voice id (fast path: one id for the whole wave).
+LBWN_DEV void gc_scatter(float* gtab, const int* ids_b, const float* DV, int t0, int T, int w, int lane, int Cd) {
+  const int tw0 = t0 + 32 * w;
+  const int nv = min(32, T - tw0);
+  if (nv <= 0) return;
+  const int* idw = ids_b + tw0;
+  const int id0 = idw[0];
+  bool uni = true;
+  for (int p = 1; p < nv; ++p) uni &= (idw[p] == id0);
+  const int o = lane, oc = o & 31;
+  const float* dvw = DV + 32 * w * DS;
+  if (oc >= Cd) return;
+  const int col = o < 32 ? oc : Cd + oc;
+  if (uni) {
+    float s = 0.f;
+    for (int p = 0; p < nv; ++p) s += dvw[p * DS + o];
+    atomicAdd(gtab + (long)id0 * 2 * Cd + col, s);
+  } else {
+    for (int p = 0; p < nv; ++p) atomicAdd(gtab + (long)idw[p] * 2 * Cd + col, dvw[p * DS + o]);
+  }
+}
 
 constexpr int CB_LDS = 2 * LP * XS + WIMG + LP * DS + 2 * LP * XS;  // Xp Xc | IMG | DV | G | OC (131 KB)
 
@@ -612,7 +648,7 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
       __syncthreads();
       // 1. recompute the gate (no cross-tile dependency)
       floatx16 acc_s, acc_g;
-      conv_init(bs, a, m, valid, h, acc_s, acc_g);
+      conv_init(bs, cond_of(a, l), m, valid, h, acc_s, acc_g);
       conv_half(Xc + r * XS, Ws + 32 * WS, pi, h, acc_s, acc_g);
       conv_half(Xp + r * XS, Ws, pi, h, acc_s, acc_g);
       floatx16 th, sg;
@@ -674,10 +710,17 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
       }
       {
         float* dvrow = DV + r * DS;
+        float* dvo = (a.dv_out && valid) ? a.dv_out + m * a.lddv + (long)l * 64 : nullptr;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          *(floatx4*)(dvrow + 8 * q + 4 * h) = floatx4{dvs[4 * q], dvs[4 * q + 1], dvs[4 * q + 2], dvs[4 * q + 3]};
-          *(floatx4*)(dvrow + 32 + 8 * q + 4 * h) = floatx4{dvg[4 * q], dvg[4 * q + 1], dvg[4 * q + 2], dvg[4 * q + 3]};
+          const floatx4 vs = floatx4{dvs[4 * q], dvs[4 * q + 1], dvs[4 * q + 2], dvs[4 * q + 3]};
+          const floatx4 vg = floatx4{dvg[4 * q], dvg[4 * q + 1], dvg[4 * q + 2], dvg[4 * q + 3]};
+          *(floatx4*)(dvrow + 8 * q + 4 * h) = vs;
+          *(floatx4*)(dvrow + 32 + 8 * q + 4 * h) = vg;
+          if (dvo) {
+            *(floatx4*)(dvo + 8 * q + 4 * h) = vs;
+            *(floatx4*)(dvo + 32 + 8 * q + 4 * h) = vg;
+          }
         }
       }
       // 4. dx: out_a = g + W1·dv, out_c0 = W0·dv
@@ -729,6 +772,7 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // also: DV complete, the weight image is dead
       if (tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
+      if (a.gc_dtab) gc_scatter(a.gc_dtab + (long)l * a.gc_ls, a.ids + mb, DV, t0, a.T, w, lane, 32);
       // 5. weight gradients of layer l over this tile
       {
         float* zrow = ZT + r * XS;
@@ -1053,28 +1097,7 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(BwdK a) {
         if (tt < a.T && oc < a.Cd) a.dv_out[(mb + tt) * a.lddv + (o < 32 ? oc : a.Cd + oc)] = DV[p * DS + o];
       }
     }
-    if (a.gc_dtab) {
-      const int tw0 = t0 + 32 * w;
-      const int nv = min(32, a.T - tw0);
-      if (nv > 0) {
-        const int* idw = a.ids + mb + tw0;
-        const int id0 = idw[0];
-        bool uni = true;
-        for (int p = 1; p < nv; ++p) uni &= (idw[p] == id0);
-        const int o = lane, oc = o & 31;
-        const float* dvw = DV + 32 * w * DS;
-        if (oc < a.Cd) {
-          const int col = o < 32 ? oc : a.Cd + oc;
-          if (uni) {
-            float s = 0.f;
-            for (int p = 0; p < nv; ++p) s += dvw[p * DS + o];
-            atomicAdd(a.gc_dtab + (long)id0 * 2 * a.Cd + col, s);
-          } else {
-            for (int p = 0; p < nv; ++p) atomicAdd(a.gc_dtab + (long)idw[p] * 2 * a.Cd + col, dvw[p * DS + o]);
-          }
-        }
-      }
-    }
+    if (a.gc_dtab) gc_scatter(a.gc_dtab, a.ids + mb, DV, t0, a.T, w, lane, a.Cd);
   }
 
   // 8. block partial -> slab: tiles 0..3 straight from their wave, dRES summed over waves
@@ -1176,7 +1199,7 @@ int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   LBWN_REQUIRE((((uintptr_t)c.X) & 15) == 0 && (c.xls & 3) == 0, "chain fwd: x not 16-B aligned");
   ChainFK k;
   k.X = c.X; k.xls = c.xls; k.Z = c.Z; k.ldz = c.ldz; k.wpack = c.wpack;
-  k.gc_tab = c.gc_tab; k.ids = c.ids; k.cond = nullptr; k.ldcond = 0;
+  k.gc_tab = c.gc_tab; k.gc_ls = c.gc_ls; k.ids = c.ids; k.cond = c.cond; k.ldcond = c.ldcond;
   k.flags = c.flags; k.status = c.status;
   k.B = c.B; k.T = c.T; k.H = c.H; k.L = c.L; k.nbl = c.nbl; k.Cd = c.Cd;
   const int tps = (c.T + LP - 1) / LP;
@@ -1194,7 +1217,8 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   ChainBK k;
   k.X = c.X; k.xls = c.xls; k.DZ = c.DZ; k.lddz = c.ldz; k.wpack = c.wpack; k.slab = c.slab;
   k.ocg = c.ocg; k.ocls = c.ocls; k.dx0_a = c.dx0_a; k.dx0_c = c.dx0_c;
-  k.gc_tab = c.gc_tab; k.ids = c.ids; k.cond = nullptr; k.ldcond = 0;
+  k.gc_tab = c.gc_tab; k.gc_ls = c.gc_ls; k.ids = c.ids; k.cond = c.cond; k.ldcond = c.ldcond;
+  k.dv_out = c.dv_out; k.lddv = c.lddv; k.gc_dtab = c.gc_dtab;
   k.flags = c.flags; k.status = c.status;
   k.B = c.B; k.T = c.T; k.H = c.H; k.L = c.L; k.nbl = c.nbl; k.Cd = c.Cd;
   const int tps = (c.T + LP - 1) / LP;

@@ -179,10 +179,9 @@ class ParamLayout:
             for i, s in enumerate(arch['lc_upsample']):
                 add('LC_UPSAMPLE_%d' % i, [s, Lo, Li if i == 0 else Lo], False, ArchCat.LC_UPSAMPLE,
                     'lc_up%d' % i)
-            # LC_SIGNAL_l / LC_GATE_l interleaved per layer: one [L][2][Clc][Cd] block
-            for l, b, bl, d in layers:
-                add('LC_SIGNAL' + sfx(b, bl), [Lo, Cd], False, ArchCat.LC_SIGNAL, 'lc_sig')
-                add('LC_GATE' + sfx(b, bl), [Lo, Cd], False, ArchCat.LC_GATE, 'lc_gate')
+            for kind, cat in (('lc_sig', ArchCat.LC_SIGNAL), ('lc_gate', ArchCat.LC_GATE)):
+                for l, b, bl, d in layers:
+                    add(cat.name + sfx(b, bl), [Lo, Cd], False, cat, kind)
         add('POST1', [Cs, Cp], False, ArchCat.POST1, 'post1')
         add('POST2', [Cp, Q], False, ArchCat.POST2, 'post2')
         self.n_weights = self._cur

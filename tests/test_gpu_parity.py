@@ -265,6 +265,51 @@ def test_chain_matches_per_layer(monkeypatch, B, T, nbl):
         close(g.cpu().double().numpy(), out['layers']['grads'][n].cpu().double().numpy(), 5e-3, n)
 
 
+def cond_arch(gc, lc, C=32):
+    a = dict(n_blocks=1, n_block_layers=4, n_quant=256, n_res=C, n_dil=C, n_skip=64, n_post=32,
+             n_gc_embed=8 if gc else 0, n_gc_category=5 if gc else 0, use_bias=True)
+    if lc:
+        a.update(n_lc_in=12, n_lc_out=16, lc_upsample=[2, 4])
+    return normalize_arch(a)
+
+
+@pytest.mark.parametrize('gc,lc,C', [(1, 0, 32), (0, 1, 32), (1, 1, 32), (1, 1, 16)])
+def test_plan_conditioning(gc, lc, C):
+    """GC (tmodel.py:92-114, :150-154) and LC (tmodel.py:68-83, :155-160) through the plan:
+    forward (SAVE, loss) and every gradient against the oracle.  C = 32 runs the persistent
+    chain kernels, C = 16 the per-layer kernels."""
+    arch = cond_arch(gc, lc, C)
+    B, T = 2, 256
+    net = make_net(arch, B)
+    q, ids = rand_batch(arch, B, T)
+    rng = np.random.default_rng(3)
+    if gc:   # voice ids change at "file" boundaries; 0 = masked
+        for b in range(B):
+            cuts = np.sort(rng.choice(np.arange(40, T), 3, replace=False))
+            v = rng.integers(1, arch['n_gc_category'] + 1, 4)
+            ids[b] = np.repeat(v, np.diff(np.r_[0, cuts, T]))
+            ids[b, cuts[1]:cuts[1] + 20] = 0
+    mel = rng.standard_normal((B, T // 8, arch['n_lc_in'])).astype(np.float32) if lc else None
+    P, S = oracle_params(net)
+    lg, cache, new_save = R.forward(arch, P, q, ids, S, mel=mel)
+    st, dlog = R.loss_fcn(arch, P, lg, q, ids, 0.0)
+    net.forward(q, mel, ids, backward=True)
+    torch.cuda.synchronize()
+    assert int(net.plan_tensor(T, 'status').view(torch.int32)[0]) == 0
+    stats = net.stats.cpu().numpy()
+    assert int(stats[1]) == st['n_valid']
+    np.testing.assert_allclose(stats[0] / st['n_valid'], st['mean_xent'], rtol=1e-5)
+    for k, v in new_save.items():
+        close(net.save_vars[k].cpu().numpy(), v, 1e-5, k)
+    G = R.backward(arch, P, cache, dlog, 0.0)
+    inv = 1.0 / st['n_valid']
+    names = net.layout.names()
+    assert any(n.startswith('GC_') for n in names) == bool(gc)
+    assert any(n.startswith('LC_') for n in names) == bool(lc)
+    for name in names:
+        close(net.grads[name].cpu().double().numpy() * inv, G[name], 2e-4, name)
+
+
 def test_staged_equals_unstaged_bitwise():
     """README.md:6-21: processing a stream in stages with the saved D-separation state is
     the same function as one long slice.  Position-wise kernels make it bit-exact."""
