@@ -1,9 +1,9 @@
 // Global / local conditioning (tmodel.py:68-83, :92-114, :150-160).
 //
 // GC: the per-layer term GC_EMBED[ids]·GC_k_l depends on the position only through its
-// voice id, so it is a lookup in a per-step table GCTAB[l][c][sig Cd | gate Cd] =
+// voice id, so it is a lookup in a per-step table GCTAB[c][l][sig Cd | gate Cd] =
 // GC_EMBED[c]·[GC_SIGNAL_l | GC_GATE_l]; the layer kernels add row ids[m].  Backward: the
-// layer kernels scatter-add dv rows into GCD[l][c][2Cd] (per voice id), and
+// layer kernels scatter-add dv rows into GCD[c][l][2Cd] (per voice id), and
 //   dGC_SIGNAL_l = GC_EMBEDᵀ·GCD_l[:, :Cd],  dGC_EMBED = Σ_l GCD_l·[GC_SIGNAL_l | GC_GATE_l]ᵀ.
 // LC: the per-layer projections LC_SIGNAL_l / LC_GATE_l are packed side by side into one
 // [Clc][L·2Cd] matrix so the whole conditioning input is ONE GEMM lc·LCcat (engine.cpp).
@@ -12,58 +12,93 @@
 
 namespace {
 
-// out[l][c][s·Cd + o] = Σ_e emb[c][e] · W_s[l][e][o]
+// Tables are [ncat+1][L·2Cd]: row c holds every layer's (sig Cd | gate Cd) block, n = l·2Cd + s·Cd + o.
+LBWN_DEV const float* gc_w(const float* wsig, const float* wgate, int n, int e, int Ge, int Cd) {
+  const int l = n / (2 * Cd), s = (n / Cd) & 1, o = n % Cd;
+  return (s == 0 ? wsig : wgate) + ((long)l * Ge + e) * Cd + o;
+}
+
+// out[c][n] = Σ_e emb[c][e] · W(n)[e]
 __global__ void gc_table_kernel(const float* __restrict__ emb, const float* __restrict__ wsig,
-                                const float* __restrict__ wgate, float* __restrict__ out, int L, int ncat1, int Ge,
+                                const float* __restrict__ wgate, float* __restrict__ out, int N, int ncat1, int Ge,
                                 int Cd) {
-  const long total = (long)L * ncat1 * 2 * Cd;
+  const long total = (long)ncat1 * N;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int n = (int)(i % (2 * Cd)), c = (int)((i / (2 * Cd)) % ncat1), l = (int)(i / (2L * Cd * ncat1));
-    const float* W = (n < Cd ? wsig : wgate) + (long)l * Ge * Cd + (n % Cd);
+    const int n = (int)(i % N), c = (int)(i / N);
     const float* e = emb + (long)c * Ge;
     float acc = 0.f;
-    for (int k = 0; k < Ge; ++k) acc += e[k] * W[(long)k * Cd];
+    for (int k = 0; k < Ge; ++k) acc += e[k] * *gc_w(wsig, wgate, n, k, Ge, Cd);
     out[i] = acc;
   }
 }
 
-// dW_s[l][e][o] = Σ_c emb[c][e] · GCD[l][c][s·Cd + o]
-__global__ void gc_wgrad_kernel(const float* __restrict__ emb, const float* __restrict__ gcd, float* __restrict__ dsig,
-                                float* __restrict__ dgate, int L, int ncat1, int Ge, int Cd) {
-  const long total = (long)L * 2 * Ge * Cd;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int o = (int)(i % Cd), e = (int)((i / Cd) % Ge), s = (int)((i / ((long)Cd * Ge)) % 2),
-              l = (int)(i / (2L * Ge * Cd));
-    const float* g = gcd + (long)l * ncat1 * 2 * Cd + s * Cd + o;
-    float acc = 0.f;
-    for (int c = 0; c < ncat1; ++c) acc += emb[(long)c * Ge + e] * g[(long)c * 2 * Cd];
-    (s == 0 ? dsig : dgate)[(long)l * Ge * Cd + (long)e * Cd + o] = acc;
+constexpr int GC_CSPLIT = 16;   // category chunks of the weight-gradient pass
+constexpr int GC_EMAX = 32;     // n_gc_embed supported by the gradient kernels
+
+// part[k][e][n] = Σ_{c in chunk k} emb[c][e] · gcd[c][n]   (grid: n blocks × GC_CSPLIT chunks)
+__global__ __launch_bounds__(256) void gc_wgrad_part_kernel(const float* __restrict__ emb,
+                                                            const float* __restrict__ gcd, float* __restrict__ part,
+                                                            int N, int ncat1, int Ge) {
+  const int n = blockIdx.x * 256 + threadIdx.x, k = blockIdx.y;
+  const int per = (ncat1 + GC_CSPLIT - 1) / GC_CSPLIT, c0 = k * per, c1 = min(ncat1, c0 + per);
+  float acc[GC_EMAX];
+#pragma unroll
+  for (int e = 0; e < GC_EMAX; ++e) acc[e] = 0.f;
+  if (n < N) {
+    for (int c = c0; c < c1; ++c) {
+      const float g = gcd[(long)c * N + n];
+#pragma unroll
+      for (int e = 0; e < GC_EMAX; ++e)
+        if (e < Ge) acc[e] += emb[(long)c * Ge + e] * g;
+    }
+#pragma unroll
+    for (int e = 0; e < GC_EMAX; ++e)
+      if (e < Ge) part[((long)k * Ge + e) * N + n] = acc[e];
   }
 }
 
-// dEMB[c][e] = Σ_l Σ_n GCD[l][c][n] · W_{n<Cd ? sig : gate}[l][e][n % Cd]; one block per c,
-// one thread per (e, partial over n), reduced in LDS.
+// dW(n)[e] = Σ_k part[k][e][n]  (fixed order: deterministic)
+__global__ void gc_wgrad_sum_kernel(const float* __restrict__ part, float* __restrict__ dsig, float* __restrict__ dgate,
+                                    int N, int Ge, int Cd) {
+  const long total = (long)Ge * N;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int n = (int)(i % N), e = (int)(i / N);
+    float s = 0.f;
+    for (int k = 0; k < GC_CSPLIT; ++k) s += part[((long)k * Ge + e) * N + n];
+    *const_cast<float*>(gc_w(dsig, dgate, n, e, Ge, Cd)) = s;
+  }
+}
+
+// dEMB[c][e] = Σ_n gcd[c][n] · W(n)[e]: one block per category, wave-then-block reduction.
 __global__ __launch_bounds__(256) void gc_egrad_kernel(const float* __restrict__ gcd, const float* __restrict__ wsig,
                                                        const float* __restrict__ wgate, float* __restrict__ demb,
-                                                       int L, int ncat1, int Ge, int Cd) {
-  __shared__ float red[256];
+                                                       int N, int Ge, int Cd) {
+  __shared__ float red[4][GC_EMAX];
   const int c = blockIdx.x;
-  for (int e0 = 0; e0 < Ge; ++e0) {
-    float acc = 0.f;
-    for (long j = threadIdx.x; j < (long)L * 2 * Cd; j += 256) {
-      const int l = (int)(j / (2 * Cd)), n = (int)(j % (2 * Cd));
-      const float* W = (n < Cd ? wsig : wgate) + (long)l * Ge * Cd + (long)e0 * Cd + (n % Cd);
-      acc += gcd[((long)l * ncat1 + c) * 2 * Cd + n] * *W;
-    }
-    red[threadIdx.x] = acc;
-    __syncthreads();
-    for (int s = 128; s > 0; s >>= 1) {
-      if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) demb[(long)c * Ge + e0] = red[0];
-    __syncthreads();
+  float acc[GC_EMAX];
+#pragma unroll
+  for (int e = 0; e < GC_EMAX; ++e) acc[e] = 0.f;
+  for (int n = threadIdx.x; n < N; n += 256) {
+    const float g = gcd[(long)c * N + n];
+    const int l = n / (2 * Cd), s = (n / Cd) & 1, o = n % Cd;
+    const float* W = (s == 0 ? wsig : wgate) + (long)l * Ge * Cd + o;
+#pragma unroll
+    for (int e = 0; e < GC_EMAX; ++e)
+      if (e < Ge) acc[e] += g * W[(long)e * Cd];
   }
+#pragma unroll
+  for (int e = 0; e < GC_EMAX; ++e) {
+    float v = acc[e];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    acc[e] = v;
+  }
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+#pragma unroll
+    for (int e = 0; e < GC_EMAX; ++e) red[w][e] = acc[e];
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < Ge) demb[(long)c * Ge + threadIdx.x] = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
 }
 
 // LCcat[i][l·2Cd + s·Cd + o] = W_s[l][i][o]  (pack = 1)  or the inverse scatter (pack = 0)
@@ -83,18 +118,25 @@ int grid_for(long n) { return (int)std::min<long>((n + 255) / 256, 4096); }
 
 }  // namespace
 
+int lbwn_gc_part_floats(int L, int Ge, int Cd) { return GC_CSPLIT * Ge * 2 * L * Cd; }
+
 int lbwn_gc_table_launch(const float* emb, const float* wsig, const float* wgate, float* out, int L, int ncat1,
                          int Ge, int Cd, hipStream_t st) {
-  gc_table_kernel<<<grid_for((long)L * ncat1 * 2 * Cd), 256, 0, st>>>(emb, wsig, wgate, out, L, ncat1, Ge, Cd);
+  const int N = 2 * L * Cd;
+  gc_table_kernel<<<grid_for((long)ncat1 * N), 256, 0, st>>>(emb, wsig, wgate, out, N, ncat1, Ge, Cd);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
 
-int lbwn_gc_grad_launch(const float* emb, const float* wsig, const float* wgate, const float* gcd, float* demb,
-                        float* dsig, float* dgate, int L, int ncat1, int Ge, int Cd, hipStream_t st) {
-  gc_wgrad_kernel<<<grid_for((long)L * 2 * Ge * Cd), 256, 0, st>>>(emb, gcd, dsig, dgate, L, ncat1, Ge, Cd);
+int lbwn_gc_grad_launch(const float* emb, const float* wsig, const float* wgate, const float* gcd, float* part,
+                        float* demb, float* dsig, float* dgate, int L, int ncat1, int Ge, int Cd, hipStream_t st) {
+  LBWN_REQUIRE(Ge >= 1 && Ge <= GC_EMAX, "gc grads: n_gc_embed must be in [1, %d]", GC_EMAX);
+  const int N = 2 * L * Cd;
+  gc_wgrad_part_kernel<<<dim3((N + 255) / 256, GC_CSPLIT), 256, 0, st>>>(emb, gcd, part, N, ncat1, Ge);
   LBWN_CHECK_LAUNCH();
-  gc_egrad_kernel<<<ncat1, 256, 0, st>>>(gcd, wsig, wgate, demb, L, ncat1, Ge, Cd);
+  gc_wgrad_sum_kernel<<<grid_for((long)Ge * N), 256, 0, st>>>(part, dsig, dgate, N, Ge, Cd);
+  LBWN_CHECK_LAUNCH();
+  gc_egrad_kernel<<<ncat1, 256, 0, st>>>(gcd, wsig, wgate, demb, N, Ge, Cd);
   LBWN_CHECK_LAUNCH();
   return 0;
 }

@@ -22,7 +22,7 @@ struct lbwn_plan {
   // workspace carving (byte offsets)
   size_t oX, oZ, oS, oR2, oLOG, oDH, oDS, oDZ, oGA[2], oGC0[2], oDX0, oSLAB, oSPLIT, oSPLIT2, oCOLS, oCOLS2,
       oHEADP, oBSUM, oWPK, oFLAGS, oSTATUS, oOCG;
-  size_t oGCTAB, oGCD, oLCACT[8], oCOND, oDVALL, oLCCAT, oDLCCAT, oDLC[2];
+  size_t oGCTAB, oGCD, oGCPART, oLCACT[8], oCOND, oDVALL, oLCCAT, oDLCCAT, oDLC[2];
   int split_dlc, split_up[8];
   size_t total;
   long x_layer_stride;  // floats
@@ -113,6 +113,7 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   LBWN_REQUIRE(a->n_res % 4 == 0 && a->n_dil % 4 == 0, "plan: n_res/n_dil must be multiples of 4");
   LBWN_REQUIRE(a->n_gc_embed >= 0 && (a->n_gc_embed == 0 || a->n_gc_category >= 1),
                "plan: GC needs n_gc_category >= 1");
+  LBWN_REQUIRE(a->n_gc_embed <= 32, "plan: n_gc_embed > 32 not supported");
   int hop = 1;
   if (a->n_lc_out > 0) {
     LBWN_REQUIRE(a->n_lc_upsample >= 1 && a->n_lc_upsample <= 8, "plan: LC needs 1..8 upsample stages");
@@ -200,6 +201,7 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     const long ncond = 2L * L * p->Cd;
     p->oGCTAB = p->Ge ? carve(cur, f * (size_t)L * p->ncat1 * 2 * p->Cd) : 0;
     p->oGCD = p->Ge ? carve(cur, f * (size_t)L * p->ncat1 * 2 * p->Cd) : 0;
+    p->oGCPART = p->Ge ? carve(cur, f * (size_t)lbwn_gc_part_floats(L, p->Ge, p->Cd)) : 0;
     long rows = (long)B * (T / hop);
     for (int i = 0; i < 8; ++i) {
       p->oLCACT[i] = 0;
@@ -236,6 +238,10 @@ int lbwn_plan_tensor(const lbwn_plan* p, const char* name, size_t* off, size_t* 
   else if (!strcmp(name, "dh")) { *off = p->oDH; *bytes = f * M * p->Cp; }
   else if (!strcmp(name, "ds")) { *off = p->oDS; *bytes = f * M * p->Cs; }
   else if (!strcmp(name, "dz")) { *off = p->oDZ; *bytes = f * M * p->L * p->Cd; }
+  else if (!strcmp(name, "cond") && p->Lo) { *off = p->oCOND; *bytes = f * M * 2 * p->L * p->Cd; }
+  else if (!strcmp(name, "dvall") && p->Lo) { *off = p->oDVALL; *bytes = f * M * 2 * p->L * p->Cd; }
+  else if (!strcmp(name, "gctab") && p->Ge) { *off = p->oGCTAB; *bytes = f * p->ncat1 * 2 * p->L * p->Cd; }
+  else if (!strcmp(name, "gcd") && p->Ge) { *off = p->oGCD; *bytes = f * p->ncat1 * 2 * p->L * p->Cd; }
   else LBWN_REQUIRE(false, "plan_tensor: unknown tensor '%s'", name);
   return 0;
 }
@@ -283,13 +289,14 @@ namespace {
 
 // Conditioning operands of the layer stack (tmodel.py:105-114, :150-160)
 struct Cond {
-  const float* gc_tab = nullptr; long gc_ls = 0;   // GCTAB [L][ncat+1][2Cd]
+  const float* gc_tab = nullptr; long gc_ld = 0;   // GCTAB [ncat+1][L·2Cd]
   const float* cond = nullptr; long ldcond = 0;     // COND [M][L·2Cd]
   float* gc_dtab = nullptr;                         // backward: GCD
   float* dv_out = nullptr;                          // backward: DVALL
   void apply(lbwn_layer_args& a, int l) const {
-    a.gc_tab = gc_tab ? gc_tab + l * gc_ls : nullptr;
-    a.gc_dtab = gc_dtab ? gc_dtab + l * gc_ls : nullptr;
+    a.gc_tab = gc_tab ? gc_tab + (long)l * 2 * a.Cd : nullptr;
+    a.gc_dtab = gc_dtab ? gc_dtab + (long)l * 2 * a.Cd : nullptr;
+    a.gc_ld = gc_ld;
     a.cond = cond ? cond + (long)l * 2 * a.Cd : nullptr;
     a.ldcond = ldcond;
     a.dv_out = dv_out ? dv_out + (long)l * 2 * a.Cd : nullptr;
@@ -306,7 +313,7 @@ int cond_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const float* mel,
     float* tab = at<float>(ws, p->oGCTAB);
     if ((e = lbwn_gc_table_launch(P->gc_embed, P->gc_sig, P->gc_gate, tab, L, p->ncat1, p->Ge, Cd, st))) return e;
     c.gc_tab = tab;
-    c.gc_ls = (long)p->ncat1 * 2 * Cd;
+    c.gc_ld = 2L * L * Cd;
   }
   if (p->Lo > 0) {
     const float* in = mel;
@@ -346,8 +353,8 @@ int cond_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G, void
   const int L = p->L, Cd = p->Cd;
   float* SPL = at<float>(ws, p->oSPLIT);
   if (p->Ge > 0) {
-    if ((e = lbwn_gc_grad_launch(P->gc_embed, P->gc_sig, P->gc_gate, at<float>(ws, p->oGCD), G->gc_embed, G->gc_sig,
-                                 G->gc_gate, L, p->ncat1, p->Ge, Cd, st)))
+    if ((e = lbwn_gc_grad_launch(P->gc_embed, P->gc_sig, P->gc_gate, at<float>(ws, p->oGCD), at<float>(ws, p->oGCPART),
+                                 G->gc_embed, G->gc_sig, G->gc_gate, L, p->ncat1, p->Ge, Cd, st)))
       return e;
   }
   if (p->Lo > 0) {
@@ -400,6 +407,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   int e;
   if ((e = ensure_device(p))) return e;
   LBWN_REQUIRE(p->Lo == 0 || mel, "train_forward: LC arch needs the mel input");
+  if (!p->chain) LBWN_HIP(hipMemsetAsync(at<char>(ws, p->oSTATUS), 0, 16, st));  // chains zero it themselves
   const int L = p->L, B = p->B, T = p->T, H = p->H, Cr = p->Cr, Cd = p->Cd;
   const long M = p->M, ldz = (long)L * Cd;
   float* X = at<float>(ws, p->oX);
@@ -423,7 +431,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     lbwn_chain_args c;
     memset(&c, 0, sizeof(c));
     c.X = X; c.xls = p->x_layer_stride; c.Z = Z; c.ldz = ldz; c.wpack = WPK; c.ids = ids;
-    c.gc_tab = cd.gc_tab; c.gc_ls = cd.gc_ls; c.cond = cd.cond; c.ldcond = cd.ldcond;
+    c.gc_tab = cd.gc_tab; c.gc_ld = cd.gc_ld; c.cond = cd.cond; c.ldcond = cd.ldcond;
     c.flags = at<unsigned>(ws, p->oFLAGS); c.status = at<unsigned>(ws, p->oSTATUS);
     c.B = B; c.T = T; c.H = H; c.L = L; c.nbl = p->nbl; c.Cr = Cr; c.Cd = Cd; c.grid = p->chain_grid;
     Probe(p, st, "layer_fwd");
@@ -551,7 +559,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   Cond cd;
   if (p->Ge > 0) {
     cd.gc_tab = at<float>(ws, p->oGCTAB);
-    cd.gc_ls = (long)p->ncat1 * 2 * Cd;
+    cd.gc_ld = 2L * L * Cd;
     cd.gc_dtab = at<float>(ws, p->oGCD);
     LBWN_HIP(hipMemsetAsync(cd.gc_dtab, 0, sizeof(float) * (size_t)L * p->ncat1 * 2 * Cd, st));
   }
@@ -569,7 +577,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     memset(&c, 0, sizeof(c));
     c.X = X; c.xls = p->x_layer_stride; c.DZ = DZ; c.ldz = ldz; c.wpack = WPK; c.ids = ids;
     c.slab = SLABS; c.ocg = at<float>(ws, p->oOCG); c.ocls = M * 32;
-    c.gc_tab = cd.gc_tab; c.gc_ls = cd.gc_ls; c.cond = cd.cond; c.ldcond = cd.ldcond;
+    c.gc_tab = cd.gc_tab; c.gc_ld = cd.gc_ld; c.cond = cd.cond; c.ldcond = cd.ldcond;
     c.gc_dtab = cd.gc_dtab; c.dv_out = cd.dv_out; c.lddv = cd.ldcond;
     c.dx0_a = at<float>(ws, p->oGA[0]); c.dx0_c = at<float>(ws, p->oGC0[0]);
     c.flags = at<unsigned>(ws, p->oFLAGS); c.status = at<unsigned>(ws, p->oSTATUS);

@@ -29,7 +29,8 @@ struct lbwn_layer_args {
   const float* b_sig; const float* b_gate;  // [Cd] nullable
   const float* w_res; const float* b_res;   // [Cd][Cr], [Cr] nullable
   const float* wpack;       // packed LDS image of this layer (lbwn_pack_layers_launch)
-  const float* gc_tab;      // [ncat+1][2*Cd] (sig | gate) nullable
+  const float* gc_tab;      // rows [ncat+1] of (sig Cd | gate Cd), row stride gc_ld (0 = 2Cd); nullable
+  long gc_ld;
   const int* ids;           // [B][T]
   const float* cond; long ldcond;  // [M][2*Cd] nullable (LC projection)
   int B, T, H, d, Cr, Cd;
@@ -65,7 +66,7 @@ struct lbwn_chain_args {
   float* X; long xls;          // x_l buffers of all layers, layer stride in floats
   float* Z; long ldz;
   const float* wpack;
-  const float* gc_tab; long gc_ls; const int* ids;   // GC table [L][ncat+1][2Cd] or null
+  const float* gc_tab; long gc_ld; const int* ids;   // GC table [ncat+1][L·2Cd] or null
   const float* cond; long ldcond;                     // LC term [M][L·2Cd] or null
   float* dv_out; long lddv; float* gc_dtab;           // backward: LC dv export, GC grad table
   unsigned* flags;             // [B·ceil(T/128)] (zeroed by the launcher)
@@ -126,6 +127,7 @@ int lbwn_bcast_rows_launch(float* dst, int L, int N, hipStream_t st);
 // Conditioning (cond.hip)
 int lbwn_gc_table_launch(const float* emb, const float* wsig, const float* wgate, float* out, int L, int ncat1,
                          int Ge, int Cd, hipStream_t st);
-int lbwn_gc_grad_launch(const float* emb, const float* wsig, const float* wgate, const float* gcd, float* demb,
-                        float* dsig, float* dgate, int L, int ncat1, int Ge, int Cd, hipStream_t st);
+int lbwn_gc_grad_launch(const float* emb, const float* wsig, const float* wgate, const float* gcd, float* part,
+                        float* demb, float* dsig, float* dgate, int L, int ncat1, int Ge, int Cd, hipStream_t st);
+int lbwn_gc_part_floats(int L, int Ge, int Cd);
 int lbwn_lc_pack_launch(float* cat, float* wsig, float* wgate, int L, int Clc, int Cd, int pack, hipStream_t st);

@@ -33,14 +33,14 @@ constexpr int RED_PARTS = 32;       // deferred reduction: parts prefetched per 
 struct FwdK {
   const float* x_in; float* x_out; float* z; const float* wpack;
   const float* gc_tab; const int* ids; const float* cond;
-  long ldz, ldcond;
+  long ldz, ldcond, gc_ld;
   int B, T, H, d, Cr, Cd;
 };
 struct BwdK {
   const float* x_in; const float* wpack; const float* dz_skip;
   const float* g_a; const float* g_c0; float* out_a; float* out_c0; float* slab;
   const float* gc_tab; const int* ids; const float* cond; float* dv_out; float* gc_dtab;
-  long lddz, ldcond, lddv;
+  long lddz, ldcond, lddv, gc_ld;
   int B, T, H, d, Cr, Cd, g_d, slab_stride;
 };
 // Standalone slab reduction (runs on an auxiliary stream, off the layer chain).
@@ -166,7 +166,7 @@ LBWN_DEV void conv_tile(const float* Xp, const float* Xc, const float* Ws, const
     acc_g[r] = bs[32 + acc_row(r, h)];
   }
   if (valid && (a.gc_tab || a.cond)) {
-    const float* cs = a.gc_tab ? a.gc_tab + (long)a.ids[m] * 2 * a.Cd : nullptr;
+    const float* cs = a.gc_tab ? a.gc_tab + (long)a.ids[m] * a.gc_ld : nullptr;
     const float* cl = a.cond ? a.cond + m * a.ldcond : nullptr;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -294,20 +294,35 @@ struct ChainFK {
   float* X; long xls;        // x_l for all layers: layer stride (floats); each [B][H+T][32]
   float* Z; long ldz;
   const float* wpack;        // L packed images
-  const float* gc_tab; long gc_ls;              // GC table [L][ncat+1][2Cd] (layer stride gc_ls) or null
+  const float* gc_tab; long gc_ld;              // GC table [ncat+1][L·2Cd] (row stride gc_ld; layer l at l·2Cd)
   const int* ids; const float* cond; long ldcond; // LC term COND [M][L·2Cd] (layer l at column l·2Cd) or null
   unsigned* flags; unsigned* status;
   int B, T, H, L, nbl, Cd;
 };
 
-// conditioning operands of one layer, in the shape conv_init reads
-struct CondRef {
-  const float* gc_tab; const int* ids; const float* cond; long ldcond; int Cd;
-};
+// GC + LC term of layer l for this lane's position, in acc layout: cv[q] = sig channels
+// 8q+4h..+3, cv[4+q] = gate channels (16-B loads; issued one layer ahead by the chains).
 template <typename K>
-LBWN_DEV CondRef cond_of(const K& a, int l) {
-  return CondRef{a.gc_tab ? a.gc_tab + (long)l * a.gc_ls : nullptr, a.ids,
-                 a.cond ? a.cond + (long)l * 2 * a.Cd : nullptr, a.ldcond, a.Cd};
+LBWN_DEV void load_cond(const K& a, int l, int myid, long m, bool valid, int h, floatx4 (&cv)[8]) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) cv[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (!valid) return;
+  if (a.gc_tab) {
+    const float* g = a.gc_tab + (long)myid * a.gc_ld + (long)l * 64;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      cv[q] += *(const floatx4*)(g + 8 * q + 4 * h);
+      cv[4 + q] += *(const floatx4*)(g + 32 + 8 * q + 4 * h);
+    }
+  }
+  if (a.cond) {
+    const float* c = a.cond + m * a.ldcond + (long)l * 64;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      cv[q] += *(const floatx4*)(c + 8 * q + 4 * h);
+      cv[4 + q] += *(const floatx4*)(c + 32 + 8 * q + 4 * h);
+    }
+  }
 }
 
 LBWN_DEV bool wait_flag_ge(unsigned* f, unsigned want, unsigned* status, unsigned code) {
@@ -326,26 +341,15 @@ LBWN_DEV void publish_flag(unsigned* f, unsigned v) {
   __hip_atomic_store((gu32*)f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// bias (+ GC / LC conditioning) into the accumulators (acc layout rows = out channel)
-template <typename K>
-LBWN_DEV void conv_init(const float* bs, const K& a, long m, bool valid, int h, floatx16& acc_s, floatx16& acc_g) {
+// bias + conditioning into the accumulators (acc layout rows = out channel)
+LBWN_DEV void conv_init(const float* bs, const floatx4 (&cv)[8], int h, floatx16& acc_s, floatx16& acc_g) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    acc_s[r] = bs[acc_row(r, h)];
-    acc_g[r] = bs[32 + acc_row(r, h)];
-  }
-  if (valid && (a.gc_tab || a.cond)) {
-    const float* cs = a.gc_tab ? a.gc_tab + (long)a.ids[m] * 2 * a.Cd : nullptr;
-    const float* cl = a.cond ? a.cond + m * a.ldcond : nullptr;
+  for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int o = acc_row(r, h);
-      if (o < a.Cd) {
-        if (cs) { acc_s[r] += cs[o]; acc_g[r] += cs[a.Cd + o]; }
-        if (cl) { acc_s[r] += cl[o]; acc_g[r] += cl[a.Cd + o]; }
-      }
+    for (int j = 0; j < 4; ++j) {
+      acc_s[4 * q + j] = bs[8 * q + 4 * h + j] + cv[q][j];
+      acc_g[4 * q + j] = bs[32 + 8 * q + 4 * h + j] + cv[4 + q][j];
     }
-  }
 }
 
 // acc += Wkᵀ·x over one tap: Wk = the 32 weight-image rows of that tap, xrow = this lane's
@@ -398,6 +402,10 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
     const bool valid = t < a.T;
     const long m = (long)b * a.T + t;
     const long sb = (long)b * (a.H + a.T) * 32;  // stream base inside a layer buffer
+    const bool has_cond = a.gc_tab || a.cond;
+    const int myid = (a.gc_tab && valid) ? a.ids[m] : 0;
+    floatx4 cv[8];
+    load_cond(a, 0, myid, m, valid && has_cond, h, cv);
     __syncthreads();  // previous tile's LDS use done
     stage_image(Ws, a.wpack, tid);
     stage_rows(sm, a.X + sb, t0, 0, a.T, a.H, 32, tid);  // x_0 (embed output, pre-launch)
@@ -419,7 +427,8 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
       }
       // 2. own tap first: W1·x[t]
       floatx16 acc_s, acc_g;
-      conv_init(bs, cond_of(a, l), m, valid, h, acc_s, acc_g);
+      conv_init(bs, cv, h, acc_s, acc_g);
+      if (has_cond && l + 1 < a.L) load_cond(a, l + 1, myid, m, valid, h, cv);
       conv_half(cur + r * XS, Ws + 32 * WS, pi, h, acc_s, acc_g);
       // 3. wait for the producer of the halo rows (x_l is layer l-1's output)
       const int ptt = tt - max(1, d / LP);
@@ -558,33 +567,39 @@ struct ChainBK {
   float* slab;                 // [L][ntiles][SLAB]
   float* ocg; long ocls;       // out_c0 hand-off rows: [L][B·T][32], layer stride ocls floats
   float* dx0_a; float* dx0_c;  // layer 0's out_a / out_c0 [B·T][32]
-  const float* gc_tab; long gc_ls; const int* ids; const float* cond; long ldcond;
+  const float* gc_tab; long gc_ld; const int* ids; const float* cond; long ldcond;
   float* dv_out; long lddv;    // dv export for the LC gradients: [M][L·2Cd] (layer l at column l·2Cd) or null
-  float* gc_dtab;              // GC gradient table [L][ncat+1][2Cd] (layer stride gc_ls), atomics, or null
+  float* gc_dtab;              // GC gradient table, layout of gc_tab, atomics, or null
   unsigned* flags; unsigned* status;
   int B, T, H, L, nbl, Cd;
 };
 
 // dv rows of wave w's 32 positions (DV, position-major) scatter-added into the GC gradient
-// table row of each position's voice id (fast path: one id for the whole wave).
-LBWN_DEV void gc_scatter(float* gtab, const int* ids_b, const float* DV, int t0, int T, int w, int lane, int Cd) {
+// table row (row stride ld) of each position's voice id.  uni_id >= 0: the caller knows the
+// run is one id (one atomic per column); otherwise the ids are checked here.
+LBWN_DEV void gc_scatter(float* gtab, long ld, const int* ids_b, const float* DV, int t0, int T, int w, int lane,
+                         int Cd, int uni_id) {
   const int tw0 = t0 + 32 * w;
   const int nv = min(32, T - tw0);
   if (nv <= 0) return;
   const int* idw = ids_b + tw0;
-  const int id0 = idw[0];
-  bool uni = true;
-  for (int p = 1; p < nv; ++p) uni &= (idw[p] == id0);
+  int id0 = uni_id;
+  if (id0 < 0) {
+    id0 = idw[0];
+    bool uni = true;
+    for (int p = 1; p < nv; ++p) uni &= (idw[p] == id0);
+    if (!uni) id0 = -1;
+  }
   const int o = lane, oc = o & 31;
   const float* dvw = DV + 32 * w * DS;
   if (oc >= Cd) return;
   const int col = o < 32 ? oc : Cd + oc;
-  if (uni) {
+  if (id0 >= 0) {
     float s = 0.f;
     for (int p = 0; p < nv; ++p) s += dvw[p * DS + o];
-    atomicAdd(gtab + (long)id0 * 2 * Cd + col, s);
+    atomicAdd(gtab + (long)id0 * ld + col, s);
   } else {
-    for (int p = 0; p < nv; ++p) atomicAdd(gtab + (long)idw[p] * 2 * Cd + col, dvw[p * DS + o]);
+    for (int p = 0; p < nv; ++p) atomicAdd(gtab + (long)idw[p] * ld + col, dvw[p * DS + o]);
   }
 }
 
@@ -616,6 +631,13 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
     const bool valid = t < a.T;
     const long mb = (long)b * a.T, m = mb + t;
     const long sb = (long)b * (a.H + a.T) * 32;
+    const bool has_cond = a.gc_tab || a.cond;
+    const int myid = (a.gc_tab && valid) ? a.ids[m] : 0;
+    floatx4 cv[8];
+    load_cond(a, a.L - 1, myid, m, valid && has_cond, h, cv);
+    // GC grads: is this wave's 32-position run one voice id?  (fast scatter path)
+    const int wave_id = __shfl(myid, 0);
+    const bool wave_uni = __all(!valid || myid == wave_id);
     __syncthreads();
     stage_image(Ws, a.wpack + (long)(a.L - 1) * WIMG, tid);
     floatx16 oa;  // out_a of layer l+1, own row
@@ -648,7 +670,8 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
       __syncthreads();
       // 1. recompute the gate (no cross-tile dependency)
       floatx16 acc_s, acc_g;
-      conv_init(bs, cond_of(a, l), m, valid, h, acc_s, acc_g);
+      conv_init(bs, cv, h, acc_s, acc_g);
+      if (has_cond && l > 0) load_cond(a, l - 1, myid, m, valid, h, cv);
       conv_half(Xc + r * XS, Ws + 32 * WS, pi, h, acc_s, acc_g);
       conv_half(Xp + r * XS, Ws, pi, h, acc_s, acc_g);
       floatx16 th, sg;
@@ -678,15 +701,13 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
           *(floatx4*)(G + row * XS + c4) = v;
         }
         __syncthreads();
-      } else {
-        for (int e = tid; e < LP * 8; e += 256) *(floatx4*)(G + (e >> 3) * XS + (e & 7) * 4) = floatx4{0.f, 0.f, 0.f, 0.f};
       }
       floatx16 gv;
-      {
+      {  // own row: + out_a (at the top layer g = 0: the row is written here, not read)
         float* grow = G + r * XS;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          floatx4 v = *(const floatx4*)(grow + 8 * q + 4 * h);
+          floatx4 v = dn ? *(const floatx4*)(grow + 8 * q + 4 * h) : floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int j = 0; j < 4; ++j) { v[j] += oa[4 * q + j]; gv[4 * q + j] = v[j]; }
           *(floatx4*)(grow + 8 * q + 4 * h) = v;
@@ -772,7 +793,8 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // also: DV complete, the weight image is dead
       if (tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
-      if (a.gc_dtab) gc_scatter(a.gc_dtab + (long)l * a.gc_ls, a.ids + mb, DV, t0, a.T, w, lane, 32);
+      if (a.gc_dtab) gc_scatter(a.gc_dtab + (long)l * 64, a.gc_ld, a.ids + mb, DV, t0, a.T, w, lane, 32,
+                                wave_uni ? wave_id : -1);
       // 5. weight gradients of layer l over this tile
       {
         float* zrow = ZT + r * XS;
@@ -1097,7 +1119,7 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(BwdK a) {
         if (tt < a.T && oc < a.Cd) a.dv_out[(mb + tt) * a.lddv + (o < 32 ? oc : a.Cd + oc)] = DV[p * DS + o];
       }
     }
-    if (a.gc_dtab) gc_scatter(a.gc_dtab, a.ids + mb, DV, t0, a.T, w, lane, a.Cd);
+    if (a.gc_dtab) gc_scatter(a.gc_dtab, a.gc_ld, a.ids + mb, DV, t0, a.T, w, lane, a.Cd, -1);
   }
 
   // 8. block partial -> slab: tiles 0..3 straight from their wave, dRES summed over waves
@@ -1129,7 +1151,7 @@ int grid_bwd(const lbwn_layer_args& a) { return std::min(lbwn_layer_nblocks(a.B,
 FwdK to_fwd(const lbwn_layer_args& a) {
   FwdK k;
   k.x_in = a.x_in; k.x_out = a.x_out; k.z = a.z; k.wpack = a.wpack; k.gc_tab = a.gc_tab; k.ids = a.ids;
-  k.cond = a.cond; k.ldz = a.ldz; k.ldcond = a.ldcond;
+  k.cond = a.cond; k.ldz = a.ldz; k.ldcond = a.ldcond; k.gc_ld = a.gc_ld ? a.gc_ld : 2L * a.Cd;
   k.B = a.B; k.T = a.T; k.H = a.H; k.d = a.d; k.Cr = a.Cr; k.Cd = a.Cd;
   return k;
 }
@@ -1138,6 +1160,7 @@ BwdK to_bwd(const lbwn_layer_args& a) {
   k.x_in = a.x_in; k.wpack = a.wpack; k.dz_skip = a.dz_skip; k.g_a = a.g_a; k.g_c0 = a.g_c0;
   k.out_a = a.out_a; k.out_c0 = a.out_c0; k.slab = a.slab; k.gc_tab = a.gc_tab; k.ids = a.ids; k.cond = a.cond;
   k.dv_out = a.dv_out; k.gc_dtab = a.gc_dtab; k.lddz = a.lddz; k.ldcond = a.ldcond; k.lddv = a.lddv;
+  k.gc_ld = a.gc_ld ? a.gc_ld : 2L * a.Cd;
   k.B = a.B; k.T = a.T; k.H = a.H; k.d = a.d; k.Cr = a.Cr; k.Cd = a.Cd; k.g_d = a.g_d; k.slab_stride = a.slab_stride;
   return k;
 }
@@ -1199,7 +1222,7 @@ int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   LBWN_REQUIRE((((uintptr_t)c.X) & 15) == 0 && (c.xls & 3) == 0, "chain fwd: x not 16-B aligned");
   ChainFK k;
   k.X = c.X; k.xls = c.xls; k.Z = c.Z; k.ldz = c.ldz; k.wpack = c.wpack;
-  k.gc_tab = c.gc_tab; k.gc_ls = c.gc_ls; k.ids = c.ids; k.cond = c.cond; k.ldcond = c.ldcond;
+  k.gc_tab = c.gc_tab; k.gc_ld = c.gc_ld; k.ids = c.ids; k.cond = c.cond; k.ldcond = c.ldcond;
   k.flags = c.flags; k.status = c.status;
   k.B = c.B; k.T = c.T; k.H = c.H; k.L = c.L; k.nbl = c.nbl; k.Cd = c.Cd;
   const int tps = (c.T + LP - 1) / LP;
@@ -1217,7 +1240,7 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   ChainBK k;
   k.X = c.X; k.xls = c.xls; k.DZ = c.DZ; k.lddz = c.ldz; k.wpack = c.wpack; k.slab = c.slab;
   k.ocg = c.ocg; k.ocls = c.ocls; k.dx0_a = c.dx0_a; k.dx0_c = c.dx0_c;
-  k.gc_tab = c.gc_tab; k.gc_ls = c.gc_ls; k.ids = c.ids; k.cond = c.cond; k.ldcond = c.ldcond;
+  k.gc_tab = c.gc_tab; k.gc_ld = c.gc_ld; k.ids = c.ids; k.cond = c.cond; k.ldcond = c.ldcond;
   k.dv_out = c.dv_out; k.lddv = c.lddv; k.gc_dtab = c.gc_dtab;
   k.flags = c.flags; k.status = c.status;
   k.B = c.B; k.T = c.T; k.H = c.H; k.L = c.L; k.nbl = c.nbl; k.Cd = c.Cd;
