@@ -148,3 +148,125 @@ class SyntheticSource:
         mel = r.normal(size=(n // self.hop, self.n_mel)).astype(np.float32) if self.n_mel else None
         vid = int(r.integers(1, self.n_voices + 1))
         return vid, wav, mel
+
+
+class MaskedSliceWav:
+    """data.MaskedSliceWav (data.py:20-293) on the host: same constructor, catalog methods,
+    iterator contract ``(file_read_count, wav[B,T], mel[B,T/hop,C], ids[B,T])`` and
+    checkpointed position.  The tf.data graph (repeat → shuffle(seed) → skip(position) →
+    slice generator → prefetch, data.py:236-268) becomes: a seeded per-epoch permutation of
+    the catalog, a skip of ``ckpt_position`` file reads on resume, the SliceDealer, and a
+    prefetch thread of ``prefetch_sz`` batches.  TF's shuffle RNG stream cannot be
+    reproduced without TF, so the file ORDER differs from a TF run with the same seed
+    (distribution and slicing semantics are identical; SliceDealer is golden-exact)."""
+
+    def __init__(self, sess, sam_file, sample_rate, slice_sz, prefetch_sz, mel_spectrum_sz, mel_hop_sz, batch_sz,
+                 n_keep_checkpoints, ckpt_path, resume_step, random_seed=None, rows=None):
+        from .ckpt import Checkpoint
+        self.sam_file = sam_file
+        self.sample_rate = sample_rate
+        self.prefetch_sz = max(1, int(prefetch_sz or 1))
+        self.mel_spectrum_sz = mel_spectrum_sz or 0
+        self.mel_hop_sz = mel_hop_sz
+        if slice_sz % mel_hop_sz != 0:      # data.py:32-36 (the dealer repeats the warning)
+            slice_sz += mel_hop_sz - (slice_sz % mel_hop_sz)
+        self.slice_sz = slice_sz
+        self.batch_sz = batch_sz
+        self.rows = rows            # DP: this rank's slot range of the global batch
+        self.random_seed = np.array([random_seed if random_seed is not None
+                                     else np.random.randint(np.iinfo(np.int32).max)], np.int64)
+        self.ckpt_position = np.zeros(1, np.int64)
+        self.ckpt = Checkpoint(ckpt_path, n_keep_checkpoints, resume_step)
+        self.recep_field_sz = None
+        self.sample_catalog = None
+        self._itr = None
+
+    def init_sample_catalog(self):
+        self.sample_catalog = []
+        with open(self.sam_file) as fh:
+            for s in fh:
+                s = s.strip()
+                if s:
+                    vid, wav_path, mel_path = s.split('\t')
+                    self.sample_catalog.append([int(vid), wav_path, mel_path])
+
+    def set_receptive_field_size(self, r_sz):
+        self.recep_field_sz = r_sz
+
+    def get_max_id(self):
+        return max(self.sample_catalog, key=lambda x: x[0])[0]
+
+    def _files(self):
+        cat = self.sample_catalog
+        rng = np.random.default_rng(int(self.random_seed[0]))
+        skip = int(self.ckpt_position[0])
+        count = 0
+        want_mel = self.mel_spectrum_sz > 0
+        while True:
+            for i in rng.permutation(len(cat)):
+                count += 1
+                if count <= skip:
+                    continue
+                vid, wp, mp = cat[i]
+                wav = np.load(wp)                          # never allow_pickle
+                mel = np.load(mp).astype(np.float32) if want_mel else None
+                yield vid, wav, mel
+
+    def build(self):
+        if self.sample_catalog is None:
+            self.init_sample_catalog()
+        if self.recep_field_sz is None:
+            raise ValueError('set_receptive_field_size first (data.py:55-56, train.py:167)')
+
+    def init_vars(self):
+        self._itr = None
+
+    def get_itr(self):
+        """Iterator of prefetched batches (starts the producer thread on first use)."""
+        if self._itr is None:
+            import queue
+            import threading
+            dealer = SliceDealer(self._files(), self.batch_sz, self.slice_sz, self.recep_field_sz,
+                                 self.mel_hop_sz, self.mel_spectrum_sz)
+            q = queue.Queue(maxsize=self.prefetch_sz)
+            rows = self.rows
+
+            def produce():
+                for cnt, wav, mel, ids in dealer:
+                    if rows is not None:
+                        wav, ids = wav[rows], ids[rows]
+                        mel = mel[rows] if mel is not None else None
+                    q.put((cnt, wav, mel, ids))
+                q.put(None)
+
+            threading.Thread(target=produce, daemon=True).start()
+
+            def gen():
+                while True:
+                    item = q.get()
+                    if item is None:
+                        return
+                    yield item
+            self._itr = gen()
+        return self._itr
+
+    def get_op(self):
+        return next(self.get_itr())
+
+    def save(self, step, read_count):
+        self.ckpt_position[0] = read_count
+        self.ckpt.saveable_objects = {'random_seed': torch_tensor(self.random_seed),
+                                      'ckpt_position': torch_tensor(self.ckpt_position)}
+        return self.ckpt.save(step)
+
+    def restore(self):
+        from .ckpt import load_tensors
+        t = load_tensors('{}-{}'.format(self.ckpt.ckpt_path, self.ckpt.resume_step))
+        self.random_seed[0] = int(t['random_seed'][0])
+        self.ckpt_position[0] = int(t['ckpt_position'][0])
+        self._itr = None
+
+
+def torch_tensor(a):
+    import torch
+    return torch.as_tensor(np.asarray(a))

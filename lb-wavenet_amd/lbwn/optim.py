@@ -29,3 +29,32 @@ class AdamOptimizer:
                                          net.layout.n_weights, net.layout.n_total, self.lr, self.b1, self.b2,
                                          self.eps, net.l2_factor, net.stats.data_ptr(), net.counters.data_ptr(),
                                          _lib.stream_ptr(stream)))
+        net.global_step_host += 1
+
+    # ---- checkpoint state: TF's slot names (<var>/Adam = m, <var>/Adam_1 = v) ----------------
+    def state_tensors(self, net):
+        m, v = self.slots(net)
+        out = {}
+        for name, t in net.layout.views(m).items():
+            out[name + '/Adam'] = t
+        for name, t in net.layout.views(v).items():
+            out[name + '/Adam_1'] = t
+        out['Adam/step'] = net.counters[2:3]
+        return out
+
+    def load_state_tensors(self, net, loaded):
+        """Restore the slots if the checkpoint has them (reference checkpoints do not:
+        tmodel.py:330 saves only the model variables, so Adam restarts from zero)."""
+        m, v = self.slots(net)
+        with torch.no_grad():
+            if 'Adam/step' not in loaded:
+                m.zero_()
+                v.zero_()
+                net.counters[2:3].zero_()
+                return False
+            for name, t in net.layout.views(m).items():
+                t.copy_(loaded[name + '/Adam'])
+            for name, t in net.layout.views(v).items():
+                t.copy_(loaded[name + '/Adam_1'])
+            net.counters[2:3].copy_(loaded['Adam/step'])
+        return True

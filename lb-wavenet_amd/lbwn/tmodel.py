@@ -18,6 +18,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .ckpt import Checkpoint
 from .arch import ParamLayout, layer_iter, n_layers, recep_field_sz, save_layout, xavier_limit
 
 
@@ -75,6 +76,10 @@ class WaveNetTrain:
         self._plans = {}
         self._ws = None
         self.init_vars(seed)
+        self.global_step_host = 0    # host mirror of GLOBAL_STEP (advanced by the optimizer)
+        # checkpoint surface (ckpt.py:13-81; the saveables are self.vars, tmodel.py:330)
+        self.ckpt = Checkpoint(ckpt_path, n_keep_checkpoints, resume_step)
+        self.ckpt.add_saveable_objects(self.state_tensors())
 
     # ---- reference API -------------------------------------------------------------------
     def get_recep_field_sz(self):
@@ -215,10 +220,26 @@ class WaveNetTrain:
 
     def maybe_print(self, file=sys.stderr):
         """The in-graph progress print (tmodel.py:272-281): every print_interval steps,
-        BEFORE the counters advance."""
-        step = int(self.counters[0])
-        if self.print_interval and step % self.print_interval == 0:
+        BEFORE the counters advance.  Uses the host mirror of GLOBAL_STEP, so steps that do
+        not print never synchronise with the device."""
+        if self.print_interval and self.global_step_host % self.print_interval == 0:
             print(self.progress_line(), file=file)
+
+    # ---- checkpoints (ckpt.py:53-81) --------------------------------------------------------
+    def save(self, step, optimizer=None):
+        """Write '<ckpt_path>-<step>.safetensors'; with ``optimizer`` its Adam slots too."""
+        if self.device.type == 'cuda':
+            torch.cuda.synchronize(self.device)
+        extra = optimizer.state_tensors(self) if optimizer is not None else None
+        return self.ckpt.save(step, extra)
+
+    def restore(self, optimizer=None):
+        """Load '<ckpt_path>-<resume_step>' into the live buffers (ckpt.py:63-81)."""
+        loaded = self.ckpt.restore()
+        if optimizer is not None:
+            optimizer.load_state_tensors(self, loaded)
+        self.global_step_host = int(self.counters[0])
+        return loaded
 
     # ---- state dicts (checkpoint surface, names as arch.py:142) ----------------------------
     def state_tensors(self):

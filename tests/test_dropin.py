@@ -1,0 +1,205 @@
+"""Host-side drop-in surface (CPU): checkpoints (ckpt.py), the MaskedSliceWav dataset
+(data.py:20-293), train.py argument handling (train.py:12-80), and the data-parallel
+gradient reduction over gloo with world_size 2."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from lbwn.arch import load_arch, normalize_arch, ParamLayout
+from lbwn.ckpt import ckpt_file, load_tensors
+from lbwn.data import MaskedSliceWav, SliceDealer
+from lbwn.optim import AdamOptimizer
+from lbwn.tmodel import WaveNetTrain
+from tests.conftest import ROOT
+
+
+def small_arch():
+    return normalize_arch(dict(n_blocks=1, n_block_layers=3, n_quant=256, n_res=8, n_dil=8, n_skip=16, n_post=8,
+                               n_gc_embed=0, n_gc_category=0, use_bias=True))
+
+
+def test_checkpoint_roundtrip_reference_names(tmp_path):
+    arch = load_arch(os.path.join(ROOT, 'par', 'arch5.json'))
+    a = WaveNetTrain(**arch, batch_sz=2, l2_factor=1e-3, device='cpu', ckpt_path=str(tmp_path / 'run.net'), seed=3)
+    opt = AdamOptimizer()
+    m, v = opt.slots(a)
+    m.uniform_(-1, 1)
+    v.uniform_(0, 1)
+    a.counters[:3] = torch.tensor([17, 12345, 16])
+    pfx = a.save(17, opt)
+    assert pfx == str(tmp_path / 'run.net') + '-17'
+    t = load_tensors(pfx)
+    # the reference's serial names (arch.py:142) and TF's Adam slot names
+    for k in ('PRE', 'SIGNAL_0_0', 'SIGNAL_4_9', 'GC_EMBED', 'LC_UPSAMPLE_3', 'LC_GATE_2_5', 'POST2_BIAS',
+              'SAVE_1_0_0', 'SAVE_512_4_9', 'GLOBAL_STEP', 'VALID_SAMPLES', 'SIGNAL_0_0/Adam', 'POST1/Adam_1'):
+        assert k in t, k
+    assert tuple(t['SAVE_512_4_9'].shape) == (2, 512, 32)
+    b = WaveNetTrain(**arch, batch_sz=2, l2_factor=1e-3, device='cpu', ckpt_path=str(tmp_path / 'run.net'),
+                     resume_step=17, seed=9)
+    opt2 = AdamOptimizer()
+    b.restore(opt2)
+    assert torch.equal(a.flat, b.flat) and torch.equal(a.save_flat, b.save_flat)
+    assert torch.equal(a.counters[:3], b.counters[:3]) and b.global_step_host == 17
+    assert all(torch.equal(x, y) for x, y in zip(opt.slots(a), opt2.slots(b)))
+
+
+def test_checkpoint_rotation_and_missing(tmp_path):
+    net = WaveNetTrain(**small_arch(), batch_sz=1, l2_factor=0.0, device='cpu', n_keep_checkpoints=2,
+                       ckpt_path=str(tmp_path / 'r.net'))
+    for s in (1, 2, 3):
+        net.save(s)
+    assert not os.path.exists(ckpt_file(str(tmp_path / 'r.net'), 1))
+    assert os.path.exists(ckpt_file(str(tmp_path / 'r.net'), 3))
+    with pytest.raises(SystemExit):
+        load_tensors(str(tmp_path / 'r.net-9'))
+
+
+def _write_catalog(tmp_path, n_files=5, hop=4, n_mel=3):
+    rng = np.random.default_rng(0)
+    lines = []
+    for i in range(n_files):
+        n = int(rng.integers(40, 90)) * hop + int(rng.integers(0, hop))
+        wav = rng.integers(0, 256, n).astype(np.int32)
+        mel = rng.standard_normal((n // hop, n_mel)).astype(np.float32)
+        wp, mp = tmp_path / ('f%d.wav.npy' % i), tmp_path / ('f%d.mel.npy' % i)
+        np.save(wp, wav)
+        np.save(mp, mel)
+        lines.append('%d\t%s\t%s' % (i % 3 + 1, wp, mp))
+    cat = tmp_path / 'samples.txt'
+    cat.write_text('\n'.join(lines) + '\n')
+    return str(cat)
+
+
+def test_masked_slice_wav_matches_dealer(tmp_path):
+    cat = _write_catalog(tmp_path)
+    F, T, B, hop = 13, 64, 3, 4
+    ds = MaskedSliceWav(None, cat, 16000, T, 2, 3, hop, B, 5, str(tmp_path / 'x.dset'), 0, random_seed=42)
+    ds.init_sample_catalog()
+    assert ds.get_max_id() == 3
+    ds.set_receptive_field_size(F)
+    ds.build()
+    got = [ds.get_op() for _ in range(6)]
+    src = MaskedSliceWav(None, cat, 16000, T, 2, 3, hop, B, 5, None, 0, random_seed=42)
+    src.init_sample_catalog()
+    ref = SliceDealer(src._files(), B, T, F, hop, 3)
+    for g, r in zip(got, ref):
+        assert g[0] == r[0]
+        np.testing.assert_array_equal(g[1], r[1])
+        np.testing.assert_array_equal(g[2], r[2])
+        np.testing.assert_array_equal(g[3], r[3])
+
+
+def test_masked_slice_wav_resume_and_rows(tmp_path):
+    cat = _write_catalog(tmp_path)
+    ds = MaskedSliceWav(None, cat, 16000, 64, 2, 3, 4, 2, 5, str(tmp_path / 'x.dset'), 0, random_seed=7)
+    ds.init_sample_catalog()
+    files = ds._files()
+    order = [next(files)[1][:5].tolist() for _ in range(8)]
+    ds.set_receptive_field_size(13)
+    ds.build()
+    cnt = ds.get_op()[0]
+    ds.save(4, cnt)
+    r = MaskedSliceWav(None, cat, 16000, 64, 2, 3, 4, 2, 5, str(tmp_path / 'x.dset'), 4)
+    r.init_sample_catalog()
+    r.restore()
+    assert int(r.random_seed[0]) == 7 and int(r.ckpt_position[0]) == cnt
+    resumed = [next(r._files())[1][:5].tolist()]
+    assert resumed[0] == order[cnt]          # continues after the files already read
+    # DP: a rank's rows of the globally dealt batch
+    full = MaskedSliceWav(None, cat, 16000, 64, 2, 3, 4, 4, 5, None, 0, random_seed=1)
+    part = MaskedSliceWav(None, cat, 16000, 64, 2, 3, 4, 4, 5, None, 0, random_seed=1, rows=slice(2, 4))
+    for d in (full, part):
+        d.init_sample_catalog()
+        d.set_receptive_field_size(13)
+        d.build()
+    a, b = full.get_op(), part.get_op()
+    np.testing.assert_array_equal(a[1][2:4], b[1])
+    np.testing.assert_array_equal(a[3][2:4], b[3])
+
+
+def test_train_cli_errors(tmp_path, monkeypatch):
+    sys.path.insert(0, os.path.join(ROOT, 'lb-wavenet_amd'))
+    import train
+    arch = tmp_path / 'a.json'
+    arch.write_text('{"n_blocks": 1, "n_block_layers": 2, "n_quant": 256, "n_res": 8, "n_dil": 8, '
+                    '"n_skip": 8, "n_post": 8, "n_gc_embed": 4, "use_bias": true}')
+    par = os.path.join(ROOT, 'par', 'par1.json')
+    with pytest.raises(SystemExit) as e:     # n_gc_category missing and no --num-global-cond
+        train.main([str(tmp_path / 'ck'), str(arch), par, 'none.txt'])
+    assert e.value.code == 1
+    with pytest.raises(SystemExit) as e:
+        train.main(['--cpu-only', str(tmp_path / 'ck'), os.path.join(ROOT, 'par', 'arch3.json'), par, 'none.txt'])
+    assert e.value.code == 1
+    args = train.get_args(['-bs', '4', '-ss', '1024', '-lr', '0.01', '-rs', '7', 'p', 'a', 'b', 'c'])
+    assert (args.batch_size, args.slice_size, args.learning_rate, args.resume_step) == (4, 1024, 0.01, 7)
+
+
+# ---- data parallel over gloo, world_size 2 -----------------------------------------------------
+
+class _FakeNet:
+    def __init__(self, grads, stats):
+        self.grad_flat = grads
+        self.stats = stats
+
+
+def _dp_worker(rank, world, port, q_np, ids_np, out_path):
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, 'lb-wavenet_amd'))
+    from oracle import wavenet_ref as R
+    from lbwn.dist import DPContext
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    arch = small_arch()
+    rng = np.random.default_rng(0)
+    P = R.init_params(arch, rng, dtype=np.float64)
+    S = R.init_save(arch, 4, rng, dtype=np.float64)
+    dp = DPContext(world, rank, rank)
+    rows = dp.rows(2)
+    Sr = {k: v[rows] for k, v in S.items()}
+    lg, cache, _ = R.forward(arch, P, q_np[rows], ids_np[rows], Sr)
+    st, dlog = R.loss_fcn(arch, P, lg, q_np[rows], ids_np[rows], 0.0)
+    G = R.backward(arch, P, cache, dlog, 0.0)
+    lay = ParamLayout(arch)
+    flat = np.zeros(lay.n_total)
+    for n, e in lay.entries.items():       # raw Σ-xent gradient, as the device buffer holds it
+        flat[e.offset:e.offset + e.numel] = (G[n] * st['n_valid']).reshape(-1)
+    net = _FakeNet(torch.tensor(flat, dtype=torch.float32),
+                   torch.tensor([st['mean_xent'] * st['n_valid'], st['n_valid'], 0.0, 0.0], dtype=torch.float32))
+    dp.reduce_grads(net)
+    if rank == 0:
+        np.savez(out_path, grads=net.grad_flat.numpy(), stats=net.stats.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_gloo_two_ranks_equals_single_process(tmp_path):
+    import torch.multiprocessing as mp
+    sys.path.insert(0, ROOT)
+    from oracle import wavenet_ref as R
+    arch = small_arch()
+    rng = np.random.default_rng(5)
+    B, T = 4, 48
+    q = rng.integers(0, 256, (B, T))
+    ids = np.ones((B, T), np.int32)
+    ids[:, :5] = 0
+    ids[3, 20:30] = 0
+    out = str(tmp_path / 'dp.npz')
+    port = 29500 + os.getpid() % 1000
+    mp.spawn(_dp_worker, args=(2, port, q, ids, out), nprocs=2, join=True)
+    got = np.load(out)
+    # single process over all 4 streams
+    rng0 = np.random.default_rng(0)
+    P = R.init_params(arch, rng0, dtype=np.float64)
+    S = R.init_save(arch, 4, rng0, dtype=np.float64)
+    lg, cache, _ = R.forward(arch, P, q, ids, S)
+    st, dlog = R.loss_fcn(arch, P, lg, q, ids, 0.0)
+    G = R.backward(arch, P, cache, dlog, 0.0)
+    assert int(got['stats'][1]) == st['n_valid']
+    lay = ParamLayout(arch)
+    for n, e in lay.entries.items():   # Adam divides the summed raw grads by the GLOBAL n_valid
+        np.testing.assert_allclose(got['grads'][e.offset:e.offset + e.numel] / got['stats'][1], G[n].reshape(-1),
+                                   rtol=2e-4, atol=1e-7, err_msg=n)
