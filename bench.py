@@ -26,6 +26,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from lbwn import _lib  # noqa: E402
+from lbwn import dist as lbdist  # noqa: E402
 from lbwn.arch import load_arch, mel_hop_sz, n_layers, recep_field_sz  # noqa: E402
 from lbwn.data import SliceDealer, SyntheticSource  # noqa: E402
 from lbwn.imodel import WaveNetGen  # noqa: E402
@@ -147,13 +148,10 @@ def main():
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
     if world != args.gpus:
         raise SystemExit('--gpus %d but WORLD_SIZE=%d (launch N>1 with torch.distributed.run)' % (args.gpus, world))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dp = lbdist.init()          # one process per GPU; RCCL when WORLD_SIZE > 1
+    rank = dp.rank
 
     arch = load_arch(args.arch, num_global_cond=args.gc)
     B, T = args.batch, args.slice
@@ -169,7 +167,7 @@ def main():
     ring = []
     for _ in range(8):
         _, wav, mel, ids = next(dealer)
-        rows = slice(rank * B, (rank + 1) * B)
+        rows = dp.rows(B)
         ring.append((torch.as_tensor(wav[rows], dtype=torch.int32).to(dev),
                      None if mel is None else torch.as_tensor(mel[rows], dtype=torch.float32).to(dev),
                      torch.as_tensor(ids[rows], dtype=torch.int32).to(dev)))
@@ -179,9 +177,7 @@ def main():
     def step(i):
         q, mel, ids = ring[i % len(ring)]
         net.forward(q, mel, ids, backward=True)
-        if world > 1:
-            dist.all_reduce(net.grad_flat)
-            dist.all_reduce(net.stats[:3])
+        dp.reduce_grads(net)
         opt.apply(net)
 
     def probe(name):
@@ -225,10 +221,7 @@ def main():
     for name, (s, e) in pending:
         samples[name].append(s.elapsed_time(e))
     ms = dt * 1000.0 / args.steps
-    if world > 1:
-        tm = torch.tensor([ms], device=dev)
-        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-        ms = float(tm.item())
+    ms = dp.max_over_ranks(ms, dev)
     value = world * B * T / (ms / 1000.0)
 
     def roof(name, ms_list):

@@ -21,18 +21,18 @@ from .ops import mu_encode_np
 
 class SliceDealer:
     def __init__(self, files, batch_sz, slice_sz, recep_field_sz, mel_hop_sz=1, mel_spectrum_sz=0,
-                 log=sys.stderr):
+                 log=None):
         if slice_sz % mel_hop_sz != 0:      # data.py:32-36
             requested = slice_sz
             slice_sz += mel_hop_sz - (slice_sz % mel_hop_sz)
             print('Warning: aligning slice size from {} to {} for mel_hop_sz {}'.format(
-                requested, slice_sz, mel_hop_sz), file=log)
+                requested, slice_sz, mel_hop_sz), file=log or sys.stderr)
         self.slice_sz = slice_sz
         self.batch_sz = batch_sz
         self.recep_field_sz = recep_field_sz
         self.mel_hop_sz = mel_hop_sz
         self.mel_spectrum_sz = mel_spectrum_sz
-        self.log = log
+        self.log = log or sys.stderr
         self.files_read = 0
         self._files = iter(files)
         self._gens = [self._slot() for _ in range(batch_sz)]

@@ -218,12 +218,12 @@ class WaveNetTrain:
         return ('{:5d}\t{:8.4f}\t{:8.4f}\t{:7.2f}\t{:5.0f}\t{:5.0f}\t{:10d}\t{:14d}\t{:5.2f}'.format(
             cnt[0], total, mean, l2, avg_diff, nv, cnt[1], int(self.n_valid_total), pct))
 
-    def maybe_print(self, file=sys.stderr):
+    def maybe_print(self, file=None):
         """The in-graph progress print (tmodel.py:272-281): every print_interval steps,
         BEFORE the counters advance.  Uses the host mirror of GLOBAL_STEP, so steps that do
         not print never synchronise with the device."""
         if self.print_interval and self.global_step_host % self.print_interval == 0:
-            print(self.progress_line(), file=file)
+            print(self.progress_line(), file=file or sys.stderr)
 
     # ---- checkpoints (ckpt.py:53-81) --------------------------------------------------------
     def save(self, step, optimizer=None):
