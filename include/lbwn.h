@@ -64,14 +64,18 @@ void lbwn_plan_destroy(lbwn_plan* plan);
 size_t lbwn_plan_workspace_bytes(const lbwn_plan* plan);
 /* Byte offset/size of a named workspace tensor (for parity tests / debugging):
  * "x" [L][B][H+T][n_res] (layer inputs with D-sep halo, H = 2^(n_block_layers-1)),
- * "z" [M][L·n_dil] (gate outputs; dZ after backward), "s" [M][n_skip] (skip sum; dS after
- * backward), "r2" [M][n_post], "logits" [M][n_quant] (dlogits after forward).  */
+ * "z" [M][L·n_dil] (gate outputs), "s" [M][n_skip] (skip sum), "r2" [M][n_post],
+ * "logits" [M][n_quant] (dlogits after forward), "dh" [M][n_post], "ds" [M][n_skip],
+ * "dz" [M][L·n_dil] (backward), "status" (int32: 0, or the code of a chain hand-off that
+ * timed out), and for conditioned archs "cond"/"dvall" [M][L·2·n_dil] (LC term, its dv),
+ * "gctab"/"gcd" [n_cat+1][L·2·n_dil] (GC table, its gradient).  */
 int lbwn_plan_tensor(const lbwn_plan* plan, const char* name, size_t* offset, size_t* bytes);
 /* One-shot timing probe: the next lbwn_train_forward/backward on this plan records
  * hipEvent_t ev_start right before and ev_stop right after the named launch(es):
- * "layer_fwd" (all residual-layer forward launches), "layer_fwd@<l>" (layer l only),
- * "layer_bwd", "layer_bwd@<l>", "skip_fwd" (S = Zcat·SKIPcat), "post1_fwd", "post2_fwd",
- * "head", "dskip" (Zcatᵀ·dS), "dz" (dS·SKIPcatᵀ), "dpost1", "dpost2".  Events are the
+ * "layer_fwd" (the residual stack: the persistent chain launch, or the span of the
+ * per-layer launches; "layer_fwd@<l>" = layer l of the per-layer path), "layer_bwd",
+ * "layer_reduce", "skip_fwd" (S = Zcat·SKIPcat), "post1_fwd", "post2_fwd", "head", "lc_cond",
+ * "dpost2", "dh", "dpost1", "ds", "dskip" (Zcatᵀ·dS), "dz" (dS·SKIPcatᵀ).  Events are the
  * caller's (e.g. torch.cuda.Event(enable_timing=True).cuda_event). */
 int lbwn_plan_probe(lbwn_plan* plan, const char* launch_name, void* ev_start, void* ev_stop);
 /* receptive field F = n_blocks·Σ2^l (tmodel.py:50-51) */
