@@ -31,6 +31,18 @@ struct lbwn_plan {
   int nblk;                      // layer-bwd blocks = slab partials per layer
   bool chain = false;            // persistent layer-chain kernels (n_res = n_dil = 32)
   int chain_grid = 0;            // resident blocks for the chain (set on first use)
+  // Backward overlap: the weight-gradient GEMMs (dPOST2, dPOST1, dSKIP) do not feed the
+  // layer chain, which keeps the MFMA pipes ~1/3 busy at one wave per SIMD, so they run on
+  // a low-priority stream in lean-LDS form (21 KB beside the chain's 131 KB block).
+  bool overlap = false;
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  size_t oSPLIT_AUX = 0, oCOLS_AUX = 0;
+  ~lbwn_plan() {
+    if (aux) (void)hipStreamDestroy(aux);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+  }
   // one-shot event probe
   char probe[32];
   hipEvent_t probe_start, probe_stop;
@@ -196,6 +208,12 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   const char* nc = getenv("LBWN_NO_CHAIN");
   p->chain = p->Cr == 32 && p->Cd == 32 && !(nc && nc[0] == '1');
   p->oOCG = p->chain ? carve(cur, sizeof(float) * (size_t)L * M * 32) : 0;
+  const char* ov = getenv("LBWN_OVERLAP");
+  p->overlap = p->chain && !(ov && ov[0] == '0');
+  if (p->overlap) {
+    p->oSPLIT_AUX = carve(cur, sizeof(float) * (size_t)p->split_floats);
+    p->oCOLS_AUX = carve(cur, sizeof(float) * (size_t)lbwn_colsum_ws_floats((int)M, std::max({p->Cs, p->Cp, p->Q})));
+  }
   {  // conditioning
     const size_t f = sizeof(float);
     const long ncond = 2L * L * p->Cd;
@@ -264,6 +282,13 @@ int ensure_device(lbwn_plan* p) {
   LBWN_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
   const int ntiles = p->B * ((p->T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS);
   p->chain_grid = std::max(1, std::min(ntiles, ncu));
+  if (p->overlap) {
+    int least = 0, greatest = 0;
+    LBWN_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    LBWN_HIP(hipStreamCreateWithPriority(&p->aux, hipStreamNonBlocking, least));
+    LBWN_HIP(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
+    LBWN_HIP(hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
+  }
   return 0;
 }
 
@@ -510,13 +535,6 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   float* SPL = at<float>(ws, p->oSPLIT);
   float* COLS = at<float>(ws, p->oCOLS);
   lbwn_gemm_args g;
-  // dPOST2 = R2ᵀ·dlogits, db2 = Σ dlogits
-  g = gemm0();
-  g.A = R2; g.lda = Cp; g.B = LOG; g.ldb = Q; g.C = G->post2; g.ldc = Q; g.M = Cp; g.N = Q; g.K = (int)M;
-  Probe(p, st, "dpost2");
-  if ((e = lbwn_gemm_launch(g, 0, 0, p->split_post2, SPL, st))) return e;
-  Probe::end(p, st, "dpost2");
-  if (G->post2_b && (e = lbwn_colsum_launch(LOG, Q, (int)M, Q, G->post2_b, 0, COLS, st))) return e;
   // dH1 = dlogits·POST2ᵀ ⊙ (R2 > 0)
   g = gemm0();
   g.A = LOG; g.lda = Q; g.B = P->post2; g.ldb = Q; g.C = DH; g.ldc = Cp; g.M = (int)M; g.N = Cp; g.K = Q;
@@ -524,14 +542,6 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   Probe(p, st, "dh");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
   Probe::end(p, st, "dh");
-  // dPOST1 = relu(S)ᵀ·dH1, db1 = Σ dH1
-  g = gemm0();
-  g.A = S; g.lda = Cs; g.relu_a = 1; g.B = DH; g.ldb = Cp; g.C = G->post1; g.ldc = Cp; g.M = Cs; g.N = Cp;
-  g.K = (int)M;
-  Probe(p, st, "dpost1");
-  if ((e = lbwn_gemm_launch(g, 0, 0, p->split_post1, SPL, st))) return e;
-  Probe::end(p, st, "dpost1");
-  if (G->post1_b && (e = lbwn_colsum_launch(DH, Cp, (int)M, Cp, G->post1_b, 0, COLS, st))) return e;
   // dS = dH1·POST1ᵀ ⊙ (S > 0)
   g = gemm0();
   g.A = DH; g.lda = Cp; g.B = P->post1; g.ldb = Cp; g.C = DS; g.ldc = Cs; g.M = (int)M; g.N = Cs; g.K = Cp;
@@ -539,22 +549,52 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   Probe(p, st, "ds");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
   Probe::end(p, st, "ds");
-  // dSKIPcat = Zcatᵀ·dS; every layer's SKIP_BIAS gets the same Σ dS
-  g = gemm0();
-  g.A = Z; g.lda = ldz; g.B = DS; g.ldb = Cs; g.C = G->skip; g.ldc = Cs; g.M = (int)ldz; g.N = Cs; g.K = (int)M;
-  Probe(p, st, "dskip");
-  if ((e = lbwn_gemm_launch(g, 0, 0, p->split_skip, SPL, st))) return e;
-  Probe::end(p, st, "dskip");
-  if (G->skip_b) {
-    if ((e = lbwn_colsum_launch(DS, Cs, (int)M, Cs, G->skip_b, 0, COLS, st))) return e;
-    if ((e = lbwn_bcast_rows_launch(G->skip_b, L, Cs, st))) return e;
-  }
   // dZ = dS·SKIPcatᵀ
   g = gemm0();
   g.A = DS; g.lda = Cs; g.B = P->skip; g.ldb = Cs; g.C = DZ; g.ldc = ldz; g.M = (int)M; g.N = (int)ldz; g.K = Cs;
   Probe(p, st, "dz");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
   Probe::end(p, st, "dz");
+  // weight gradients of the head and skip GEMMs: beside the layer chain (aux stream) or here
+  hipStream_t ws_st = st;
+  float* WSPL = SPL;
+  float* WCOLS = COLS;
+  auto wgemm = [&](const lbwn_gemm_args& a, int split) {
+    return p->overlap ? lbwn_gemm_launch_lean(a, 0, 0, split, WSPL, ws_st) : lbwn_gemm_launch(a, 0, 0, split, WSPL, ws_st);
+  };
+  if (p->overlap) {
+    ws_st = p->aux;
+    WSPL = at<float>(ws, p->oSPLIT_AUX);
+    WCOLS = at<float>(ws, p->oCOLS_AUX);
+    LBWN_HIP(hipEventRecord(p->ev_fork, st));
+    LBWN_HIP(hipStreamWaitEvent(ws_st, p->ev_fork, 0));
+  }
+  // dPOST2 = R2ᵀ·dlogits, db2 = Σ dlogits
+  g = gemm0();
+  g.A = R2; g.lda = Cp; g.B = LOG; g.ldb = Q; g.C = G->post2; g.ldc = Q; g.M = Cp; g.N = Q; g.K = (int)M;
+  Probe(p, ws_st, "dpost2");
+  if ((e = wgemm(g, p->split_post2))) return e;
+  Probe::end(p, ws_st, "dpost2");
+  if (G->post2_b && (e = lbwn_colsum_launch(LOG, Q, (int)M, Q, G->post2_b, 0, WCOLS, ws_st))) return e;
+  // dPOST1 = relu(S)ᵀ·dH1, db1 = Σ dH1
+  g = gemm0();
+  g.A = S; g.lda = Cs; g.relu_a = 1; g.B = DH; g.ldb = Cp; g.C = G->post1; g.ldc = Cp; g.M = Cs; g.N = Cp;
+  g.K = (int)M;
+  Probe(p, ws_st, "dpost1");
+  if ((e = wgemm(g, p->split_post1))) return e;
+  Probe::end(p, ws_st, "dpost1");
+  if (G->post1_b && (e = lbwn_colsum_launch(DH, Cp, (int)M, Cp, G->post1_b, 0, WCOLS, ws_st))) return e;
+  // dSKIPcat = Zcatᵀ·dS; every layer's SKIP_BIAS gets the same Σ dS
+  g = gemm0();
+  g.A = Z; g.lda = ldz; g.B = DS; g.ldb = Cs; g.C = G->skip; g.ldc = Cs; g.M = (int)ldz; g.N = Cs; g.K = (int)M;
+  Probe(p, ws_st, "dskip");
+  if ((e = wgemm(g, p->split_skip))) return e;
+  Probe::end(p, ws_st, "dskip");
+  if (G->skip_b) {
+    if ((e = lbwn_colsum_launch(DS, Cs, (int)M, Cs, G->skip_b, 0, WCOLS, ws_st))) return e;
+    if ((e = lbwn_bcast_rows_launch(G->skip_b, L, Cs, ws_st))) return e;
+  }
+  if (p->overlap) LBWN_HIP(hipEventRecord(p->ev_join, ws_st));
   // residual stack in reverse (conditioning recomputed from the forward's GCTAB / COND)
   Cond cd;
   if (p->Ge > 0) {
@@ -630,5 +670,6 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   if ((e = lbwn_gemm_launch(g, 0, 0, p->split_pre, at<float>(ws, p->oSPLIT2), st))) return e;
   if (G->pre_b && (e = lbwn_colsum_launch(DX0, Cr, (int)M, Cr, G->pre_b, 0, at<float>(ws, p->oCOLS2), st)))
     return e;
+  if (p->overlap) LBWN_HIP(hipStreamWaitEvent(st, p->ev_join, 0));
   return 0;
 }

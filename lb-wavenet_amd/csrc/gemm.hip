@@ -12,21 +12,27 @@
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 16, NT = 256;
-constexpr int KCS = BK + 4;  // padded row (floats) of a k-contiguous LDS image: 80 B -> conflict-free b128
+constexpr int BM = 128, BN = 128, NT = 256;
+// padded row of an mn-contiguous image: fragment reads of lane halves h = 0/1 are rows 4 apart,
+// and 4·(BMN+8) ≡ 32 (mod 64 banks) puts the halves on disjoint banks
+constexpr int MNPAD = 8;
 
-template <bool KC, int BMN>
+// BK = 16: the default (37 KB LDS, 2 blocks/CU).  BK = 8: the lean variant (21 KB) that fits
+// beside a resident persistent chain block (131 KB) to run weight-gradient GEMMs concurrently.
+template <bool KC, int BMN, int BK>
 struct Stage {
-  // per-thread registers for one BK tile of one operand (2 x float4)
-  floatx4 v[2];
-  static constexpr int LDS_FLOATS = KC ? BMN * KCS : BK * BMN;
+  static constexpr int SREG = BK * BMN / (4 * NT);   // float4 staging registers per thread
+  static constexpr int KCS = BK + 4;                 // padded k-contiguous row: conflict-free b128
+  static constexpr int RS = BMN + MNPAD;             // row stride of the mn-contiguous image
+  floatx4 v[SREG];
+  static constexpr int LDS_FLOATS = KC ? BMN * KCS : BK * RS;
 
   LBWN_DEV void load(const float* __restrict__ P, long ld, int mn0, int MN, int k0, int K, int tid,
                      bool relu, const int* codes = nullptr) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < SREG; ++i) {
       int r, c;  // r: index along M/N, c: along K
-      if (KC) { r = tid / 4 + 64 * i; c = (tid % 4) * 4; }
+      if (KC) { r = tid / (BK / 4) + (NT / (BK / 4)) * i; c = (tid % (BK / 4)) * 4; }
       else    { c = tid / 32 + 8 * i; r = (tid % 32) * 4; }
       int gr = mn0 + r, gk = k0 + c;
       floatx4 x = {0.f, 0.f, 0.f, 0.f};
@@ -50,9 +56,12 @@ struct Stage {
   }
   LBWN_DEV void store(float* lds, int tid) const {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      if (KC) { int r = tid / 4 + 64 * i, c = (tid % 4) * 4; *(floatx4*)(lds + r * KCS + c) = v[i]; }
-      else    { int c = tid / 32 + 8 * i, r = (tid % 32) * 4; *(floatx4*)(lds + c * BMN + r) = v[i]; }
+    for (int i = 0; i < SREG; ++i) {
+      if (KC) {
+        int r = tid / (BK / 4) + (NT / (BK / 4)) * i, c = (tid % (BK / 4)) * 4;
+        *(floatx4*)(lds + r * KCS + c) = v[i];
+      }
+      else    { int c = tid / 32 + 8 * i, r = (tid % 32) * 4; *(floatx4*)(lds + c * RS + r) = v[i]; }
     }
   }
   // fragment for rows [base, base+32) of group g: element j = value at k = 8g+4h+j
@@ -61,7 +70,7 @@ struct Stage {
     if (KC) return *(const floatx4*)(lds + (base + i) * KCS + 8 * g + 4 * h);
     floatx4 f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) f[j] = lds[(8 * g + 4 * h + j) * BMN + base + i];
+    for (int j = 0; j < 4; ++j) f[j] = lds[(8 * g + 4 * h + j) * RS + base + i];
     return f;
   }
 };
@@ -73,10 +82,10 @@ LBWN_DEV int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
-template <bool A_KC, bool B_KC>
+template <bool A_KC, bool B_KC, int BK>
 __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(lbwn_gemm_args g) {
-  using SA = Stage<A_KC, BM>;
-  using SB = Stage<B_KC, BN>;
+  using SA = Stage<A_KC, BM, BK>;
+  using SB = Stage<B_KC, BN, BK>;
   __shared__ __attribute__((aligned(16))) float smem[2 * (SA::LDS_FLOATS + SB::LDS_FLOATS)];
   auto As = [&](int i) { return smem + i * SA::LDS_FLOATS; };
   auto Bs = [&](int i) { return smem + 2 * SA::LDS_FLOATS + i * SB::LDS_FLOATS; };
@@ -186,8 +195,9 @@ __global__ void splitk_reduce_kernel(lbwn_gemm_args g, const float* __restrict__
 
 }  // namespace
 
-int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
-                     hipStream_t st) {
+namespace {
+template <int BK>
+int gemm_launch_t(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws, hipStream_t st) {
   LBWN_REQUIRE(a.M > 0 && a.N > 0 && a.K > 0, "gemm: empty shape M=%d N=%d K=%d", a.M, a.N, a.K);
   LBWN_REQUIRE(a.K % 4 == 0 || !a_kcontig, "gemm: K %% 4 != 0 with k-contiguous A");
   LBWN_REQUIRE(a.K % 4 == 0 || !b_kcontig, "gemm: K %% 4 != 0 with k-contiguous B");
@@ -213,10 +223,10 @@ int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int 
   } else {
     g.split_stride = 0;
   }
-  if (a_kcontig && b_kcontig) gemm_f32_kernel<true, true><<<grid, NT, 0, st>>>(g);
-  else if (a_kcontig) gemm_f32_kernel<true, false><<<grid, NT, 0, st>>>(g);
-  else if (b_kcontig) gemm_f32_kernel<false, true><<<grid, NT, 0, st>>>(g);
-  else gemm_f32_kernel<false, false><<<grid, NT, 0, st>>>(g);
+  if (a_kcontig && b_kcontig) gemm_f32_kernel<true, true, BK><<<grid, NT, 0, st>>>(g);
+  else if (a_kcontig) gemm_f32_kernel<true, false, BK><<<grid, NT, 0, st>>>(g);
+  else if (b_kcontig) gemm_f32_kernel<false, true, BK><<<grid, NT, 0, st>>>(g);
+  else gemm_f32_kernel<false, false, BK><<<grid, NT, 0, st>>>(g);
   LBWN_CHECK_LAUNCH();
   if (split_k > 1) {
     const long total = (long)a.M * (a.N / 4);
@@ -225,4 +235,15 @@ int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int 
     LBWN_CHECK_LAUNCH();
   }
   return 0;
+}
+}  // namespace
+
+int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
+                     hipStream_t st) {
+  return gemm_launch_t<16>(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
+}
+
+int lbwn_gemm_launch_lean(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
+                          hipStream_t st) {
+  return gemm_launch_t<8>(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
 }

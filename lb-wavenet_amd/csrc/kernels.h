@@ -18,6 +18,9 @@ struct lbwn_gemm_args {
 };
 int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                      hipStream_t st);
+// same product with a 21 KB LDS footprint (BK = 8) so it can co-reside with a chain block
+int lbwn_gemm_launch_lean(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
+                          hipStream_t st);
 
 // One residual layer (tmodel.py:117-184).  x buffers are [B][H+T][Cr]; rows [H-d, H) of
 // x_in hold the D-separation state SAVE_l (prepended by lbwn_dsep_prepend).

@@ -1,0 +1,49 @@
+"""Time lbwn_gemm_f32 on the training step's GEMM shapes (arch3, M = 32768) next to
+torch.matmul fp32 (the vendor BLAS) on the same operands.  Usage: python tools/gemm_bench.py [LBWN_LIB]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'lb-wavenet_amd'))
+import torch  # noqa: E402
+from lbwn import _lib  # noqa: E402
+
+lib = _lib.load()
+M = 32768
+# name, M, N, K, a_kcontig, b_kcontig, split
+SHAPES = [('skip_fwd', M, 512, 1600, 1, 0, 1), ('dz', M, 1600, 512, 1, 1, 1), ('dskip', 1600, 512, M, 0, 0, 19),
+          ('post1_fwd', M, 512, 512, 1, 0, 1), ('ds', M, 512, 512, 1, 1, 1), ('dpost1', 512, 512, M, 0, 0, 4),
+          ('post2_fwd', M, 256, 512, 1, 0, 1), ('dh', M, 512, 256, 1, 1, 1), ('dpost2', 512, 256, M, 0, 0, 8)]
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e-3
+
+
+for name, m, n, k, akc, bkc, split in SHAPES:
+    A = torch.randn(m, k, device='cuda') if akc else torch.randn(k, m, device='cuda')
+    B = torch.randn(n, k, device='cuda') if bkc else torch.randn(k, n, device='cuda')
+    C = torch.empty(m, n, device='cuda')
+    slab = torch.empty(max(1, split) * m * n, device='cuda')
+    st = _lib.stream_ptr()
+
+    def ours():
+        _lib.check(lib.lbwn_gemm_f32(A.data_ptr(), A.shape[1], akc, B.data_ptr(), B.shape[1], bkc, C.data_ptr(), n,
+                                     m, n, k, None, 0, 0, None, 0, 0, split, slab.data_ptr(), st))
+    Am = A if akc else A.t()
+    Bm = B.t() if bkc else B
+
+    def ref():
+        torch.matmul(Am, Bm, out=C)
+    t0, t1 = timeit(ours), timeit(ref)
+    fl = 2.0 * m * n * k
+    print('%-10s M%6d N%5d K%6d  ours %7.1f us %6.1f TF | torch %7.1f us %6.1f TF' % (
+        name, m, n, k, t0 * 1e6, fl / t0 / 1e12, t1 * 1e6, fl / t1 / 1e12), flush=True)
