@@ -7,12 +7,14 @@
 // (B[n*ldb+k]).  The LDS image follows the global layout (no transposing stage), and the
 // MFMA k-order is permuted so a k-contiguous operand feeds four v_mfma_f32_32x32x2_f32
 // steps from one ds_read_b128: at step j of an 8-deep group, lane half h uses k = 8g+4h+j.
+#include <stdlib.h>
+
 #include "common.h"
 #include "kernels.h"
 
 namespace {
 
-constexpr int BM = 128, BN = 128, NT = 256;
+constexpr int NT = 256;
 // padded row of an mn-contiguous image: fragment reads of lane halves h = 0/1 are rows 4 apart,
 // and 4·(BMN+8) ≡ 32 (mod 64 banks) puts the halves on disjoint banks
 constexpr int MNPAD = 8;
@@ -28,12 +30,12 @@ struct Stage {
   static constexpr int LDS_FLOATS = KC ? BMN * KCS : BK * RS;
 
   LBWN_DEV void load(const float* __restrict__ P, long ld, int mn0, int MN, int k0, int K, int tid,
-                     bool relu, const int* codes = nullptr) {
+                     bool /*relu: applied in store()*/, const int* codes = nullptr) {
 #pragma unroll
     for (int i = 0; i < SREG; ++i) {
       int r, c;  // r: index along M/N, c: along K
       if (KC) { r = tid / (BK / 4) + (NT / (BK / 4)) * i; c = (tid % (BK / 4)) * 4; }
-      else    { c = tid / 32 + 8 * i; r = (tid % 32) * 4; }
+      else    { c = tid / (BMN / 4) + (NT / (BMN / 4)) * i; r = (tid % (BMN / 4)) * 4; }
       int gr = mn0 + r, gk = k0 + c;
       floatx4 x = {0.f, 0.f, 0.f, 0.f};
       if (KC) {
@@ -47,21 +49,21 @@ struct Stage {
       } else {
         if (gk < K && gr < MN) x = *(const floatx4*)(P + (long)gk * ld + gr);
       }
-      if (relu) {
-        x[0] = fmaxf(x[0], 0.f); x[1] = fmaxf(x[1], 0.f);
-        x[2] = fmaxf(x[2], 0.f); x[3] = fmaxf(x[3], 0.f);
-      }
-      v[i] = x;
+      v[i] = x;   // relu (if any) is applied at store time: here it would force a vmcnt wait
     }
   }
-  LBWN_DEV void store(float* lds, int tid) const {
+  LBWN_DEV void store(float* lds, int tid, bool relu = false) {
 #pragma unroll
     for (int i = 0; i < SREG; ++i) {
+      if (relu) {
+        v[i][0] = fmaxf(v[i][0], 0.f); v[i][1] = fmaxf(v[i][1], 0.f);
+        v[i][2] = fmaxf(v[i][2], 0.f); v[i][3] = fmaxf(v[i][3], 0.f);
+      }
       if (KC) {
         int r = tid / (BK / 4) + (NT / (BK / 4)) * i, c = (tid % (BK / 4)) * 4;
         *(floatx4*)(lds + r * KCS + c) = v[i];
       }
-      else    { int c = tid / 32 + 8 * i, r = (tid % 32) * 4; *(floatx4*)(lds + c * RS + r) = v[i]; }
+      else    { int c = tid / (BMN / 4) + (NT / (BMN / 4)) * i, r = (tid % (BMN / 4)) * 4; *(floatx4*)(lds + c * RS + r) = v[i]; }
     }
   }
   // fragment for rows [base, base+32) of group g: element j = value at k = 8g+4h+j
@@ -82,8 +84,10 @@ LBWN_DEV int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
-template <bool A_KC, bool B_KC, int BK>
+// Block tile BMT × BNT, 4 waves as 2 × 2, each wave (BMT/2) × (BNT/2) = MI × NI MFMA tiles.
+template <bool A_KC, bool B_KC, int BK, int BMT, int BNT>
 __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(lbwn_gemm_args g) {
+  constexpr int BM = BMT, BN = BNT, MI = BMT / 64, NI = BNT / 64;
   using SA = Stage<A_KC, BM, BK>;
   using SB = Stage<B_KC, BN, BK>;
   __shared__ __attribute__((aligned(16))) float smem[2 * (SA::LDS_FLOATS + SB::LDS_FLOATS)];
@@ -99,11 +103,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(lbwn_gemm_args g) {
   const int kz1 = min(g.K, kz0 + g.k_per_split);
   const int ntiles = (kz1 - kz0 + BK - 1) / BK;
 
-  floatx16 acc[2][2];
+  floatx16 acc[MI][NI];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < MI; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < NI; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
@@ -112,7 +116,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(lbwn_gemm_args g) {
   if (ntiles > 0) {
     sa.load(g.A, g.lda, m0, g.M, kz0, kz1, tid, g.relu_a, g.a_codes);
     sb.load(g.B, g.ldb, n0, g.N, kz0, kz1, tid, false);
-    sa.store(As(0), tid);
+    sa.store(As(0), tid, g.relu_a);
     sb.store(Bs(0), tid);
   }
   __syncthreads();
@@ -125,20 +129,20 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(lbwn_gemm_args g) {
     }
 #pragma unroll
     for (int gg = 0; gg < BK / 8; ++gg) {
-      floatx4 fa[2], fb[2];
+      floatx4 fa[MI], fb[NI];
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi) fa[mi] = sa.frag(As(cur), wm * 64 + mi * 32, gg, lane);
+      for (int mi = 0; mi < MI; ++mi) fa[mi] = sa.frag(As(cur), wm * (BM / 2) + mi * 32, gg, lane);
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni) fb[ni] = sb.frag(Bs(cur), wn * 64 + ni * 32, gg, lane);
+      for (int ni = 0; ni < NI; ++ni) fb[ni] = sb.frag(Bs(cur), wn * (BN / 2) + ni * 32, gg, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
+        for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = mfma32(fa[mi][j], fb[ni][j], acc[mi][ni]);
+          for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = mfma32(fa[mi][j], fb[ni][j], acc[mi][ni]);
     }
     if (kt + 1 < ntiles) {
-      sa.store(As(cur ^ 1), tid);
+      sa.store(As(cur ^ 1), tid, g.relu_a);
       sb.store(Bs(cur ^ 1), tid);
     }
     __syncthreads();
@@ -149,15 +153,15 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(lbwn_gemm_args g) {
   float* C = g.C + (long)blockIdx.z * g.split_stride;
   const bool raw = g.split_stride != 0;
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
+  for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      const int col = n0 + wn * 64 + ni * 32 + ci;
+    for (int ni = 0; ni < NI; ++ni) {
+      const int col = n0 + wn * (BN / 2) + ni * 32 + ci;
       if (col >= g.N) continue;
       const float bv = (!raw && g.bias) ? g.bias[col] : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * 64 + mi * 32 + acc_row(r, h);
+        const int row = m0 + wm * (BM / 2) + mi * 32 + acc_row(r, h);
         if (row >= g.M) continue;
         float v = acc[mi][ni][r];
         const long o = (long)row * g.ldc + col;
@@ -196,8 +200,9 @@ __global__ void splitk_reduce_kernel(lbwn_gemm_args g, const float* __restrict__
 }  // namespace
 
 namespace {
-template <int BK>
+template <int BK, int BMT, int BNT>
 int gemm_launch_t(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws, hipStream_t st) {
+  constexpr int BM = BMT, BN = BNT;
   LBWN_REQUIRE(a.M > 0 && a.N > 0 && a.K > 0, "gemm: empty shape M=%d N=%d K=%d", a.M, a.N, a.K);
   LBWN_REQUIRE(a.K % 4 == 0 || !a_kcontig, "gemm: K %% 4 != 0 with k-contiguous A");
   LBWN_REQUIRE(a.K % 4 == 0 || !b_kcontig, "gemm: K %% 4 != 0 with k-contiguous B");
@@ -223,10 +228,10 @@ int gemm_launch_t(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int spl
   } else {
     g.split_stride = 0;
   }
-  if (a_kcontig && b_kcontig) gemm_f32_kernel<true, true, BK><<<grid, NT, 0, st>>>(g);
-  else if (a_kcontig) gemm_f32_kernel<true, false, BK><<<grid, NT, 0, st>>>(g);
-  else if (b_kcontig) gemm_f32_kernel<false, true, BK><<<grid, NT, 0, st>>>(g);
-  else gemm_f32_kernel<false, false, BK><<<grid, NT, 0, st>>>(g);
+  if (a_kcontig && b_kcontig) gemm_f32_kernel<true, true, BK, BMT, BNT><<<grid, NT, 0, st>>>(g);
+  else if (a_kcontig) gemm_f32_kernel<true, false, BK, BMT, BNT><<<grid, NT, 0, st>>>(g);
+  else if (b_kcontig) gemm_f32_kernel<false, true, BK, BMT, BNT><<<grid, NT, 0, st>>>(g);
+  else gemm_f32_kernel<false, false, BK, BMT, BNT><<<grid, NT, 0, st>>>(g);
   LBWN_CHECK_LAUNCH();
   if (split_k > 1) {
     const long total = (long)a.M * (a.N / 4);
@@ -240,10 +245,14 @@ int gemm_launch_t(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int spl
 
 int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                      hipStream_t st) {
-  return gemm_launch_t<16>(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
+  // tall products (M = B·T positions): 256 × 128 block tiles, each wave 128 × 64
+  static const char* env = getenv("LBWN_GEMM_TILE");
+  const bool tall = (env && env[0] == '2') && a.M >= 8192 && split_k <= 1;   // measured slower: opt-in
+  if (tall) return gemm_launch_t<16, 256, 128>(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
+  return gemm_launch_t<16, 128, 128>(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
 }
 
 int lbwn_gemm_launch_lean(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                           hipStream_t st) {
-  return gemm_launch_t<8>(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
+  return gemm_launch_t<8, 128, 128>(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
 }

@@ -28,7 +28,10 @@ def timeit(fn, reps=20):
     return s.elapsed_time(e) / reps * 1e-3
 
 
+only = os.environ.get('GEMM_ONLY')
 for name, m, n, k, akc, bkc, split in SHAPES:
+    if only and name not in only.split(','):
+        continue
     A = torch.randn(m, k, device='cuda') if akc else torch.randn(k, m, device='cuda')
     B = torch.randn(n, k, device='cuda') if bkc else torch.randn(k, n, device='cuda')
     C = torch.empty(m, n, device='cuda')
