@@ -5,12 +5,13 @@
 // form of the D-separation cache: layer l keeps its last d inputs, slot t mod d, replacing
 // imodel's shift-by-chunk buffers imodel.py:88-98, :190-207), the next input code, the
 // teacher vector and a counter-based RNG.  One step =
-//   gen_chain   1 workgroup per 16 streams: PRE row (+bias), 50 × [dilated conv (VALU; B is
-//               ~10 so a 32-wide MFMA tile would be mostly padding), gate, residual], z_cat out
-//   gen_rowvec  × 3: skip = z_cat·SKIPcat + Σb, h = relu(relu(skip)·POST1 + b1),
-//               logits = h·POST2 + b2 (weights L2-resident across steps)
-//   gen_sample  inverse-CDF draw of softmax(logits) with u = hash(seed, stream, step),
-//               µ-law decode, next input = teacher[t] or the draw (imodel.py:167-187, :260-269)
+//   gen_wave     one wave per stream, no barriers: PRE row (+bias), 50 × [dilated conv
+//                (lane = output channel, 64-term dot over LDS broadcasts), gate (lane pairs),
+//                residual], weights from a lane-coalesced image prefetched a layer ahead
+//   gen_gemv × 3 K-split row-vector products with deterministic partial sums:
+//                skip = z_cat·SKIPcat, h = relu(relu(skip + Σb)·POST1 + b1), logits = h·POST2
+//   gen_sample   logits = Σ partials + b2; inverse-CDF draw with u = hash(seed, stream, step),
+//                µ-law decode, next input = teacher[t] or the draw (imodel.py:167-187, :260-269)
 #include <math.h>
 #include <string.h>
 
@@ -21,252 +22,245 @@
 
 namespace {
 
-constexpr int GB = 16;                 // streams per chain workgroup
-constexpr int RV_MAXI = 32;            // row-vector GEMM: K <= 64·32 = 2048
-constexpr int WIMG_G = 64 * 64 + 32 * 32 + 96;  // conv W[k][o] (64×64) | RES[c][o] (32×32) | b_conv[64] | b_res[32]
 
-struct ChainK {
-  const float* pre; const float* pre_b;
-  const float* sig; const float* gate; const float* sig_b; const float* gate_b;
-  const float* res; const float* res_b;
-  const float* gc_proj;   // [L][B][64] or null
-  float* rings;           // packed per layer [B][d][Cr]
-  float* zcat;            // [B][L*Cd]
-  const long long* step;  // current step t
-  int* code;              // [B] input code for this step (-1 = zero vector)
-  int B, L, nbl, Cr, Cd, Q, pre_bias;
-};
+// Wave-level LDS sync for single-wave workgroups: orders the wave's own LDS traffic without
+// the vmcnt(0) that __syncthreads() implies (which would also wait for the next layer's
+// weight prefetch, putting its L2 latency back on the chain).
+LBWN_DEV void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Σ_q p[q·stride], q < n: independent loads in batches of 8 (a plain loop waits on each)
+LBWN_DEV float sum_parts(const float* p, long stride, int n) {
+  float s = 0.f;
+  int q = 0;
+  for (; q + 8 <= n; q += 8) {
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = p[(q + i) * stride];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += v[i];
+  }
+  for (; q < n; ++q) s += p[q * stride];
+  return s;
+}
 
 LBWN_DEV long ring_offset(int l, int nbl, int B, int Cr) {
   const long s = (long)(l / nbl) * ((1L << nbl) - 1) + ((1L << (l % nbl)) - 1);
   return s * B * Cr;
 }
 
-// stage layer l's weights (reference layouts) into registers -> LDS image
-struct WStage {
-  static constexpr int N = (WIMG_G + 1023) / 1024;  // 6 per thread
-  float v[N];
-  LBWN_DEV void load(const ChainK& a, int l, int tid) {
-    const int Cr = a.Cr, Cd = a.Cd;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int e = tid + 1024 * i;
-      float x = 0.f;
-      if (e < 64 * 64) {
-        const int k = e >> 6, o = e & 63, tap = k >> 5, in = k & 31, oc = o & 31;
-        if (in < Cr && oc < Cd) x = (o < 32 ? a.sig : a.gate)[(long)l * 2 * Cr * Cd + (tap * Cr + in) * Cd + oc];
-      } else if (e < 64 * 64 + 32 * 32) {
-        const int f = e - 64 * 64, c = f >> 5, o = f & 31;
-        if (c < Cd && o < Cr) x = a.res[(long)l * Cd * Cr + c * Cr + o];
-      } else if (e < WIMG_G) {
-        const int f = e - 64 * 64 - 32 * 32;
-        if (f < 64) {
-          const float* bb = f < 32 ? a.sig_b : a.gate_b;
-          if (bb && (f & 31) < Cd) x = bb[(long)l * Cd + (f & 31)];
-        } else if (a.res_b && f - 64 < Cr) {
-          x = a.res_b[(long)l * Cr + f - 64];
-        }
-      }
-      v[i] = x;
-    }
-  }
-  LBWN_DEV void store(float* W, int tid) const {
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int e = tid + 1024 * i;
-      if (e < WIMG_G) W[e] = v[i];
-    }
-  }
+// ---- per-stream wave chain ---------------------------------------------------------------
+// One wave per stream, no barriers: lane o computes conv output o (sig 0-31 | gate 32-63) as
+// a 64-term dot product over [x[t-d] | x[t]] (LDS broadcasts), the gate pairs lane o with
+// lane o+32 (shuffle), the residual reads z back through wave-private LDS.  Weights come
+// from a lane-coalesced per-layer image (packed once per gen_start) as 26 16-B loads per
+// lane, prefetched one layer ahead into a register double buffer.
+constexpr int GI_W = 16 * 64 * 4;           // conv: [kq 16][lane 64][4]  W[4kq+j][lane]
+constexpr int GI_R = 8 * 64 * 4;            // residual: [cq 8][lane 64][4] RES[4cq+j][lane] (lane < 32)
+constexpr int GIMG = GI_W + GI_R + 128;     // + conv bias [64] + residual bias [64]
+
+struct LayerRegs {
+  floatx4 w[16];
+  floatx4 r[8];
+  float bc, br, gc;
 };
 
-// LDS: all L layers' lookback taps (read once, up front), 2 weight images, x/z rows,
-// conv partials over 2 K-halves.  GBS streams per workgroup (16, or 8 for deep stacks).
-template <int GBS>
-__global__ __launch_bounds__(1024) void gen_chain_kernel(ChainK a) {
+struct WaveK {
+  const float* pre; const float* pre_b; const float* img; const float* gc_proj;
+  float* rings; float* zcat; const long long* step; const int* code;
+  int B, L, nbl, Cr, Cd, pre_bias;
+};
+
+LBWN_DEV void load_layer(LayerRegs& R, const WaveK& a, int l, int b, int lane) {
+  const float* base = a.img + (long)l * GIMG;
+#pragma unroll
+  for (int kq = 0; kq < 16; ++kq) R.w[kq] = *(const floatx4*)(base + (kq * 64 + lane) * 4);
+#pragma unroll
+  for (int cq = 0; cq < 8; ++cq) R.r[cq] = *(const floatx4*)(base + GI_W + (cq * 64 + lane) * 4);
+  R.bc = base[GI_W + GI_R + lane];
+  R.br = base[GI_W + GI_R + 64 + lane];
+  R.gc = a.gc_proj ? a.gc_proj[((long)l * a.B + b) * 64 + lane] : 0.f;
+}
+
+LBWN_DEV float dot4(const floatx4& w, const floatx4& x, float acc) {
+  acc = fmaf(w[0], x[0], acc);
+  acc = fmaf(w[1], x[1], acc);
+  acc = fmaf(w[2], x[2], acc);
+  return fmaf(w[3], x[3], acc);
+}
+
+__global__ __launch_bounds__(64) void gen_wave_kernel(WaveK a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* Wb0 = sm;
-  float* Wb1 = sm + WIMG_G;
-  float* X = Wb1 + WIMG_G;          // [GBS][32]
-  float* Z = X + GBS * 32;          // [GBS][32]
-  float* P = Z + GBS * 32;          // [2][GBS][64]
-  float* PV = P + 2 * GBS * 64;     // [L][GBS][32]
-  const int tid = threadIdx.x;
-  const int b0 = blockIdx.x * GBS;
-  const int nb = min(GBS, a.B - b0);
+  float* XP = sm;                    // [L][32] dilated taps of this step
+  float* X = XP + a.L * 32;          // [32] current layer input
+  float* Z = X + 32;                 // [32] gate output
+  const int lane = threadIdx.x, b = blockIdx.x;
   const long t = *a.step;
-  const int Cr = a.Cr, Cd = a.Cd, L = a.L;
-
-  WStage ws;
-  ws.load(a, 0, tid);
-  // every layer's prev tap: input of layer l at t - d_l (ring slot t mod d_l, zero-initialised)
+  const int Cr = a.Cr, L = a.L;
+  LayerRegs RA, RB;
+  load_layer(RA, a, 0, b, lane);
+  // every layer's tap: input of layer l at t - d_l (ring slot t mod d, zero-initialised).
+  // d is a power of two: slot = t & (d-1); ring offsets accumulate (no integer division)
   {
-    const int n = L * GBS * 32;
-    for (int base = tid; base < n; base += 1024 * 8) {
-      float v[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int e = base + 1024 * i;
-        v[i] = 0.f;
-        if (e < n) {
-          const int l = e / (GBS * 32), r = e % (GBS * 32), b = r >> 5, c = r & 31;
-          const int d = 1 << (l % a.nbl);
-          if (b < nb && c < Cr) v[i] = a.rings[ring_offset(l, a.nbl, a.B, Cr) + ((long)(b0 + b) * d + (t % d)) * Cr + c];
-        }
+    long roff = 0;
+    int bl = 0;
+    for (int l = 0; l < L; ++l) {
+      const int d = 1 << bl;
+      if ((lane >> 5) == (l & 1) && (lane & 31) < Cr) {
+        const int c = lane & 31;
+        XP[l * 32 + c] = a.rings[roff + ((long)b * d + (t & (d - 1))) * Cr + c];
+      } else if ((lane >> 5) == (l & 1)) {
+        XP[l * 32 + (lane & 31)] = 0.f;
       }
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (base + 1024 * i < n) PV[base + 1024 * i] = v[i];
+      roff += (long)d * a.B * Cr;
+      bl = (bl + 1 == a.nbl) ? 0 : bl + 1;
     }
   }
-  // input z0 = onehot(code)·PRE (+ PRE_BIAS): zero vector at step 0 (imodel.py:61-79)
-  if (tid < GBS * 32) {
-    const int b = tid >> 5, c = tid & 31;
-    float v = 0.f;
-    if (b < nb && c < Cr) {
-      const int code = a.code[b0 + b];
-      if (code >= 0) v = a.pre[(long)code * Cr + c];
-      if (a.pre_bias && a.pre_b) v += a.pre_b[c];
+  // step input: PRE row of the previous draw (+ PRE_BIAS); the zero vector at step 0
+  float xr = 0.f;   // lane c < 32: x[c] of the current layer input
+  if (lane < 32) {
+    if (lane < Cr) {
+      const int code = a.code[b];
+      if (code >= 0) xr = a.pre[(long)code * Cr + lane];
+      if (a.pre_bias && a.pre_b) xr += a.pre_b[lane];
     }
-    X[tid] = v;
+    X[lane] = xr;
   }
-  ws.store(Wb0, tid);
-  __syncthreads();
+  wave_sync();
 
-  constexpr int SPG = GBS / 8;   // streams per conv thread
-  for (int l = 0; l < L; ++l) {
-    const float* W = (l & 1) ? Wb1 : Wb0;
-    float* Wn = (l & 1) ? Wb0 : Wb1;
-    const float* pv = PV + l * GBS * 32;
-    if (l + 1 < L) ws.load(a, l + 1, tid);   // next layer's weights land during this layer
-    // ring write: this layer's input becomes the tap of step t + d (slot t mod d)
-    if (tid < GBS * 32) {
-      const int b = tid >> 5, c = tid & 31;
-      const int d = 1 << (l % a.nbl);
-      if (b < nb && c < Cr)
-        a.rings[ring_offset(l, a.nbl, a.B, Cr) + ((long)(b0 + b) * d + (t % d)) * Cr + c] = X[tid];
-    }
-    // conv partials: thread (o, K-half kh, stream group bg): SPG streams × 32 k
-    {
-      const int o = tid & 63, kh = (tid >> 6) & 1, bg = tid >> 7;
-      const float* xin = kh ? X : pv;
-      float acc[SPG];
+  long roff = 0;   // ring offset of layer l
+  int bl = 0;      // l % nbl
+  auto layer = [&](int l, LayerRegs& R, LayerRegs& N) {
+    if (l + 1 < L) load_layer(N, a, l + 1, b, lane);
+    const int d = 1 << bl;
+    if (lane < Cr) a.rings[roff + ((long)b * d + (t & (d - 1))) * Cr + lane] = xr;
+    roff += (long)d * a.B * Cr;
+    bl = (bl + 1 == a.nbl) ? 0 : bl + 1;
+    const float* xp = XP + l * 32;
+    float acc0 = R.bc + R.gc, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
 #pragma unroll
-      for (int j = 0; j < SPG; ++j) acc[j] = 0.f;
-#pragma unroll 8
-      for (int k = 0; k < 32; ++k) {
-        const float w = W[(kh * 32 + k) * 64 + o];
+    for (int kq = 0; kq < 8; kq += 2) {
+      acc0 = dot4(R.w[kq], *(const floatx4*)(xp + 4 * kq), acc0);
+      acc1 = dot4(R.w[kq + 1], *(const floatx4*)(xp + 4 * kq + 4), acc1);
+    }
 #pragma unroll
-        for (int j = 0; j < SPG; ++j) acc[j] = fmaf(xin[(bg * SPG + j) * 32 + k], w, acc[j]);
-      }
+    for (int kq = 0; kq < 8; kq += 2) {
+      acc2 = dot4(R.w[8 + kq], *(const floatx4*)(X + 4 * kq), acc2);
+      acc3 = dot4(R.w[8 + kq + 1], *(const floatx4*)(X + 4 * kq + 4), acc3);
+    }
+    const float v = (acc0 + acc1) + (acc2 + acc3);
+    const float vg = __shfl_xor(v, 32);
+    const float z = tanhf_(v) * sigmoidf_(vg);      // valid on lanes < 32 (padded channels: v = 0 -> z = 0)
+    if (lane < a.Cd) a.zcat[(long)b * L * a.Cd + (long)l * a.Cd + lane] = z;
+    if (lane < 32) Z[lane] = z;
+    wave_sync();
+    float r0 = R.br, r1 = 0.f;
 #pragma unroll
-      for (int j = 0; j < SPG; ++j) P[(kh * GBS + bg * SPG + j) * 64 + o] = acc[j];
+    for (int cq = 0; cq < 8; cq += 2) {
+      r0 = dot4(R.r[cq], *(const floatx4*)(Z + 4 * cq), r0);
+      r1 = dot4(R.r[cq + 1], *(const floatx4*)(Z + 4 * cq + 4), r1);
     }
-    __syncthreads();
-    // gate
-    if (tid < GBS * 32) {
-      const int b = tid >> 5, c = tid & 31;
-      const float* bs = W + 64 * 64 + 32 * 32;
-      float vs = bs[c] + P[b * 64 + c] + P[(GBS + b) * 64 + c];
-      float vg = bs[32 + c] + P[b * 64 + 32 + c] + P[(GBS + b) * 64 + 32 + c];
-      if (a.gc_proj && b < nb) {
-        const float* g = a.gc_proj + ((long)l * a.B + b0 + b) * 64;
-        vs += g[c];
-        vg += g[32 + c];
-      }
-      const float z = (c < Cd && b < nb) ? tanhf_(vs) * sigmoidf_(vg) : 0.f;
-      Z[tid] = z;
-      if (b < nb && c < Cd) a.zcat[(long)(b0 + b) * L * Cd + l * Cd + c] = z;
-    }
-    __syncthreads();
-    // residual: x += z·RES + b
-    if (tid < GBS * 32) {
-      const int b = tid >> 5, o = tid & 31;
-      const float* R = W + 64 * 64;
-      float r = W[64 * 64 + 32 * 32 + 64 + o];   // b_res
-#pragma unroll 8
-      for (int c = 0; c < 32; ++c) r = fmaf(Z[b * 32 + c], R[c * 32 + o], r);
-      X[tid] += r;
-    }
-    if (l + 1 < L) ws.store(Wn, tid);
-    __syncthreads();
+    xr += r0 + r1;
+    if (lane < 32) X[lane] = xr;
+    wave_sync();
+  };
+  for (int l = 0; l < L; l += 2) {
+    layer(l, RA, RB);
+    if (l + 1 < L) layer(l + 1, RB, RA);
   }
 }
 
-size_t chain_lds_bytes(int gbs, int L) { return 4 * (size_t)(2 * WIMG_G + 2 * gbs * 32 + 2 * gbs * 64 + (size_t)L * gbs * 32); }
+// per-layer lane-coalesced weight image (reference layouts in, GIMG floats per layer out)
+__global__ void gen_pack_kernel(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
+                                const float* res, const float* res_b, float* img, int Cr, int Cd) {
+  const int l = blockIdx.x;
+  float* o = img + (long)l * GIMG;
+  for (int e = threadIdx.x; e < GIMG; e += blockDim.x) {
+    float v = 0.f;
+    if (e < GI_W) {
+      const int kq = e / 256, lane = (e % 256) / 4, j = e % 4, k = 4 * kq + j;
+      const int tap = k >> 5, in = k & 31, oc = lane & 31;
+      if (in < Cr && oc < Cd) v = (lane < 32 ? sig : gate)[(long)l * 2 * Cr * Cd + (tap * Cr + in) * Cd + oc];
+    } else if (e < GI_W + GI_R) {
+      const int f = e - GI_W, cq = f / 256, lane = (f % 256) / 4, j = f % 4, c = 4 * cq + j;
+      if (lane < Cr && c < Cd) v = res[(long)l * Cd * Cr + c * Cr + lane];
+    } else {
+      const int f = e - GI_W - GI_R;
+      if (f < 64) {
+        const float* bb = f < 32 ? sig_b : gate_b;
+        if (bb && (f & 31) < Cd) v = bb[(long)l * Cd + (f & 31)];
+      } else if (res_b && f - 64 < Cr) {
+        v = res_b[(long)l * Cr + f - 64];
+      }
+    }
+    o[e] = v;
+  }
+}
 
-// out[b][n] = epi( Σ_k act(in[b][k])·W[k][n] + bias ), b < B (≤ 64 per launch row loop),
-// block = 4 columns; thread (c = tid & 3, ks = tid >> 2): K slice, all streams.
-struct RowK {
-  const float* in; long ldin; const float* W; long ldw; float* out; long ldout;
-  const float* bias;                  // [N] nullable
-  int B, K, N, relu_in, relu_out;
+// ---- K-split row-vector GEMV --------------------------------------------------------------
+// part[ks][b][n] = Σ_{k in slice ks} act(in[b][k])·W[k][n]: block = 64 columns (lane = n) ×
+// one K slice, 4 waves over the slice's rows.  The input is either a plain [B][K] row buffer
+// or the previous GEMV's partials, summed here in a fixed order (+ bias, relu): the chain of
+// skip -> post1 -> post2 -> sample stays deterministic without atomics.
+constexpr int GV_KSL_MAX = 64;   // K rows per slice (runtime KSL <= this, multiple of 4)
+
+struct GemvK {
+  const float* in; long ldin;                   // plain input rows, or
+  const float* in_part; int in_parts;           // partials [in_parts][B][K]
+  const float* in_bias; int relu_in;            // applied after the sum
+  const float* W; long ldw;
+  float* out_part;                              // [ceil(K/KSL)][B][N]
+  int B, K, N, KSL;
 };
 
-__global__ __launch_bounds__(256) void gen_rowvec_kernel(RowK a) {
-  extern __shared__ __attribute__((aligned(16))) float xin[];   // [16][K] (act applied)
-  __shared__ float red[64][4][17];
-  const int c = threadIdx.x & 3, ks = threadIdx.x >> 2;  // 64 K slices
-  const int n = blockIdx.x * 4 + c;
-  float acc[16];
-  // every weight of this thread's K slice is issued first (K <= 64·RV_MAXI); it lands while
-  // the activations are staged
-  float wr[RV_MAXI];
+__global__ __launch_bounds__(256) void gen_gemv_kernel(GemvK a) {
+  __shared__ __attribute__((aligned(16))) float xs[16][GV_KSL_MAX];
+  __shared__ float red[4][16][64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int n = blockIdx.x * 64 + lane;
+  const int KSL = a.KSL, ks = blockIdx.y, k0 = ks * KSL, k1 = min(a.K, k0 + KSL);
+  float wr[GV_KSL_MAX / 4];
 #pragma unroll
-  for (int i = 0; i < RV_MAXI; ++i) {
-    const int k = ks + 64 * i;
-    wr[i] = (n < a.N && k < a.K) ? a.W[(long)k * a.ldw + n] : 0.f;
+  for (int i = 0; i < GV_KSL_MAX / 4; ++i) {
+    const int k = k0 + w + 4 * i;
+    wr[i] = (4 * i < KSL && k < k1 && n < a.N) ? a.W[(long)k * a.ldw + n] : 0.f;
   }
-  for (int bb0 = 0; bb0 < a.B; bb0 += 16) {
-    const int nbb = min(16, a.B - bb0);
-    {
-      const int nf4 = 16 * a.K / 4;   // K % 4 == 0, ldin % 4 == 0
-      for (int base = threadIdx.x; base < nf4; base += 256 * 8) {
-        floatx4 v[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int e = base + 256 * i;
-          v[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-          if (e < nf4) {
-            const int j = (4 * e) / a.K, k = (4 * e) % a.K;
-            if (j < nbb) {
-              v[i] = *(const floatx4*)(a.in + (long)(bb0 + j) * a.ldin + k);
-              if (a.relu_in) {
-                v[i][0] = fmaxf(v[i][0], 0.f); v[i][1] = fmaxf(v[i][1], 0.f);
-                v[i][2] = fmaxf(v[i][2], 0.f); v[i][3] = fmaxf(v[i][3], 0.f);
-              }
-            }
-          }
+  for (int b0 = 0; b0 < a.B; b0 += 16) {
+    const int nbb = min(16, a.B - b0);
+    for (int e = tid; e < 16 * KSL; e += 256) {
+      const int j = e / KSL, kk = e % KSL, k = k0 + kk;
+      float v = 0.f;
+      if (j < nbb && k < a.K) {
+        if (a.in_part) {
+          v = sum_parts(a.in_part + (long)(b0 + j) * a.K + k, (long)a.B * a.K, a.in_parts);
+          if (a.in_bias) v += a.in_bias[k];
+        } else {
+          v = a.in[(long)(b0 + j) * a.ldin + k];
         }
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if (base + 256 * i < nf4) *(floatx4*)(xin + 4 * (base + 256 * i)) = v[i];
+        if (a.relu_in) v = fmaxf(v, 0.f);
       }
+      xs[j][kk] = v;
     }
     __syncthreads();
+    float acc[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = 0.f;
-    if (n < a.N) {
 #pragma unroll
-      for (int i = 0; i < RV_MAXI; ++i) {
-        const int k = ks + 64 * i;
-        if (k < a.K) {
+    for (int i = 0; i < GV_KSL_MAX / 4; ++i)
+      if (4 * i < KSL) {
 #pragma unroll
-          for (int j = 0; j < 16; ++j) acc[j] = fmaf(xin[j * a.K + k], wr[i], acc[j]);
-        }
+        for (int j = 0; j < 16; ++j) acc[j] = fmaf(xs[j][w + 4 * i], wr[i], acc[j]);
       }
-    }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) red[ks][c][j] = acc[j];
+    for (int j = 0; j < 16; ++j) red[w][j][lane] = acc[j];
     __syncthreads();
-    if (threadIdx.x < 64) {
-      const int cc = threadIdx.x & 3, j = threadIdx.x >> 2;
-      const int nn = blockIdx.x * 4 + cc;
-      if (nn < a.N && j < nbb) {
-        float s = a.bias ? a.bias[nn] : 0.f;
-        for (int q = 0; q < 64; ++q) s += red[q][cc][j];
-        if (a.relu_out) s = fmaxf(s, 0.f);
-        a.out[(long)(bb0 + j) * a.ldout + nn] = s;
-      }
+    for (int e = tid; e < 16 * 64; e += 256) {
+      const int j = e >> 6, c = e & 63, nn = blockIdx.x * 64 + c;
+      if (j < nbb && nn < a.N)
+        a.out_part[((long)ks * a.B + b0 + j) * a.N + nn] = ((red[0][j][c] + red[1][j][c]) + red[2][j][c]) + red[3][j][c];
     }
     __syncthreads();
   }
@@ -280,7 +274,8 @@ LBWN_DEV uint64_t splitmix(uint64_t seed, uint64_t stream, uint64_t step) {
 }
 
 struct SampleK {
-  const float* logits; int Q, B;
+  float* logits; int Q, B;
+  const float* log_part; int parts; const float* bias;   // logits = Σ parts + bias (written to logits)
   long long* step; int* code; const int* teacher; long long n_teacher;
   int* samples; float* wav; long long max_steps; unsigned long long seed;
 };
@@ -288,10 +283,18 @@ struct SampleK {
 // one block; wave w handles streams w, w+16, ...: softmax CDF in a fixed order, first k with
 // cumsum(e)[k] > u·Σe (oracle/wavenet_ref.py sample_from_logits restates the same transform).
 __global__ __launch_bounds__(1024) void gen_sample_kernel(SampleK a) {
+  extern __shared__ float lgs[];   // [16][Q]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const long long t = *a.step;
   for (int b = w; b < a.B; b += 16) {
-    const float* lg = a.logits + (long)b * a.Q;
+    float* lg = lgs + w * a.Q;
+    for (int c = lane; c < a.Q; c += 64) {
+      float v = sum_parts(a.log_part + (long)b * a.Q + c, (long)a.B * a.Q, a.parts);
+      if (a.bias) v += a.bias[c];
+      lg[c] = v;
+      a.logits[(long)b * a.Q + c] = v;
+    }
+    wave_sync();
     float mx = -INFINITY;
     for (int c = lane; c < a.Q; c += 64) mx = fmaxf(mx, lg[c]);
 #pragma unroll
@@ -376,7 +379,8 @@ struct lbwn_gen_plan {
   lbwn_arch a;
   int B, L, nbl, Cr, Cd, Cs, Cp, Q;
   long long max_steps;
-  size_t oRING, oZCAT, oSKIP, oH, oLOG, oSTEP, oCODE, oTEACH, oSAMP, oWAV, oGCP, oBSUM, total;
+  size_t oRING, oZCAT, oSKP, oHP, oLGP, oLOG, oSTEP, oCODE, oTEACH, oSAMP, oWAV, oGCP, oBSUM, oGIMG, total;
+  int ksl_skip, ks_skip, ks_h, ks_lg;
   long n_ring;
   long long n_teacher, max_teacher;
   unsigned long long seed;
@@ -393,10 +397,7 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
                                     lbwn_gen_plan** out) {
   LBWN_REQUIRE(a && out && B >= 1 && max_steps >= 1 && max_teacher >= 0, "gen_plan_create: bad arguments");
   LBWN_REQUIRE(a->n_res <= 32 && a->n_dil <= 32, "gen: n_res/n_dil must be <= 32");
-  LBWN_REQUIRE(a->n_skip % 4 == 0 && a->n_post % 4 == 0 && ((long)a->n_blocks * a->n_block_layers * a->n_dil) % 4 == 0,
-               "gen: row-vector GEMM needs K %% 4 == 0");
-  LBWN_REQUIRE((long)a->n_blocks * a->n_block_layers * a->n_dil <= 2048 && a->n_skip <= 2048 && a->n_post <= 2048,
-               "gen: row-vector GEMM K too large for LDS staging");
+  LBWN_REQUIRE(a->n_blocks * a->n_block_layers * 32 * 4 + 256 <= 64 * 1024, "gen: too many layers for the tap cache");
   LBWN_REQUIRE(a->n_lc_out == 0, "gen: local conditioning is not supported by the cached generator "
                                  "(imodel.py has no LC path)");
   lbwn_gen_plan* p = new lbwn_gen_plan();
@@ -412,8 +413,14 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
   size_t cur = 0;
   p->oRING = gcarve(cur, 4 * (size_t)p->n_ring);
   p->oZCAT = gcarve(cur, 4 * (size_t)B * p->L * p->Cd);
-  p->oSKIP = gcarve(cur, 4 * (size_t)B * p->Cs);
-  p->oH = gcarve(cur, 4 * (size_t)B * p->Cp);
+  // K-split GEMV partials: skip (K = L·Cd, 64-row slices), post1 and post2 (32-row slices)
+  p->ksl_skip = 64;
+  p->ks_skip = (p->L * p->Cd + p->ksl_skip - 1) / p->ksl_skip;
+  p->ks_h = (p->Cs + 31) / 32;
+  p->ks_lg = (p->Cp + 31) / 32;
+  p->oSKP = gcarve(cur, 4 * (size_t)p->ks_skip * B * p->Cs);
+  p->oHP = gcarve(cur, 4 * (size_t)p->ks_h * B * p->Cp);
+  p->oLGP = gcarve(cur, 4 * (size_t)p->ks_lg * B * p->Q);
   p->oLOG = gcarve(cur, 4 * (size_t)B * p->Q);
   p->oSTEP = gcarve(cur, 8);
   p->oCODE = gcarve(cur, 4 * (size_t)B);
@@ -422,6 +429,7 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
   p->oWAV = gcarve(cur, 4 * (size_t)B * max_steps);
   p->oGCP = gcarve(cur, 4 * (size_t)p->L * B * 64);
   p->oBSUM = gcarve(cur, 4 * (size_t)p->Cs);
+  p->oGIMG = gcarve(cur, 4 * (size_t)p->L * GIMG);
   p->total = cur;
   *out = p;
   return 0;
@@ -469,6 +477,9 @@ extern "C" int lbwn_gen_start(lbwn_gen_plan* p, const lbwn_params* P, void* ws, 
   if (P->skip_b) {
     if (int e = lbwn_sum_bias_launch(P->skip_b, p->L, p->Cs, gat<float>(ws, p->oBSUM), st)) return e;
   }
+  gen_pack_kernel<<<p->L, 256, 0, st>>>(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b, gat<float>(ws, p->oGIMG),
+                                        p->Cr, p->Cd);
+  LBWN_CHECK_LAUNCH();
   if (p->a.n_gc_embed > 0) {
     gen_gc_proj_kernel<<<p->L, 256, 0, st>>>(P->gc_embed, P->gc_sig, P->gc_gate, gc_ids, gat<float>(ws, p->oGCP),
                                              p->B, p->a.n_gc_embed, p->Cd);
@@ -480,37 +491,39 @@ extern "C" int lbwn_gen_start(lbwn_gen_plan* p, const lbwn_params* P, void* ws, 
 extern "C" int lbwn_gen_run(lbwn_gen_plan* p, const lbwn_params* P, void* ws, int n_steps, void* stream) {
   LBWN_REQUIRE(p && P && ws && n_steps >= 0, "gen_run: bad arguments");
   hipStream_t st = (hipStream_t)stream;
-  ChainK c;
-  c.pre = P->pre; c.pre_b = P->pre_b; c.sig = P->sig; c.gate = P->gate; c.sig_b = P->sig_b; c.gate_b = P->gate_b;
-  c.res = P->res; c.res_b = P->res_b;
+  WaveK c;
+  c.pre = P->pre; c.pre_b = P->pre_b; c.img = gat<float>(ws, p->oGIMG);
   c.gc_proj = p->a.n_gc_embed > 0 ? gat<float>(ws, p->oGCP) : nullptr;
   c.rings = gat<float>(ws, p->oRING); c.zcat = gat<float>(ws, p->oZCAT);
   c.step = gat<long long>(ws, p->oSTEP); c.code = gat<int>(ws, p->oCODE);
-  c.B = p->B; c.L = p->L; c.nbl = p->nbl; c.Cr = p->Cr; c.Cd = p->Cd; c.Q = p->Q; c.pre_bias = p->pre_bias;
-  RowK sk, p1, p2;
-  sk.in = c.zcat; sk.ldin = (long)p->L * p->Cd; sk.W = P->skip; sk.ldw = p->Cs; sk.out = gat<float>(ws, p->oSKIP);
-  sk.ldout = p->Cs; sk.bias = P->skip_b ? gat<float>(ws, p->oBSUM) : nullptr; sk.B = p->B; sk.K = p->L * p->Cd; sk.N = p->Cs;
-  sk.relu_in = 0; sk.relu_out = 0;
-  p1.in = sk.out; p1.ldin = p->Cs; p1.W = P->post1; p1.ldw = p->Cp; p1.out = gat<float>(ws, p->oH); p1.ldout = p->Cp;
-  p1.bias = P->post1_b; p1.B = p->B; p1.K = p->Cs; p1.N = p->Cp; p1.relu_in = 1; p1.relu_out = 1;
-  p2.in = p1.out; p2.ldin = p->Cp; p2.W = P->post2; p2.ldw = p->Q; p2.out = gat<float>(ws, p->oLOG); p2.ldout = p->Q;
-  p2.bias = P->post2_b; p2.B = p->B; p2.K = p->Cp; p2.N = p->Q; p2.relu_in = 0; p2.relu_out = 0;
+  c.B = p->B; c.L = p->L; c.nbl = p->nbl; c.Cr = p->Cr; c.Cd = p->Cd; c.pre_bias = p->pre_bias;
+  const size_t wave_lds = 4 * ((size_t)p->L * 32 + 64);
+  // skip = z_cat·SKIPcat (+Σb and relu applied by the consumer), h = relu(relu(skip)·POST1 + b1),
+  // logits = h·POST2 + b2 (summed in the sampler)
+  GemvK sk, p1, p2;
+  memset(&sk, 0, sizeof(sk));
+  sk.in = c.zcat; sk.ldin = (long)p->L * p->Cd; sk.W = P->skip; sk.ldw = p->Cs; sk.out_part = gat<float>(ws, p->oSKP);
+  sk.B = p->B; sk.K = p->L * p->Cd; sk.N = p->Cs; sk.KSL = p->ksl_skip;
+  p1 = sk;
+  p1.in = nullptr; p1.in_part = sk.out_part; p1.in_parts = p->ks_skip; p1.in_bias = P->skip_b ? gat<float>(ws, p->oBSUM) : nullptr;
+  p1.relu_in = 1; p1.W = P->post1; p1.ldw = p->Cp; p1.out_part = gat<float>(ws, p->oHP); p1.K = p->Cs; p1.N = p->Cp; p1.KSL = 32;
+  p2 = p1;
+  p2.in_part = p1.out_part; p2.in_parts = p->ks_h; p2.in_bias = P->post1_b; p2.relu_in = 1;
+  p2.W = P->post2; p2.ldw = p->Q; p2.out_part = gat<float>(ws, p->oLGP); p2.K = p->Cp; p2.N = p->Q; p2.KSL = 32;
   SampleK sm;
-  sm.logits = p2.out; sm.Q = p->Q; sm.B = p->B; sm.step = gat<long long>(ws, p->oSTEP); sm.code = c.code;
+  sm.logits = gat<float>(ws, p->oLOG); sm.Q = p->Q; sm.B = p->B;
+  sm.log_part = p2.out_part; sm.parts = p->ks_lg; sm.bias = P->post2_b;
+  sm.step = gat<long long>(ws, p->oSTEP); sm.code = gat<int>(ws, p->oCODE);
   sm.teacher = gat<int>(ws, p->oTEACH); sm.n_teacher = p->n_teacher; sm.samples = gat<int>(ws, p->oSAMP);
   sm.wav = gat<float>(ws, p->oWAV); sm.max_steps = p->max_steps; sm.seed = p->seed;
-  const bool wide = chain_lds_bytes(16, p->L) <= 160 * 1024;
-  const int gbs = wide ? 16 : 8;
-  LBWN_REQUIRE(chain_lds_bytes(gbs, p->L) <= 160 * 1024, "gen: too many layers for the LDS tap cache");
-  const int gchain = (p->B + gbs - 1) / gbs;
-  const size_t lds = chain_lds_bytes(gbs, p->L);
+  const dim3 gsk((sk.N + 63) / 64, p->ks_skip), gp1((p1.N + 63) / 64, (p1.K + 31) / 32), gp2((p2.N + 63) / 64, (p2.K + 31) / 32);
+  const size_t sample_lds = 4 * (size_t)16 * p->Q;
   for (int i = 0; i < n_steps; ++i) {
-    if (wide) gen_chain_kernel<16><<<gchain, 1024, lds, st>>>(c);
-    else gen_chain_kernel<8><<<gchain, 1024, lds, st>>>(c);
-    gen_rowvec_kernel<<<(sk.N + 3) / 4, 256, 64 * sk.K, st>>>(sk);
-    gen_rowvec_kernel<<<(p1.N + 3) / 4, 256, 64 * p1.K, st>>>(p1);
-    gen_rowvec_kernel<<<(p2.N + 3) / 4, 256, 64 * p2.K, st>>>(p2);
-    gen_sample_kernel<<<1, 1024, 0, st>>>(sm);
+    gen_wave_kernel<<<p->B, 64, wave_lds, st>>>(c);
+    gen_gemv_kernel<<<gsk, 256, 0, st>>>(sk);
+    gen_gemv_kernel<<<gp1, 256, 0, st>>>(p1);
+    gen_gemv_kernel<<<gp2, 256, 0, st>>>(p2);
+    gen_sample_kernel<<<1, 1024, sample_lds, st>>>(sm);
     LBWN_CHECK_LAUNCH();
   }
   return 0;
