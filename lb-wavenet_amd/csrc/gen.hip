@@ -5,9 +5,10 @@
 // form of the D-separation cache: layer l keeps its last d inputs, slot t mod d, replacing
 // imodel's shift-by-chunk buffers imodel.py:88-98, :190-207), the next input code, the
 // teacher vector and a counter-based RNG.  One step =
-//   gen_wave     one wave per stream, no barriers: PRE row (+bias), 50 × [dilated conv
+//   gen_wave     one workgroup per stream: a compute wave runs PRE row (+bias), 50 × [dilated conv
 //                (lane = output channel, 64-term dot over LDS broadcasts), gate (lane pairs),
-//                residual], weights from a lane-coalesced image prefetched a layer ahead
+//                residual] while three loader waves stream the per-layer weight images into an
+//                LDS ring by LDS-DMA, several layers ahead
 //   gen_gemv × 3 K-split row-vector products with deterministic partial sums:
 //                skip = z_cat·SKIPcat, h = relu(relu(skip + Σb)·POST1 + b1), logits = h·POST2
 //   gen_sample   logits = Σ partials + b2; inverse-CDF draw with u = hash(seed, stream, step),
@@ -47,43 +48,44 @@ LBWN_DEV float sum_parts(const float* p, long stride, int n) {
   return s;
 }
 
-LBWN_DEV long ring_offset(int l, int nbl, int B, int Cr) {
-  const long s = (long)(l / nbl) * ((1L << nbl) - 1) + ((1L << (l % nbl)) - 1);
-  return s * B * Cr;
-}
-
-// ---- per-stream wave chain ---------------------------------------------------------------
-// One wave per stream, no barriers: lane o computes conv output o (sig 0-31 | gate 32-63) as
-// a 64-term dot product over [x[t-d] | x[t]] (LDS broadcasts), the gate pairs lane o with
-// lane o+32 (shuffle), the residual reads z back through wave-private LDS.  Weights come
-// from a lane-coalesced per-layer image (packed once per gen_start) as 26 16-B loads per
-// lane, prefetched one layer ahead into a register double buffer.
-constexpr int GI_W = 16 * 64 * 4;           // conv: [kq 16][lane 64][4]  W[4kq+j][lane]
-constexpr int GI_R = 8 * 64 * 4;            // residual: [cq 8][lane 64][4] RES[4cq+j][lane] (lane < 32)
-constexpr int GIMG = GI_W + GI_R + 128;     // + conv bias [64] + residual bias [64]
-
-struct LayerRegs {
-  floatx4 w[16];
-  floatx4 r[8];
-  float bc, br, gc;
-};
+// ---- per-stream layer chain --------------------------------------------------------------
+// One workgroup of 8 waves per stream: waves 0-3 compute (one per SIMD), waves 4-7 move data.
+//   compute wave w owns channels 8w..8w+7 (lane group c = lane>>3 <-> channel 8w+c):
+//     conv      lane = (c, sg = sig|gate, kq = k-quarter): 16 FMAs over its quarter of
+//               [x[t-d] | x[t]] (4 weight + 4 broadcast input ds_read_b128), the quarters summed
+//               by two DPP quad permutes, the sig/gate partner fetched by row_half_mirror,
+//               z = tanh(sig)·σ(gate) on all 8 lanes of the group
+//     residual  lane = (c, kp = k-eighth): 4 FMAs over z[4kp..4kp+3], DPP-reduced over kp
+//   Splitting the layer over the four SIMDs is what pays: one wave doing all 64 outputs
+//   reads 43 KB of LDS per layer through one SIMD's return path (~16 cycles per 1-KiB
+//   ds_read_b128), ~1,500 cycles per layer.
+//   loader waves  (a) this step's dilated taps x_l[t-d_l] (ring slot t mod d_l) into the LDS tap
+//                 table, two layers per 4-byte LDS-DMA; (b) every layer's slot — weights (20 ×
+//                 1 KiB, packed once per gen_start) + bias rows + the stream's GC-projection
+//                 row — into an NS-slot LDS ring, NS-1 layers ahead: 5 pieces + 1 row per loader
+//                 per layer (counted vmcnt, inside the 6-bit counter).
+// Two raw s_barriers per layer: B1 (x of layer l written; before it each loader retires layer
+// l's pieces, and the compute waves' reads of slot l-1 retired, so the loaders refill it after
+// B1) and B2 (z of layer l written).  No global loads on the compute chain.
+constexpr int GI_W = 16 * 256;              // conv: [w 4][m 4][lane 64][4]  W[16kq+4m+j][32sg+8w+c]
+constexpr int GI_R = 4 * 256;               // residual: [w 4][lane 64][4] RES[4kp+j][8w+c]
+constexpr int GI_WR = GI_W + GI_R;          // 20 pieces of 1 KiB
+constexpr int GIMG = GI_WR + 192;           // global image: + conv bias [64] + residual bias [64] + zeros [64]
+constexpr int G_SLOT = GI_WR + 256;         // LDS slot: weights | bc [64] | br [64] | gc [64] | pad [64]
+constexpr int G_NS = 6;                     // LDS ring depth (layers)
+constexpr int G_PIECES = 5;                 // 1-KiB pieces per loader wave per layer (4 loaders)
+constexpr int G_DMA = G_PIECES + 1;         // + one 256-B row
+constexpr int G_MAXL = 256;                 // tap table rows
+constexpr int G_LDS = G_NS * G_SLOT + (G_MAXL + 2) * 32 + 64;   // ring | taps | x | z  (162,304 B)
+static_assert(4 * G_PIECES * 256 == GI_WR, "image pieces");
+static_assert(G_LDS * 4 <= 160 * 1024, "LDS");
 
 struct WaveK {
   const float* pre; const float* pre_b; const float* img; const float* gc_proj;
   float* rings; float* zcat; const long long* step; const int* code;
   int B, L, nbl, Cr, Cd, pre_bias;
+  long long* trace;   // non-null (LBWN_GEN_TRACE set at plan creation): stream 0's cycle stamps
 };
-
-LBWN_DEV void load_layer(LayerRegs& R, const WaveK& a, int l, int b, int lane) {
-  const float* base = a.img + (long)l * GIMG;
-#pragma unroll
-  for (int kq = 0; kq < 16; ++kq) R.w[kq] = *(const floatx4*)(base + (kq * 64 + lane) * 4);
-#pragma unroll
-  for (int cq = 0; cq < 8; ++cq) R.r[cq] = *(const floatx4*)(base + GI_W + (cq * 64 + lane) * 4);
-  R.bc = base[GI_W + GI_R + lane];
-  R.br = base[GI_W + GI_R + 64 + lane];
-  R.gc = a.gc_proj ? a.gc_proj[((long)l * a.B + b) * 64 + lane] : 0.f;
-}
 
 LBWN_DEV float dot4(const floatx4& w, const floatx4& x, float acc) {
   acc = fmaf(w[0], x[0], acc);
@@ -92,113 +94,179 @@ LBWN_DEV float dot4(const floatx4& w, const floatx4& x, float acc) {
   return fmaf(w[3], x[3], acc);
 }
 
-__global__ __launch_bounds__(64) void gen_wave_kernel(WaveK a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* XP = sm;                    // [L][32] dilated taps of this step
-  float* X = XP + a.L * 32;          // [32] current layer input
-  float* Z = X + 32;                 // [32] gate output
-  const int lane = threadIdx.x, b = blockIdx.x;
-  const long t = *a.step;
-  const int Cr = a.Cr, L = a.L;
-  LayerRegs RA, RB;
-  load_layer(RA, a, 0, b, lane);
-  // every layer's tap: input of layer l at t - d_l (ring slot t mod d, zero-initialised).
-  // d is a power of two: slot = t & (d-1); ring offsets accumulate (no integer division)
-  {
-    long roff = 0;
-    int bl = 0;
-    for (int l = 0; l < L; ++l) {
-      const int d = 1 << bl;
-      if ((lane >> 5) == (l & 1) && (lane & 31) < Cr) {
-        const int c = lane & 31;
-        XP[l * 32 + c] = a.rings[roff + ((long)b * d + (t & (d - 1))) * Cr + c];
-      } else if ((lane >> 5) == (l & 1)) {
-        XP[l * 32 + (lane & 31)] = 0.f;
-      }
-      roff += (long)d * a.B * Cr;
-      bl = (bl + 1 == a.nbl) ? 0 : bl + 1;
-    }
-  }
-  // step input: PRE row of the previous draw (+ PRE_BIAS); the zero vector at step 0
-  float xr = 0.f;   // lane c < 32: x[c] of the current layer input
-  if (lane < 32) {
-    if (lane < Cr) {
-      const int code = a.code[b];
-      if (code >= 0) xr = a.pre[(long)code * Cr + lane];
-      if (a.pre_bias && a.pre_b) xr += a.pre_b[lane];
-    }
-    X[lane] = xr;
-  }
-  wave_sync();
+template <int CTRL>
+LBWN_DEV float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141;
 
+// workgroup barrier that retires only this wave's LDS ops: no vmcnt wait (outstanding global
+// stores and LDS-DMA pieces stay in flight across it); the "memory" clobber pins LDS accesses
+LBWN_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// LDS-DMA: lane i's SIZE bytes from src land at lds_dst + i·SIZE (lds_dst wave-uniform)
+LBWN_DEV void dma16(const float* src, float* lds_dst) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+LBWN_DEV void dma4(const float* src, float* lds_dst) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 4, 0, 0);
+}
+
+__global__ __launch_bounds__(512) void gen_wave_kernel(WaveK a) {
+  __shared__ __attribute__((aligned(16))) float sm[G_LDS];
+  float* RING = sm;                  // [G_NS][G_SLOT]
+  float* XP = sm + G_NS * G_SLOT;    // [L (+2)][32] dilated taps of this step
+  float* X = XP + (G_MAXL + 2) * 32; // [32] current layer input
+  float* Z = X + 32;                 // [32] gate output
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, b = blockIdx.x, L = a.L;
+  const long t = *a.step;
+
+  if (wid >= 4) {   // ---- loader waves
+    const int lw = wid - 4;
+    const float* zeros = a.img + GI_WR + 128;   // the image's zero row (layer 0)
+    // (a) taps: pair q = layers 2q, 2q+1 (lane half h) by loader q % 4; d is a power of two,
+    // slot = t & (d-1); ring offsets carried in scalars (no integer division)
+    {
+      const int h = lane >> 5, c = lane & 31;
+      long roff = 0;
+      int bl = 0;
+      for (int q = 0; 2 * q < L; ++q) {
+        const int dE = 1 << bl;
+        const long roffO = roff + (long)dE * a.B * a.Cr;
+        const int blO = (bl + 1 == a.nbl) ? 0 : bl + 1;
+        const int dO = 1 << blO;
+        if ((q & 3) == lw) {
+          const int d = h ? dO : dE, l = 2 * q + h;
+          const float* src = (l < L && c < a.Cr)
+                                 ? a.rings + (h ? roffO : roff) + ((long)b * d + (t & (d - 1))) * a.Cr + c
+                                 : zeros + c;
+          dma4(src, XP + 2 * q * 32);
+        }
+        roff = roffO + (long)dO * a.B * a.Cr;
+        bl = (blO + 1 == a.nbl) ? 0 : blO + 1;
+      }
+    }
+    // (b) slots: pieces [5lw, 5lw+5) + row lw (bc | br | gc | pad)
+    auto issue = [&](int l) {
+      const float* src = a.img + (long)l * GIMG;
+      float* dst = RING + (l % G_NS) * G_SLOT;
+#pragma unroll
+      for (int p = 0; p < G_PIECES; ++p) {
+        const int pc = lw * G_PIECES + p;
+        dma16(src + pc * 256 + lane * 4, dst + pc * 256);
+      }
+      const float* row = lw < 2 ? src + GI_WR + lw * 64
+                       : lw == 2 ? (a.gc_proj ? a.gc_proj + ((long)l * a.B + b) * 64 : zeros)
+                                 : zeros;
+      dma4(row + lane, dst + GI_WR + lw * 64);
+    };
+    for (int l = 0; l < G_NS - 1 && l < L; ++l) issue(l);
+    for (int k = 0; k < L; ++k) {
+      // issued so far: taps, layers 0 .. min(k+NS-2, L-1); retire everything up to layer k
+      if (k + G_NS - 2 < L) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G_DMA * (G_NS - 2)) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();                                   // B1 of layer k
+      if (k + G_NS - 1 < L) issue(k + G_NS - 1);      // into slot (k-1) % NS, read-retired before B1
+      lds_barrier();                                   // B2 of layer k
+    }
+    return;
+  }
+
+  // ---- compute waves
+  const int w = wid, Cr = a.Cr, Cd = a.Cd;
+  const int c = lane >> 3, sg = (lane >> 2) & 1, kq = lane & 3, kp = lane & 7;
+  const int ch = 8 * w + c;                 // the channel this lane group owns (z and x)
+  const int o = 32 * sg + ch;               // conv output of this lane
+  const bool lead = kp == 0;                // one lane per group stores
+  const bool tr = a.trace && b == 0 && w == 0 && lane == 0;
+  if (tr) a.trace[0] = clock64();
+  // step input: PRE row of the previous draw (+ PRE_BIAS); the zero vector at step 0
+  float xr = 0.f;   // x[ch] of the current layer input (all 8 lanes of the group)
+  if (ch < Cr) {
+    const int code = a.code[b];
+    if (code >= 0) xr = a.pre[(long)code * Cr + ch];
+    if (a.pre_bias && a.pre_b) xr += a.pre_b[ch];
+  }
+  if (lead) X[ch] = xr;
+  if (tr) a.trace[1] = clock64();
+  // conv inputs of this lane: k-quarter kq of [x[t-d] (tap row) | x[t] (X)]
+  const int xin_off = kq < 2 ? 16 * kq : 16 * (kq - 2);
   long roff = 0;   // ring offset of layer l
   int bl = 0;      // l % nbl
-  auto layer = [&](int l, LayerRegs& R, LayerRegs& N) {
-    if (l + 1 < L) load_layer(N, a, l + 1, b, lane);
+  for (int l = 0; l < L; ++l) {
+    lds_barrier();   // B1: x of layer l, taps and layer l's slot are in LDS
+    if (tr && l == 0) a.trace[2] = clock64();
+    const float* S = RING + (l % G_NS) * G_SLOT;
+    const float* xin = (kq < 2 ? XP + l * 32 : X) + xin_off;
+    floatx4 wv[4], xv[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      wv[m] = *(const floatx4*)(S + (w * 4 + m) * 256 + lane * 4);
+      xv[m] = *(const floatx4*)(xin + 4 * m);
+    }
+    const floatx4 rw = *(const floatx4*)(S + GI_W + w * 256 + lane * 4);
+    const float bco = S[GI_WR + o] + S[GI_WR + 128 + o], bro = S[GI_WR + 64 + ch];
+    __builtin_amdgcn_sched_barrier(0);
     const int d = 1 << bl;
-    if (lane < Cr) a.rings[roff + ((long)b * d + (t & (d - 1))) * Cr + lane] = xr;
+    if (lead && ch < Cr) a.rings[roff + ((long)b * d + (t & (d - 1))) * Cr + ch] = xr;
     roff += (long)d * a.B * Cr;
     bl = (bl + 1 == a.nbl) ? 0 : bl + 1;
-    const float* xp = XP + l * 32;
-    float acc0 = R.bc + R.gc, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-#pragma unroll
-    for (int kq = 0; kq < 8; kq += 2) {
-      acc0 = dot4(R.w[kq], *(const floatx4*)(xp + 4 * kq), acc0);
-      acc1 = dot4(R.w[kq + 1], *(const floatx4*)(xp + 4 * kq + 4), acc1);
+    float acc0 = dot4(wv[0], xv[0], 0.f), acc1 = dot4(wv[1], xv[1], 0.f);
+    acc0 = dot4(wv[2], xv[2], acc0);
+    acc1 = dot4(wv[3], xv[3], acc1);
+    float v = acc0 + acc1;
+    v += dpp<DPP_XOR1>(v);
+    v += dpp<DPP_XOR2>(v);
+    v += bco;                                      // conv output o (+ bias + GC term)
+    const float vp = dpp<DPP_HALF_MIRROR>(v);      // the partner output (sig <-> gate, same channel)
+    const float z = tanhf_(sg ? vp : v) * sigmoidf_(sg ? v : vp);
+    if (tr) a.trace[4 + 2 * l] = clock64();
+    if (lead) {
+      Z[ch] = z;
+      if (ch < Cd) a.zcat[(long)b * L * Cd + (long)l * Cd + ch] = z;
     }
-#pragma unroll
-    for (int kq = 0; kq < 8; kq += 2) {
-      acc2 = dot4(R.w[8 + kq], *(const floatx4*)(X + 4 * kq), acc2);
-      acc3 = dot4(R.w[8 + kq + 1], *(const floatx4*)(X + 4 * kq + 4), acc3);
-    }
-    const float v = (acc0 + acc1) + (acc2 + acc3);
-    const float vg = __shfl_xor(v, 32);
-    const float z = tanhf_(v) * sigmoidf_(vg);      // valid on lanes < 32 (padded channels: v = 0 -> z = 0)
-    if (lane < a.Cd) a.zcat[(long)b * L * a.Cd + (long)l * a.Cd + lane] = z;
-    if (lane < 32) Z[lane] = z;
-    wave_sync();
-    float r0 = R.br, r1 = 0.f;
-#pragma unroll
-    for (int cq = 0; cq < 8; cq += 2) {
-      r0 = dot4(R.r[cq], *(const floatx4*)(Z + 4 * cq), r0);
-      r1 = dot4(R.r[cq + 1], *(const floatx4*)(Z + 4 * cq + 4), r1);
-    }
-    xr += r0 + r1;
-    if (lane < 32) X[lane] = xr;
-    wave_sync();
-  };
-  for (int l = 0; l < L; l += 2) {
-    layer(l, RA, RB);
-    if (l + 1 < L) layer(l + 1, RB, RA);
+    lds_barrier();   // B2: z of layer l
+    const floatx4 zv = *(const floatx4*)(Z + 4 * kp);
+    float r = dot4(rw, zv, 0.f);
+    r += dpp<DPP_XOR1>(r);
+    r += dpp<DPP_XOR2>(r);
+    r += dpp<DPP_HALF_MIRROR>(r);
+    xr += r + bro;
+    if (lead) X[ch] = xr;
+    if (tr) a.trace[5 + 2 * l] = clock64();
   }
 }
 
-// per-layer lane-coalesced weight image (reference layouts in, GIMG floats per layer out)
+// per-layer weight image in the compute waves' lane order (reference layouts in, GIMG floats
+// per layer out): SIGNAL/GATE [l][tap][Cr][Cd] (tap 0 = x[t-d]), RESIDUAL [l][Cd][Cr]
 __global__ void gen_pack_kernel(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                                 const float* res, const float* res_b, float* img, int Cr, int Cd) {
   const int l = blockIdx.x;
-  float* o = img + (long)l * GIMG;
+  float* out = img + (long)l * GIMG;
   for (int e = threadIdx.x; e < GIMG; e += blockDim.x) {
     float v = 0.f;
     if (e < GI_W) {
-      const int kq = e / 256, lane = (e % 256) / 4, j = e % 4, k = 4 * kq + j;
-      const int tap = k >> 5, in = k & 31, oc = lane & 31;
-      if (in < Cr && oc < Cd) v = (lane < 32 ? sig : gate)[(long)l * 2 * Cr * Cd + (tap * Cr + in) * Cd + oc];
-    } else if (e < GI_W + GI_R) {
-      const int f = e - GI_W, cq = f / 256, lane = (f % 256) / 4, j = f % 4, c = 4 * cq + j;
-      if (lane < Cr && c < Cd) v = res[(long)l * Cd * Cr + c * Cr + lane];
+      const int w = e / 1024, m = (e / 256) % 4, ln = (e % 256) / 4, j = e % 4;
+      const int c = ln >> 3, sg = (ln >> 2) & 1, kq = ln & 3;
+      const int k = 16 * kq + 4 * m + j, tap = k >> 5, in = k & 31, oc = 8 * w + c;
+      if (in < Cr && oc < Cd) v = (sg ? gate : sig)[(long)l * 2 * Cr * Cd + (tap * Cr + in) * Cd + oc];
+    } else if (e < GI_WR) {
+      const int f = e - GI_W, w = f / 256, ln = (f % 256) / 4, j = f % 4;
+      const int zc = 4 * (ln & 7) + j, oc = 8 * w + (ln >> 3);
+      if (zc < Cd && oc < Cr) v = res[(long)l * Cd * Cr + zc * Cr + oc];
     } else {
-      const int f = e - GI_W - GI_R;
+      const int f = e - GI_WR;
       if (f < 64) {
         const float* bb = f < 32 ? sig_b : gate_b;
         if (bb && (f & 31) < Cd) v = bb[(long)l * Cd + (f & 31)];
-      } else if (res_b && f - 64 < Cr) {
-        v = res_b[(long)l * Cr + f - 64];
+      } else if (f < 128) {
+        if (res_b && f - 64 < Cr) v = res_b[(long)l * Cr + f - 64];
       }
     }
-    o[e] = v;
+    out[e] = v;
   }
 }
+
 
 // ---- K-split row-vector GEMV --------------------------------------------------------------
 // part[ks][b][n] = Σ_{k in slice ks} act(in[b][k])·W[k][n]: block = 64 columns (lane = n) ×
@@ -379,7 +447,8 @@ struct lbwn_gen_plan {
   lbwn_arch a;
   int B, L, nbl, Cr, Cd, Cs, Cp, Q;
   long long max_steps;
-  size_t oRING, oZCAT, oSKP, oHP, oLGP, oLOG, oSTEP, oCODE, oTEACH, oSAMP, oWAV, oGCP, oBSUM, oGIMG, total;
+  size_t oRING, oZCAT, oSKP, oHP, oLGP, oLOG, oSTEP, oCODE, oTEACH, oSAMP, oWAV, oGCP, oBSUM, oGIMG, oTRACE, total;
+  bool trace;
   int ksl_skip, ks_skip, ks_h, ks_lg;
   long n_ring;
   long long n_teacher, max_teacher;
@@ -397,7 +466,7 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
                                     lbwn_gen_plan** out) {
   LBWN_REQUIRE(a && out && B >= 1 && max_steps >= 1 && max_teacher >= 0, "gen_plan_create: bad arguments");
   LBWN_REQUIRE(a->n_res <= 32 && a->n_dil <= 32, "gen: n_res/n_dil must be <= 32");
-  LBWN_REQUIRE(a->n_blocks * a->n_block_layers * 32 * 4 + 256 <= 64 * 1024, "gen: too many layers for the tap cache");
+  LBWN_REQUIRE(a->n_blocks * a->n_block_layers <= G_MAXL, "gen: more than %d layers (tap cache)", G_MAXL);
   LBWN_REQUIRE(a->n_lc_out == 0, "gen: local conditioning is not supported by the cached generator "
                                  "(imodel.py has no LC path)");
   lbwn_gen_plan* p = new lbwn_gen_plan();
@@ -430,6 +499,8 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
   p->oGCP = gcarve(cur, 4 * (size_t)p->L * B * 64);
   p->oBSUM = gcarve(cur, 4 * (size_t)p->Cs);
   p->oGIMG = gcarve(cur, 4 * (size_t)p->L * GIMG);
+  p->oTRACE = gcarve(cur, 8 * (size_t)(2 * p->L + 8));
+  p->trace = getenv("LBWN_GEN_TRACE") != nullptr;
   p->total = cur;
   *out = p;
   return 0;
@@ -445,6 +516,7 @@ extern "C" int lbwn_gen_tensor(const lbwn_gen_plan* p, const char* name, size_t*
   else if (!strcmp(name, "wav")) { *off = p->oWAV; *bytes = 4 * B * p->max_steps; }
   else if (!strcmp(name, "logits")) { *off = p->oLOG; *bytes = 4 * B * p->Q; }
   else if (!strcmp(name, "step")) { *off = p->oSTEP; *bytes = 8; }
+  else if (!strcmp(name, "trace")) { *off = p->oTRACE; *bytes = 8 * (size_t)(2 * p->L + 8); }
   else if (!strcmp(name, "rings")) { *off = p->oRING; *bytes = 4 * (size_t)p->n_ring; }
   else if (!strcmp(name, "teacher")) { *off = p->oTEACH; *bytes = 4 * (size_t)std::max<long long>(1, p->n_teacher); }
   else LBWN_REQUIRE(false, "gen_tensor: unknown tensor '%s'", name);
@@ -496,8 +568,8 @@ extern "C" int lbwn_gen_run(lbwn_gen_plan* p, const lbwn_params* P, void* ws, in
   c.gc_proj = p->a.n_gc_embed > 0 ? gat<float>(ws, p->oGCP) : nullptr;
   c.rings = gat<float>(ws, p->oRING); c.zcat = gat<float>(ws, p->oZCAT);
   c.step = gat<long long>(ws, p->oSTEP); c.code = gat<int>(ws, p->oCODE);
+  c.trace = p->trace ? gat<long long>(ws, p->oTRACE) : nullptr;
   c.B = p->B; c.L = p->L; c.nbl = p->nbl; c.Cr = p->Cr; c.Cd = p->Cd; c.pre_bias = p->pre_bias;
-  const size_t wave_lds = 4 * ((size_t)p->L * 32 + 64);
   // skip = z_cat·SKIPcat (+Σb and relu applied by the consumer), h = relu(relu(skip)·POST1 + b1),
   // logits = h·POST2 + b2 (summed in the sampler)
   GemvK sk, p1, p2;
@@ -519,7 +591,7 @@ extern "C" int lbwn_gen_run(lbwn_gen_plan* p, const lbwn_params* P, void* ws, in
   const dim3 gsk((sk.N + 63) / 64, p->ks_skip), gp1((p1.N + 63) / 64, (p1.K + 31) / 32), gp2((p2.N + 63) / 64, (p2.K + 31) / 32);
   const size_t sample_lds = 4 * (size_t)16 * p->Q;
   for (int i = 0; i < n_steps; ++i) {
-    gen_wave_kernel<<<p->B, 64, wave_lds, st>>>(c);
+    gen_wave_kernel<<<p->B, 512, 0, st>>>(c);
     gen_gemv_kernel<<<gsk, 256, 0, st>>>(sk);
     gen_gemv_kernel<<<gp1, 256, 0, st>>>(p1);
     gen_gemv_kernel<<<gp2, 256, 0, st>>>(p2);

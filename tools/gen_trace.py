@@ -1,0 +1,39 @@
+"""Cycle-stamp trace of one cached-generation step (stream 0): prologue (weights + taps),
+step input, then per layer conv+gate and residual.  Needs LBWN_GEN_TRACE=1 (set here)."""
+import os
+import sys
+
+os.environ['LBWN_GEN_TRACE'] = '1'
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'lb-wavenet_amd'))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from lbwn.arch import load_arch  # noqa: E402
+from lbwn.imodel import WaveNetGen  # noqa: E402
+from lbwn.tmodel import WaveNetTrain  # noqa: E402
+
+arch = load_arch(os.path.join(ROOT, 'par', 'arch3.json'))
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+net = WaveNetTrain(**arch, batch_sz=1, l2_factor=0.0, print_interval=0, seed=0)
+g = WaveNetGen(arch['n_blocks'], arch['n_block_layers'], arch['n_quant'], arch['n_res'], arch['n_dil'],
+               arch['n_skip'], arch['n_post'], arch['n_gc_embed'], arch['n_gc_category'], arch['use_bias'],
+               B, 200, None, seed=1, graph=False)
+g.load_params(net)
+g.build_graph(2000)
+g.init_buffers(list(range(1, B + 1)) if arch['n_gc_embed'] else None)
+g.step(1000)
+torch.cuda.synchronize()
+L = arch['n_blocks'] * arch['n_block_layers']
+rows = []
+for _ in range(5):
+    g.step(1)
+    torch.cuda.synchronize()
+    tr = g.tensor('trace', torch.int64).cpu().numpy()[:4 + 2 * L]
+    rows.append(np.diff(np.concatenate([tr[:3], tr[4:4 + 2 * L]])))
+d = np.median(np.array(rows), axis=0)
+print('cycles: input %d  wait for taps+layer 0 %d  first-conv %d' % (d[0], d[1], d[2]))
+conv, res = d[4::2], d[3::2][:L]
+print('per layer (median over layers): conv+gate %.0f  residual %.0f   total %.0f cycles' %
+      (np.median(conv), np.median(res), np.median(conv) + np.median(res)))
+print('layers:', ' '.join('%d/%d' % (c, r) for c, r in zip(d[2::2][:L], d[3::2][:L])))
+print('total kernel cycles (stamps): %d' % (np.sum(d)))
