@@ -33,18 +33,18 @@ LBWN_DEV void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Σ_q p[q·stride], q < n: independent loads in batches of 8 (a plain loop waits on each)
+// Σ_q p[q·stride], q < n, in a fixed order: all loads of a 32-chunk are issued before the
+// first add (the index is clamped instead of predicated, so no load sits behind a branch and
+// hipcc counts them as one group: one memory round trip per 32 partials, not one per 8)
 LBWN_DEV float sum_parts(const float* p, long stride, int n) {
   float s = 0.f;
-  int q = 0;
-  for (; q + 8 <= n; q += 8) {
-    float v[8];
+  for (int q0 = 0; q0 < n; q0 += 32) {
+    float v[32];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = p[(q + i) * stride];
+    for (int i = 0; i < 32; ++i) v[i] = p[(long)min(q0 + i, n - 1) * stride];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s += v[i];
+    for (int i = 0; i < 32; ++i) s += (q0 + i < n) ? v[i] : 0.f;
   }
-  for (; q < n; ++q) s += p[q * stride];
   return s;
 }
 
@@ -282,6 +282,7 @@ struct GemvK {
   const float* W; long ldw;
   float* out_part;                              // [ceil(K/KSL)][B][N]
   int B, K, N, KSL;
+  long long* step_advance;                      // non-null: block (0,0) advances the step counter
 };
 
 __global__ __launch_bounds__(256) void gen_gemv_kernel(GemvK a) {
@@ -296,21 +297,59 @@ __global__ __launch_bounds__(256) void gen_gemv_kernel(GemvK a) {
     const int k = k0 + w + 4 * i;
     wr[i] = (4 * i < KSL && k < k1 && n < a.N) ? a.W[(long)k * a.ldw + n] : 0.f;
   }
+  if (a.step_advance && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0)   // no-return atomic: no wait
+    __hip_atomic_fetch_add(a.step_advance, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (int b0 = 0; b0 < a.B; b0 += 16) {
     const int nbb = min(16, a.B - b0);
-    for (int e = tid; e < 16 * KSL; e += 256) {
-      const int j = e / KSL, kk = e % KSL, k = k0 + kk;
-      float v = 0.f;
-      if (j < nbb && k < a.K) {
-        if (a.in_part) {
-          v = sum_parts(a.in_part + (long)(b0 + j) * a.K + k, (long)a.B * a.K, a.in_parts);
-          if (a.in_bias) v += a.in_bias[k];
-        } else {
-          v = a.in[(long)(b0 + j) * a.ldin + k];
+    // stage the input slice: every load of this thread issued before the first is consumed
+    // (at most GV_EPT elements per thread; partial sums as in sum_parts, two elements at once)
+    constexpr int GV_EPT = 16 * GV_KSL_MAX / 256;
+    if (a.in_part) {
+      for (int r0 = 0; r0 < GV_EPT; r0 += 2) {
+        float s2[2] = {0.f, 0.f};
+        for (int q0 = 0; q0 < a.in_parts; q0 += 16) {
+          float v[2][16];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int e = tid + 256 * (r0 + h), j = min(e / KSL, nbb - 1), k = min(k0 + e % KSL, a.K - 1);
+            const float* pp = a.in_part + (long)(b0 + j) * a.K + k;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[h][i] = pp[(long)min(q0 + i, a.in_parts - 1) * a.B * a.K];
+          }
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s2[h] += (q0 + i < a.in_parts) ? v[h][i] : 0.f;
         }
-        if (a.relu_in) v = fmaxf(v, 0.f);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e = tid + 256 * (r0 + h);
+          if (e >= 16 * KSL) continue;
+          const int j = e / KSL, kk = e % KSL, k = k0 + kk;
+          float v = 0.f;
+          if (j < nbb && k < a.K) {
+            v = s2[h] + (a.in_bias ? a.in_bias[k] : 0.f);
+            if (a.relu_in) v = fmaxf(v, 0.f);
+          }
+          xs[j][kk] = v;
+        }
       }
-      xs[j][kk] = v;
+    } else {
+      float v[GV_EPT];
+#pragma unroll
+      for (int r = 0; r < GV_EPT; ++r) {
+        const int e = tid + 256 * r, j = min(e / KSL, nbb - 1), k = min(k0 + e % KSL, a.K - 1);
+        v[r] = a.in[(long)(b0 + j) * a.ldin + k];
+      }
+#pragma unroll
+      for (int r = 0; r < GV_EPT; ++r) {
+        const int e = tid + 256 * r;
+        if (e >= 16 * KSL) continue;
+        const int j = e / KSL, kk = e % KSL;
+        float x = (j < nbb && k0 + kk < a.K) ? v[r] : 0.f;
+        if (a.relu_in) x = fmaxf(x, 0.f);
+        xs[j][kk] = x;
+      }
     }
     __syncthreads();
     float acc[16];
@@ -348,68 +387,66 @@ struct SampleK {
   int* samples; float* wav; long long max_steps; unsigned long long seed;
 };
 
-// one block; wave w handles streams w, w+16, ...: softmax CDF in a fixed order, first k with
-// cumsum(e)[k] > u·Σe (oracle/wavenet_ref.py sample_from_logits restates the same transform).
-__global__ __launch_bounds__(1024) void gen_sample_kernel(SampleK a) {
-  extern __shared__ float lgs[];   // [16][Q]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long long t = *a.step;
-  for (int b = w; b < a.B; b += 16) {
-    float* lg = lgs + w * a.Q;
-    for (int c = lane; c < a.Q; c += 64) {
-      float v = sum_parts(a.log_part + (long)b * a.Q + c, (long)a.B * a.Q, a.parts);
-      if (a.bias) v += a.bias[c];
-      lg[c] = v;
-      a.logits[(long)b * a.Q + c] = v;
-    }
-    wave_sync();
-    float mx = -INFINITY;
-    for (int c = lane; c < a.Q; c += 64) mx = fmaxf(mx, lg[c]);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-    // each lane owns a contiguous run of Q/64 codes: local sums, then an exclusive scan
-    const int per = (a.Q + 63) / 64, c0 = lane * per;
-    float loc = 0.f;
-    for (int j = 0; j < per; ++j)
-      if (c0 + j < a.Q) loc += expf(lg[c0 + j] - mx);
-    float incl = loc;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const float v = __shfl_up(incl, o);
-      if (lane >= o) incl += v;
-    }
-    const float total = __shfl(incl, 63);
-    const float excl = incl - loc;
-    const uint64_t h = splitmix(a.seed, (uint64_t)b, (uint64_t)t);
-    const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
-    const float target = u * total;
-    // lane whose run contains the crossing point
-    int found = a.Q;
-    if (excl <= target && target < incl) {
-      float run = excl;
-      for (int j = 0; j < per; ++j) {
-        if (c0 + j >= a.Q) break;
-        run += expf(lg[c0 + j] - mx);
-        if (run > target) { found = c0 + j; break; }
-      }
-      if (found == a.Q) found = min(c0 + per, a.Q) - 1;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) found = min(found, __shfl_xor(found, o));
-    if (found >= a.Q) found = a.Q - 1;
-    if (lane == 0) {
-      if (t < a.max_steps) {
-        a.samples[(long)b * a.max_steps + t] = found;
-        const float mu = (float)(a.Q - 1), inv = 1.f / mu;               // ops.py:12-20
-        const float aa = (2.f * (float)found - 1.f) * inv - 1.f;
-        const float sg = aa > 0.f ? 1.f : (aa < 0.f ? -1.f : 0.f);
-        a.wav[(long)b * a.max_steps + t] = sg * (powf(1.f + mu, fabsf(aa)) - 1.f) * inv;
-      }
-      a.code[b] = (t < a.n_teacher) ? a.teacher[t] : found;              // imodel.py:260-269
-    }
+// one block per stream: thread c sums code c's logit partials (+b2), then wave 0 draws from
+// the softmax CDF in a fixed order: the first k with cumsum(e)[k] > u·Σe
+// (oracle/wavenet_ref.py sample_from_logits restates the same transform).  The step counter
+// was advanced by this step's skip GEMV, so this step is *step - 1.
+__global__ __launch_bounds__(256) void gen_sample_kernel(SampleK a) {
+  extern __shared__ float lg[];   // [Q]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, b = blockIdx.x;
+  const long long t = *a.step - 1;
+  for (int c = threadIdx.x; c < a.Q; c += blockDim.x) {
+    float v = sum_parts(a.log_part + (long)b * a.Q + c, (long)a.B * a.Q, a.parts);
+    if (a.bias) v += a.bias[c];
+    lg[c] = v;
+    a.logits[(long)b * a.Q + c] = v;
   }
   __syncthreads();
-  if (threadIdx.x == 0) *a.step = t + 1;
+  if (w != 0) return;
+  float mx = -INFINITY;
+  for (int c = lane; c < a.Q; c += 64) mx = fmaxf(mx, lg[c]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  // each lane owns a contiguous run of Q/64 codes: local sums, then an exclusive scan
+  const int per = (a.Q + 63) / 64, c0 = lane * per;
+  float loc = 0.f;
+  for (int j = 0; j < per; ++j)
+    if (c0 + j < a.Q) loc += expf(lg[c0 + j] - mx);
+  float incl = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  const float total = __shfl(incl, 63);
+  const float excl = incl - loc;
+  const uint64_t h = splitmix(a.seed, (uint64_t)b, (uint64_t)t);
+  const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+  const float target = u * total;
+  // lane whose run contains the crossing point
+  int found = a.Q;
+  if (excl <= target && target < incl) {
+    float run = excl;
+    for (int j = 0; j < per; ++j) {
+      if (c0 + j >= a.Q) break;
+      run += expf(lg[c0 + j] - mx);
+      if (run > target) { found = c0 + j; break; }
+    }
+    if (found == a.Q) found = min(c0 + per, a.Q) - 1;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) found = min(found, __shfl_xor(found, o));
+  if (found >= a.Q) found = a.Q - 1;
+  if (lane == 0) {
+    if (t < a.max_steps) {
+      a.samples[(long)b * a.max_steps + t] = found;
+      const float mu = (float)(a.Q - 1), inv = 1.f / mu;               // ops.py:12-20
+      const float aa = (2.f * (float)found - 1.f) * inv - 1.f;
+      const float sg = aa > 0.f ? 1.f : (aa < 0.f ? -1.f : 0.f);
+      a.wav[(long)b * a.max_steps + t] = sg * (powf(1.f + mu, fabsf(aa)) - 1.f) * inv;
+    }
+    a.code[b] = (t < a.n_teacher) ? a.teacher[t] : found;              // imodel.py:260-269
+  }
 }
 
 // gc_proj[l][b][o] = GC_EMBED[gc_id[b]] · [GC_SIGNAL_l | GC_GATE_l]  (imodel.py:53-56, :113-118)
@@ -428,12 +465,15 @@ __global__ void gen_gc_proj_kernel(const float* emb, const float* gsig, const fl
   }
 }
 
-__global__ void gen_reset_kernel(float* rings, long n_ring, int* code, int B, long long* step) {
+__global__ void gen_reset_kernel(float* rings, long n_ring, int* code, int B, long long* step, int* status) {
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n_ring; e += (long)gridDim.x * blockDim.x)
     rings[e] = 0.f;
   if (blockIdx.x == 0) {
     for (int b = threadIdx.x; b < B; b += blockDim.x) code[b] = -1;
-    if (threadIdx.x == 0) *step = 0;
+    if (threadIdx.x == 0) {
+      *step = 0;
+      *status = 0;
+    }
   }
 }
 
@@ -491,7 +531,7 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
   p->oHP = gcarve(cur, 4 * (size_t)p->ks_h * B * p->Cp);
   p->oLGP = gcarve(cur, 4 * (size_t)p->ks_lg * B * p->Q);
   p->oLOG = gcarve(cur, 4 * (size_t)B * p->Q);
-  p->oSTEP = gcarve(cur, 8);
+  p->oSTEP = gcarve(cur, 16);   // step counter + status word
   p->oCODE = gcarve(cur, 4 * (size_t)B);
   p->oTEACH = gcarve(cur, 4 * (size_t)std::max<int64_t>(1, max_teacher));
   p->oSAMP = gcarve(cur, 4 * (size_t)B * max_steps);
@@ -516,6 +556,7 @@ extern "C" int lbwn_gen_tensor(const lbwn_gen_plan* p, const char* name, size_t*
   else if (!strcmp(name, "wav")) { *off = p->oWAV; *bytes = 4 * B * p->max_steps; }
   else if (!strcmp(name, "logits")) { *off = p->oLOG; *bytes = 4 * B * p->Q; }
   else if (!strcmp(name, "step")) { *off = p->oSTEP; *bytes = 8; }
+  else if (!strcmp(name, "status")) { *off = p->oSTEP + 8; *bytes = 4; }   // reserved: 0 (the barrier-synchronised chain has no failure path)
   else if (!strcmp(name, "trace")) { *off = p->oTRACE; *bytes = 8 * (size_t)(2 * p->L + 8); }
   else if (!strcmp(name, "rings")) { *off = p->oRING; *bytes = 4 * (size_t)p->n_ring; }
   else if (!strcmp(name, "teacher")) { *off = p->oTEACH; *bytes = 4 * (size_t)std::max<long long>(1, p->n_teacher); }
@@ -539,7 +580,7 @@ extern "C" int lbwn_gen_start(lbwn_gen_plan* p, const lbwn_params* P, void* ws, 
   p->seed = seed;
   p->pre_bias = pre_bias;
   gen_reset_kernel<<<256, 256, 0, st>>>(gat<float>(ws, p->oRING), p->n_ring, gat<int>(ws, p->oCODE), p->B,
-                                        gat<long long>(ws, p->oSTEP));
+                                        gat<long long>(ws, p->oSTEP), gat<int>(ws, p->oSTEP + 8));
   LBWN_CHECK_LAUNCH();
   if (p->n_teacher > 0) {
     hipError_t e = hipMemcpyAsync(gat<int>(ws, p->oTEACH), teacher, 4 * (size_t)p->n_teacher, hipMemcpyDeviceToDevice,
@@ -572,11 +613,13 @@ extern "C" int lbwn_gen_run(lbwn_gen_plan* p, const lbwn_params* P, void* ws, in
   c.B = p->B; c.L = p->L; c.nbl = p->nbl; c.Cr = p->Cr; c.Cd = p->Cd; c.pre_bias = p->pre_bias;
   // skip = z_cat·SKIPcat (+Σb and relu applied by the consumer), h = relu(relu(skip)·POST1 + b1),
   // logits = h·POST2 + b2 (summed in the sampler)
-  GemvK sk, p1, p2;
+  GemvK sk = {}, p1 = {}, p2 = {};
   memset(&sk, 0, sizeof(sk));
   sk.in = c.zcat; sk.ldin = (long)p->L * p->Cd; sk.W = P->skip; sk.ldw = p->Cs; sk.out_part = gat<float>(ws, p->oSKP);
   sk.B = p->B; sk.K = p->L * p->Cd; sk.N = p->Cs; sk.KSL = p->ksl_skip;
+  sk.step_advance = gat<long long>(ws, p->oSTEP);   // the sampler reads step - 1
   p1 = sk;
+  p1.step_advance = nullptr;
   p1.in = nullptr; p1.in_part = sk.out_part; p1.in_parts = p->ks_skip; p1.in_bias = P->skip_b ? gat<float>(ws, p->oBSUM) : nullptr;
   p1.relu_in = 1; p1.W = P->post1; p1.ldw = p->Cp; p1.out_part = gat<float>(ws, p->oHP); p1.K = p->Cs; p1.N = p->Cp; p1.KSL = 32;
   p2 = p1;
@@ -589,13 +632,13 @@ extern "C" int lbwn_gen_run(lbwn_gen_plan* p, const lbwn_params* P, void* ws, in
   sm.teacher = gat<int>(ws, p->oTEACH); sm.n_teacher = p->n_teacher; sm.samples = gat<int>(ws, p->oSAMP);
   sm.wav = gat<float>(ws, p->oWAV); sm.max_steps = p->max_steps; sm.seed = p->seed;
   const dim3 gsk((sk.N + 63) / 64, p->ks_skip), gp1((p1.N + 63) / 64, (p1.K + 31) / 32), gp2((p2.N + 63) / 64, (p2.K + 31) / 32);
-  const size_t sample_lds = 4 * (size_t)16 * p->Q;
+  const size_t sample_lds = 4 * (size_t)p->Q;
   for (int i = 0; i < n_steps; ++i) {
     gen_wave_kernel<<<p->B, 512, 0, st>>>(c);
     gen_gemv_kernel<<<gsk, 256, 0, st>>>(sk);
     gen_gemv_kernel<<<gp1, 256, 0, st>>>(p1);
     gen_gemv_kernel<<<gp2, 256, 0, st>>>(p2);
-    gen_sample_kernel<<<1, 1024, sample_lds, st>>>(sm);
+    gen_sample_kernel<<<p->B, 256, sample_lds, st>>>(sm);
     LBWN_CHECK_LAUNCH();
   }
   return 0;

@@ -43,6 +43,7 @@ def test_gen_free_running_matches_oracle(pre_bias):
     _, wav, _ = g.run(n)
     torch.cuda.synchronize()
     s_ref, w_ref = R.generate(arch, P, B, n, seed=7, pre_bias=pre_bias)
+    assert int(g.tensor('status', torch.int32).item()) == 0     # no hand-off spin timed out
     np.testing.assert_array_equal(g.samples().cpu().numpy()[:, :n], s_ref)
     np.testing.assert_allclose(wav.cpu().numpy(), w_ref[:, :wav.shape[1]], rtol=1e-6, atol=1e-6)
 
@@ -74,3 +75,4 @@ def test_gen_arch3_b10_graph_replay():
     mism = int((got != s_ref).sum())
     assert mism == 0, '%d / %d draws differ' % (mism, got.size)
     assert int(g.tensor('step', torch.int64).item()) == n
+    assert int(g.tensor('status', torch.int32).item()) == 0
