@@ -48,6 +48,13 @@ def kernel_work(name, arch, M):
     }
     if name in flops:
         return 'mfma', flops[name]
+    if name == 'layer_bwd':
+        # the whole residual stack backward (persistent chain): conv bwd 2 x (8 Cr Cd) and
+        # residual bwd 2 x (2 Cd Cr) FLOP per layer and position; at
+        # AI = 20 Cr Cd / 640 B = 32 FLOP/B it sits right of the fp32 ridge (19.7): MFMA-bound.
+        # (The gate recompute and the weight-gradient products the chain also does are not
+        # counted: algorithmic work only.)
+        return 'mfma', 20.0 * M * Cr * Cd * L
     if name == 'layer_fwd':
         # the whole residual stack (persistent chain launch, or the span of the L per-layer
         # launches): per layer and position x_l in (Cr), x_{l+1} out (Cr), z out (Cd); the
@@ -188,8 +195,9 @@ def main():
         return s, e
 
     M = B * T
-    # single-launch GEMMs (the skip GEMM / dZ run as per-block chunks overlapping the layer chain)
-    cands = ['dskip', 'post1_fwd', 'dpost1', 'ds', 'post2_fwd', 'dpost2', 'dh']
+    # candidates for the dominant kernel, likeliest first (one probe per warmup step): the
+    # backward and forward layer chains, then the single-launch GEMMs
+    cands = ['layer_bwd', 'dskip', 'layer_fwd', 'post1_fwd', 'dpost1', 'ds', 'post2_fwd', 'dpost2', 'dh']
     warm_t = {}
     for i in range(args.warmup):
         pr = None
@@ -199,7 +207,7 @@ def main():
         if pr:
             torch.cuda.synchronize()
             warm_t[pr[0]] = pr[1][0].elapsed_time(pr[1][1])
-    dom = args.probe if args.probe != 'auto' else (max(warm_t, key=warm_t.get) if warm_t else 'dskip')
+    dom = args.probe if args.probe != 'auto' else (max(warm_t, key=warm_t.get) if warm_t else 'layer_bwd')
 
     # ---- timed region ----
     samples = {dom: [], 'layer_fwd': []}

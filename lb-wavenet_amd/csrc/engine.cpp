@@ -20,13 +20,13 @@ struct lbwn_plan {
   int Ge, ncat1, Li, Lo, nup, hop, up[8];   // conditioning (Ge = 0: no GC, Lo = 0: no LC)
   long M;
   // workspace carving (byte offsets)
-  size_t oX, oZ, oS, oR2, oLOG, oDH, oDS, oDZ, oGA[2], oGC0[2], oDX0, oSLAB, oSPLIT, oSPLIT2, oCOLS, oCOLS2,
+  size_t oX, oZ, oS, oR2, oLOG, oDH, oDS, oDZ, oGA[2], oGC0[2], oSLAB, oSPLIT, oSPLIT2, oCOLS,
       oHEADP, oBSUM, oWPK, oFLAGS, oSTATUS, oOCG;
   size_t oGCTAB, oGCD, oGCPART, oLCACT[8], oCOND, oDVALL, oLCCAT, oDLCCAT, oDLC[2];
   int split_dlc, split_up[8];
   size_t total;
   long x_layer_stride;  // floats
-  int split_post2, split_post1, split_skip, split_pre;
+  int split_post2, split_post1, split_skip;
   long split_floats;
   int nblk;                      // layer-bwd blocks = slab partials per layer
   bool chain = false;            // persistent layer-chain kernels (n_res = n_dil = 32)
@@ -166,9 +166,8 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->split_post2 = pick_split(p->Cp, p->Q, M);
   p->split_post1 = pick_split(p->Cs, p->Cp, M);
   p->split_skip = pick_split(L * p->Cd, p->Cs, M);
-  p->split_pre = pick_split(p->Q, p->Cr, M);
   p->split_floats = std::max({(long)p->split_post2 * p->Cp * p->Q, (long)p->split_post1 * p->Cs * p->Cp,
-                              (long)p->split_skip * ldz * p->Cs, (long)p->split_pre * p->Q * p->Cr});
+                              (long)p->split_skip * ldz * p->Cs});
   if (p->Lo > 0) {
     p->split_dlc = pick_split(p->Lo, 2 * L * p->Cd, M);
     p->split_floats = std::max(p->split_floats, (long)p->split_dlc * p->Lo * 2 * L * p->Cd);
@@ -197,11 +196,9 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   }
   const int ntiles = B * ((T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS);
   p->oSLAB = carve(cur, sizeof(float) * (size_t)L * std::max(nblk, ntiles) * lbwn_layer_slab_stride());
-  p->oDX0 = carve(cur, sizeof(float) * (size_t)M * p->Cr);
   p->oSPLIT = carve(cur, sizeof(float) * (size_t)p->split_floats);
-  p->oSPLIT2 = carve(cur, sizeof(float) * (size_t)p->split_pre * p->Q * p->Cr);
+  p->oSPLIT2 = carve(cur, sizeof(float) * (size_t)lbwn_pre_grad_ws_floats(p->Q, p->Cr));   // dPRE partials
   p->oCOLS = carve(cur, sizeof(float) * (size_t)lbwn_colsum_ws_floats((int)M, std::max({p->Cs, p->Cp, p->Q, p->Cr})));
-  p->oCOLS2 = carve(cur, sizeof(float) * (size_t)lbwn_colsum_ws_floats((int)M, p->Cr));
   // [status (16 B) | hand-off flags], zeroed together before every chain launch
   p->oSTATUS = carve(cur, 16 + sizeof(unsigned) * (size_t)B * ((T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS));
   p->oFLAGS = p->oSTATUS + 16;
@@ -569,7 +566,9 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     LBWN_HIP(hipEventRecord(p->ev_fork, st));
     LBWN_HIP(hipStreamWaitEvent(ws_st, p->ev_fork, 0));
   }
-  // dPOST2 = R2ᵀ·dlogits, db2 = Σ dlogits
+  // dPOST2 = R2ᵀ·dlogits, db2 = Σ dlogits.  (Kept on the aux stream: moving it to the main
+  // stream at full rate measured slower, 3.83 vs 3.68 ms: the lean GEMMs get ~25 TF beside the
+  // chain at one wave per SIMD, so the aux stream mostly runs after the chain either way.)
   g = gemm0();
   g.A = R2; g.lda = Cp; g.B = LOG; g.ldb = Q; g.C = G->post2; g.ldc = Q; g.M = Cp; g.N = Q; g.K = (int)M;
   Probe(p, ws_st, "dpost2");
@@ -659,16 +658,9 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     if ((e = lbwn_layer_reduce_all_launch(r, L, (long)p->nblk * sstr, st))) return e;
   }
   if ((e = cond_backward(p, P, G, ws, mel, st))) return e;
-  // dx_0 = (g + dcur) + shift(dprev); dPRE = onehot(q)ᵀ·dx_0, dPRE_BIAS = Σ dx_0
-  float* DX0 = at<float>(ws, p->oDX0);
-  if ((e = lbwn_shift_add_launch(DX0, at<float>(ws, p->oGA[0]), at<float>(ws, p->oGC0[0]), 1, B, T, Cr, st)))
-    return e;
-  g = gemm0();
-  g.a_codes = wav_q; g.B = DX0; g.ldb = Cr; g.C = G->pre; g.ldc = Cr; g.M = Q; g.N = Cr; g.K = (int)M;
-  g.lda = 4;  // unused (one-hot A)
-  LBWN_REQUIRE(Cr % 4 == 0, "train_backward: n_res %% 4 != 0 not supported for the PRE gradient yet");
-  if ((e = lbwn_gemm_launch(g, 0, 0, p->split_pre, at<float>(ws, p->oSPLIT2), st))) return e;
-  if (G->pre_b && (e = lbwn_colsum_launch(DX0, Cr, (int)M, Cr, G->pre_b, 0, at<float>(ws, p->oCOLS2), st)))
+  // dx_0 = (g + dcur) + shift(dprev) formed inside the scatter; dPRE = onehot(q)ᵀ·dx_0, dPRE_BIAS = Σ dx_0
+  if ((e = lbwn_pre_grad_launch(wav_q, at<float>(ws, p->oGA[0]), at<float>(ws, p->oGC0[0]), 1, B, T, Cr, Q, G->pre,
+                                G->pre_b, at<float>(ws, p->oSPLIT2), st)))
     return e;
   if (p->overlap) LBWN_HIP(hipStreamWaitEvent(st, p->ev_join, 0));
   return 0;

@@ -119,6 +119,11 @@ int lbwn_adam_launch2(float* params, const float* grads, float* m, float* v, lon
                       float lr, float b1, float b2, float eps, float l2, const float* stats,
                       const long long* counters, hipStream_t st);
 int lbwn_counters_launch(long long* counters, const float* stats, int adam_applied, hipStream_t st);
+// dPRE = onehot(q)ᵀ·dx0 as an LDS-histogram scatter + fixed-order reduction; dPRE_B = Σ dx0 (nullable);
+// dx0[m] = g[m] + (t+gd < T ? dprev[m+gd] : 0) formed on the fly
+int lbwn_pre_grad_ws_floats(int Q, int Cr);
+int lbwn_pre_grad_launch(const int* q, const float* g, const float* dprev, int gd, int B, int T, int Cr, int Q,
+                         float* dpre, float* dpre_b, float* ws, hipStream_t st);
 int lbwn_shift_add_launch(float* out, const float* a, const float* c0, int gd, int B, int T, int C,
                           hipStream_t st);
 int lbwn_head_nblocks(long M);

@@ -68,6 +68,79 @@ __global__ void shift_add_kernel(float* out, const float* a, const float* c0, in
   }
 }
 
+// ---- PRE-embedding gradient -------------------------------------------------------------
+// dPRE[q][c] = Σ_{t: code_t = q} dx0[t][c] and dPRE_B[c] = Σ_t dx0[t][c]: the transpose of the
+// one-hot product (tmodel.py:64-66; tf.one_hot: a code outside [0, Q) has no row).  A scatter
+// into an LDS histogram, not a dense GEMM against the one-hot matrix (K = B·T, M = Q, N = Cr:
+// ~200 µs of tiles that are almost all zeros).  dx0 = g + shift(dprev) (layer 0's input
+// gradient, as shift_add forms it) is formed on the fly and never stored.  One wave per block
+// walks its chunk two positions per instruction (half-wave h takes h, h+2, ...) with
+// no-return LDS float atomics (ds_add_f32: no read-modify-write round trip); a single wave's
+// atomics are applied in program and lane order, so the sums are deterministic, and the
+// block partials are reduced in a fixed order.
+constexpr int PG_BLOCKS = 128;
+constexpr int PG_BATCH = 32;
+
+__global__ __launch_bounds__(64) void pre_grad_part_kernel(const int* __restrict__ q, const float* __restrict__ g,
+                                                           const float* __restrict__ dprev, int gd, int B, int T,
+                                                           int Cr, int Q, float* part, float* bpart) {
+  extern __shared__ __attribute__((aligned(16))) float hist[];   // [Q][32]
+  const int lane = threadIdx.x, h = lane >> 5, c = lane & 31, cc = min(c, Cr - 1);
+  for (int i = lane; i < Q * 32 / 4; i += 64) ((float4*)hist)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  const long M = (long)B * T;
+  const long chunk = (M + gridDim.x - 1) / gridDim.x, m0 = blockIdx.x * chunk, m1 = min(M, m0 + chunk);
+  float bsum = 0.f;
+  for (long mb = m0 + h; mb < m1; mb += 2 * PG_BATCH) {
+    int cd[PG_BATCH];
+    float v[PG_BATCH], w[PG_BATCH];
+#pragma unroll
+    for (int i = 0; i < PG_BATCH; ++i) {   // loads first (clamped indices: no branch per load)
+      const long m = min(mb + 2 * i, m1 - 1);
+      const long ms = min(m + gd, M - 1);
+      cd[i] = q[m];
+      v[i] = g[m * Cr + cc];
+      w[i] = dprev[ms * Cr + cc];
+    }
+#pragma unroll
+    for (int i = 0; i < PG_BATCH; ++i) {
+      const long m = mb + 2 * i;
+      if (m >= m1 || c >= Cr) continue;
+      const float x = v[i] + ((int)(m % T) + gd < T ? w[i] : 0.f);
+      bsum += x;
+      if (cd[i] >= 0 && cd[i] < Q)
+        __hip_atomic_fetch_add(hist + cd[i] * 32 + c, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  __syncthreads();
+  float* P = part + (long)blockIdx.x * Q * Cr;
+  for (int e = lane; e < Q * Cr; e += 64) {
+    const int qq = e / Cr, c2 = e % Cr;
+    P[e] = hist[qq * 32 + c2];
+  }
+  const float bo = __shfl_xor(bsum, 32);
+  if (lane < Cr) bpart[(long)blockIdx.x * Cr + lane] = bsum + bo;
+}
+
+__global__ __launch_bounds__(256) void pre_grad_reduce_kernel(const float* part, const float* bpart, int nparts,
+                                                              int Q, int Cr, float* dpre, float* dpre_b) {
+  const int e = blockIdx.x * 256 + threadIdx.x, n = Q * Cr;
+  const bool bias = e >= n;
+  if (bias && (dpre_b == nullptr || e - n >= Cr)) return;
+  const float* p = bias ? bpart + (e - n) : part + e;
+  const long stride = bias ? Cr : n;
+  float s = 0.f;
+  for (int q0 = 0; q0 < nparts; q0 += 32) {
+    float v[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) v[i] = p[(long)min(q0 + i, nparts - 1) * stride];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) s += (q0 + i < nparts) ? v[i] : 0.f;
+  }
+  if (bias) dpre_b[e - n] = s;
+  else dpre[e] = s;
+}
+
 // ---- softmax cross-entropy head ------------------------------------------------------------
 // One wave per position row; dlogits (unnormalised) written in place.
 
@@ -303,6 +376,21 @@ int lbwn_dsep_save_launch(const float* xall, long xls, float* save, int L, int n
 int lbwn_embed_launch(const int* q, const float* pre, const float* pre_b, float* x0, int B, int T, int H, int Cr,
                       int Q, hipStream_t st) {
   embed_kernel<<<grid_for((long)B * T * Cr), 256, 0, st>>>(q, pre, pre_b, x0, B, T, H, Cr, Q);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_pre_grad_ws_floats(int Q, int Cr) { return PG_BLOCKS * (Q * Cr + Cr); }
+
+int lbwn_pre_grad_launch(const int* q, const float* g, const float* dprev, int gd, int B, int T, int Cr, int Q,
+                         float* dpre, float* dpre_b, float* ws, hipStream_t st) {
+  LBWN_REQUIRE(Cr >= 1 && Cr <= 32 && Q >= 1 && Q * 32 * 4 <= 65536, "pre_grad: Cr <= 32 and Q <= 512 required");
+  float* part = ws;
+  float* bpart = ws + (long)PG_BLOCKS * Q * Cr;
+  pre_grad_part_kernel<<<PG_BLOCKS, 64, Q * 32 * 4, st>>>(q, g, dprev, gd, B, T, Cr, Q, part, bpart);
+  LBWN_CHECK_LAUNCH();
+  const int n = Q * Cr + Cr;
+  pre_grad_reduce_kernel<<<(n + 255) / 256, 256, 0, st>>>(part, bpart, PG_BLOCKS, Q, Cr, dpre, dpre_b);
   LBWN_CHECK_LAUNCH();
   return 0;
 }

@@ -2,16 +2,17 @@
 dispatch).  gfx950: FETCH_SIZE counts ½ of the bytes of wide coalesced reads, so
 hbm_bytes = (2·FETCH_SIZE + WRITE_SIZE)·1024 (MI355X_MICROARCH.md § HBM).  Dispatches are
 split into training steps at pack_layers_kernel and named in launch order: the chain
-kernels by name, the GEMMs by their position in engine.cpp's fixed sequence (arch without
-LC: skip_fwd, post1_fwd, post2_fwd, dpost2, dh, dpost1, ds, dskip, dz, dpre)."""
+kernels by name, the GEMMs by their position in engine.cpp's fixed enqueue sequence (arch
+without LC or GC: skip_fwd, post1_fwd, post2_fwd, then dh, ds, dz on the main stream and
+dpost2, dpost1, dskip on the aux stream; dispatch ids follow enqueue order)."""
 import csv
 import glob
 import json
 import sys
 
-GEMM_ORDER = ['skip_fwd', 'post1_fwd', 'post2_fwd', 'dpost2', 'dh', 'dpost1', 'ds', 'dskip', 'dz', 'dpre']
+GEMM_ORDER = ['skip_fwd', 'post1_fwd', 'post2_fwd', 'dh', 'ds', 'dz', 'dpost2', 'dpost1', 'dskip']
 NAMED = {'chain_fwd_kernel': 'layer_fwd', 'chain_bwd_kernel': 'layer_bwd', 'head_kernel': 'head',
-         'layer_reduce_all_kernel': 'layer_reduce'}
+         'layer_reduce_all_kernel': 'layer_reduce', 'pre_grad_part_kernel': 'dpre'}
 
 
 def dispatches(d, counter):
