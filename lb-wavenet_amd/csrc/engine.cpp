@@ -21,7 +21,8 @@ struct lbwn_plan {
   long M;
   // workspace carving (byte offsets)
   size_t oX, oZ, oS, oR2, oLOG, oDH, oDS, oDZ, oGA[2], oGC0[2], oSLAB, oSPLIT, oSPLIT2, oCOLS,
-      oHEADP, oBSUM, oWPK, oFLAGS, oSTATUS, oOCG;
+      oHEADP, oBSUM, oWPK, oFLAGS, oSTATUS, oOCG, oCTRACE;
+  int ctrace_blk = -1;            // LBWN_CHAIN_TRACE=<block>: chain cycle stamps (debug)
   size_t oGCTAB, oGCD, oGCPART, oLCACT[8], oCOND, oDVALL, oLCCAT, oDLCCAT, oDLC[2];
   int split_dlc, split_up[8];
   size_t total;
@@ -202,6 +203,11 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   // [status (16 B) | hand-off flags], zeroed together before every chain launch
   p->oSTATUS = carve(cur, 16 + sizeof(unsigned) * (size_t)B * ((T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS));
   p->oFLAGS = p->oSTATUS + 16;
+  {
+    const char* ct = getenv("LBWN_CHAIN_TRACE");
+    p->ctrace_blk = ct ? atoi(ct) : -1;
+    p->oCTRACE = carve(cur, 8 * 2 * 16 * (size_t)L);   // [fwd, bwd][L][16]
+  }
   const char* nc = getenv("LBWN_NO_CHAIN");
   p->chain = p->Cr == 32 && p->Cd == 32 && !(nc && nc[0] == '1');
   p->oOCG = p->chain ? carve(cur, sizeof(float) * (size_t)L * M * 32) : 0;
@@ -250,6 +256,7 @@ int lbwn_plan_tensor(const lbwn_plan* p, const char* name, size_t* off, size_t* 
   else if (!strcmp(name, "r2")) { *off = p->oR2; *bytes = f * M * p->Cp; }
   else if (!strcmp(name, "logits")) { *off = p->oLOG; *bytes = f * M * p->Q; }
   else if (!strcmp(name, "status")) { *off = p->oSTATUS; *bytes = 16; }
+  else if (!strcmp(name, "ctrace")) { *off = p->oCTRACE; *bytes = 8 * 2 * 16 * (size_t)p->a.n_blocks * p->a.n_block_layers; }
   else if (!strcmp(name, "dh")) { *off = p->oDH; *bytes = f * M * p->Cp; }
   else if (!strcmp(name, "ds")) { *off = p->oDS; *bytes = f * M * p->Cs; }
   else if (!strcmp(name, "dz")) { *off = p->oDZ; *bytes = f * M * p->L * p->Cd; }
@@ -455,6 +462,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     c.X = X; c.xls = p->x_layer_stride; c.Z = Z; c.ldz = ldz; c.wpack = WPK; c.ids = ids;
     c.gc_tab = cd.gc_tab; c.gc_ld = cd.gc_ld; c.cond = cd.cond; c.ldcond = cd.ldcond;
     c.flags = at<unsigned>(ws, p->oFLAGS); c.status = at<unsigned>(ws, p->oSTATUS);
+    if (p->ctrace_blk >= 0) { c.trace = at<long long>(ws, p->oCTRACE); c.trace_blk = p->ctrace_blk; }
     c.B = B; c.T = T; c.H = H; c.L = L; c.nbl = p->nbl; c.Cr = Cr; c.Cd = Cd; c.grid = p->chain_grid;
     Probe(p, st, "layer_fwd");
     if ((e = lbwn_chain_fwd_launch(c, st))) return e;
@@ -620,6 +628,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     c.gc_dtab = cd.gc_dtab; c.dv_out = cd.dv_out; c.lddv = cd.ldcond;
     c.dx0_a = at<float>(ws, p->oGA[0]); c.dx0_c = at<float>(ws, p->oGC0[0]);
     c.flags = at<unsigned>(ws, p->oFLAGS); c.status = at<unsigned>(ws, p->oSTATUS);
+    if (p->ctrace_blk >= 0) { c.trace = at<long long>(ws, p->oCTRACE); c.trace_blk = p->ctrace_blk; }
     c.B = B; c.T = T; c.H = p->H; c.L = L; c.nbl = p->nbl; c.Cr = Cr; c.Cd = Cd; c.grid = p->chain_grid;
     Probe(p, st, "layer_bwd");
     if ((e = lbwn_chain_bwd_launch(c, st))) return e;

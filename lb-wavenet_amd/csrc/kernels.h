@@ -81,6 +81,8 @@ struct lbwn_chain_args {
   float* slab;                 // [L][ntiles][slab_stride]
   float* ocg; long ocls;       // out_c0 hand-off rows per layer [L][B·T][32]
   float* dx0_a; float* dx0_c;  // layer 0's dx parts [B·T][32]
+  long long* trace = nullptr;  // debug: cycle stamps of block trace_blk, [L][16] (LBWN_CHAIN_TRACE)
+  int trace_blk = 0;
 };
 int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st);
 int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st);

@@ -95,8 +95,10 @@ LBWN_DEV void stage_rows(float* dst, const float* __restrict__ xb, int t0, int s
     for (int i = 0; i < 4; ++i) {
       const int e = tid + 256 * i;
       const int r = e >> 3, c4 = (e & 7) * 4;
-      v[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-      if (t0 + r < T) v[i] = *(const floatx4*)(xb + (long)(H + t0 + r + shift) * 32 + c4);
+      // unconditional load of a clamped row, then select: a predicated load would sit behind
+      // a branch and hipcc waits for each one (one memory round trip per row group)
+      v[i] = *(const floatx4*)(xb + (long)(H + min(t0 + r, T - 1) + shift) * 32 + c4);
+      if (t0 + r >= T) v[i] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -126,10 +128,10 @@ LBWN_DEV void stage_g(float* G, const float* __restrict__ ga, const float* __res
     for (int i = 0; i < 4; ++i) {
       const int e = tid + 256 * i;
       const int r = e >> 3, c4 = (e & 7) * 4, t = t0 + r;
-      v[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-      u[i] = v[i];
-      if (t < T) v[i] = *(const floatx4*)(ga + (mb + t) * 32 + c4);
-      if (t + gd < T) u[i] = *(const floatx4*)(gc + (mb + t + gd) * 32 + c4);
+      v[i] = *(const floatx4*)(ga + (mb + min(t, T - 1)) * 32 + c4);       // clamped, then select
+      u[i] = *(const floatx4*)(gc + (mb + min(t + gd, T - 1)) * 32 + c4);
+      if (t >= T) v[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (t + gd >= T) u[i] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -298,6 +300,7 @@ struct ChainFK {
   const int* ids; const float* cond; long ldcond; // LC term COND [M][L·2Cd] (layer l at column l·2Cd) or null
   unsigned* flags; unsigned* status;
   int B, T, H, L, nbl, Cd;
+  long long* trace; int trace_blk;   // debug stamps (null in production)
 };
 
 // GC + LC term of layer l for this lane's position, in acc layout: cv[q] = sig channels
@@ -422,7 +425,7 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
 #pragma unroll
         for (int i = 0; i < IMG_PF; ++i) {
           const int e = tid + 256 * i;
-          if (e < WIMG / 4) pf[i] = src[e];
+          pf[i] = src[min(e, WIMG / 4 - 1)];   // clamped: no load behind a branch
         }
       }
       // 2. own tap first: W1·x[t]
@@ -443,10 +446,16 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
         const int nh = min(d, LP);
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc(xl, (short)0, (int)((long)(a.H + a.T) * 32 * 4), BUF_DW3);
-        for (int e = tid; e < nh * 8; e += 256) {
-          const int row = e >> 3, c4 = (e & 7) * 4;
-          const int off = ((a.H + t0 + row - d) * 32 + c4) * 4;
-          *(floatx4*)(HALO + row * XS + c4) = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+        floatx4 hv[4];   // all four issued before the first is stored (clamped rows)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = min(tid + 256 * i, nh * 8 - 1), row = e >> 3, c4 = (e & 7) * 4;
+          hv[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((a.H + t0 + row - d) * 32 + c4) * 4, 0, 16);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = tid + 256 * i;
+          if (e < nh * 8) *(floatx4*)(HALO + (e >> 3) * XS + (e & 7) * 4) = hv[i];
         }
       }
       __syncthreads();
@@ -572,6 +581,7 @@ struct ChainBK {
   float* gc_dtab;              // GC gradient table, layout of gc_tab, atomics, or null
   unsigned* flags; unsigned* status;
   int B, T, H, L, nbl, Cd;
+  long long* trace; int trace_blk;   // debug stamps (null in production)
 };
 
 // dv rows of wave w's 32 positions (DV, position-major) scatter-added into the GC gradient
@@ -643,7 +653,10 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
     floatx16 oa;  // out_a of layer l+1, own row
 #pragma unroll
     for (int q = 0; q < 16; ++q) oa[q] = 0.f;
+    const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && it == (int)blockIdx.x;
+#define CSTAMP(i) if (trc) a.trace[16 * l + (i)] = clock64()
     for (int l = a.L - 1; l >= 0; --l) {
+      CSTAMP(0);
       const int d = 1 << (l % a.nbl);
       const int dn = (l + 1 < a.L) ? 1 << ((l + 1) % a.nbl) : 0;
       const float* xl = a.X + (long)l * a.xls + sb;
@@ -653,8 +666,8 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
       floatx16 dz;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        floatx4 v = {0.f, 0.f, 0.f, 0.f};
-        if (valid) v = *(const floatx4*)(a.DZ + m * a.lddz + (long)l * a.Cd + 8 * q + 4 * h);
+        floatx4 v = *(const floatx4*)(a.DZ + (mb + min(t, a.T - 1)) * a.lddz + (long)l * a.Cd + 8 * q + 4 * h);
+        if (!valid) v = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < 4; ++j) dz[4 * q + j] = v[j];
       }
@@ -664,10 +677,11 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
 #pragma unroll
         for (int i = 0; i < IMG_PF; ++i) {
           const int e = tid + 256 * i;
-          if (e < WIMG / 4) pf[i] = src[e];
+          pf[i] = src[min(e, WIMG / 4 - 1)];   // clamped: no load behind a branch
         }
       }
       __syncthreads();
+      CSTAMP(1);
       // 1. recompute the gate (no cross-tile dependency)
       floatx16 acc_s, acc_g;
       conv_init(bs, cv, h, acc_s, acc_g);
@@ -680,6 +694,7 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
         th[q] = tanhf_(acc_s[q]);
         sg[q] = sigmoidf_(acc_g[q]);
       }
+      CSTAMP(2);
       // 2. G = dx_{l+1} rows of this tile: out_c0_{l+1}[t + dn] (own LDS / published rows) + out_a
       if (dn) {
         const int ptt = tt + max(1, dn / LP);
@@ -691,17 +706,26 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
         }
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)(l + 1) * a.ocls, (short)0, oc_bytes, BUF_DW3);
-        for (int e = tid; e < LP * 8; e += 256) {
-          const int row = e >> 3, c4 = (e & 7) * 4, sr = row + dn, ts = t0 + sr;
-          floatx4 v = {0.f, 0.f, 0.f, 0.f};
-          if (ts < a.T) {
-            if (sr < LP) v = *(const floatx4*)(OC + sr * XS + c4);
-            else v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
-          }
+        // rows from the own tile's OC (LDS) or the producer's published rows (sc1 loads): all
+        // loads issued unconditionally at clamped indices, then selected (no load behind a branch)
+        floatx4 gl[4], go[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = tid + 256 * i, row = e >> 3, c4 = (e & 7) * 4, sr = row + dn;
+          const int ts = min(t0 + sr, a.T - 1);
+          gl[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
+          go[i] = *(const floatx4*)(OC + min(sr, LP - 1) * XS + c4);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = tid + 256 * i, row = e >> 3, c4 = (e & 7) * 4, sr = row + dn, ts = t0 + sr;
+          floatx4 v = sr < LP ? go[i] : gl[i];
+          if (ts >= a.T) v = floatx4{0.f, 0.f, 0.f, 0.f};
           *(floatx4*)(G + row * XS + c4) = v;
         }
         __syncthreads();
       }
+      CSTAMP(3);
       floatx16 gv;
       {  // own row: + out_a (at the top layer g = 0: the row is written here, not read)
         float* grow = G + r * XS;
@@ -744,6 +768,7 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
           }
         }
       }
+      CSTAMP(4);
       // 4. dx: out_a = g + W1·dv, out_c0 = W0·dv
       floatx16 acc_a = gv, acc_c;
 #pragma unroll
@@ -789,12 +814,14 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
         store_rows16(a.dx0_c + m * 32, acc_c, 32, h);
       }
       oa = acc_a;
+      CSTAMP(5);
       // publish out_c0_l (every wave drains its sc1 stores, barrier, one lane signals)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // also: DV complete, the weight image is dead
       if (tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
       if (a.gc_dtab) gc_scatter(a.gc_dtab + (long)l * 64, a.gc_ld, a.ids + mb, DV, t0, a.T, w, lane, 32,
                                 wave_uni ? wave_id : -1);
+      CSTAMP(6);
       // 5. weight gradients of layer l over this tile
       {
         float* zrow = ZT + r * XS;
@@ -810,28 +837,34 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) { accW[q] = 0.f; accR[q] = 0.f; }
       {  // dSIG/dGATE tile w: A[i=in][k=pos] = X[pos][in], B[k][j=o] = DV[pos][o]
+        // Operands for 16 MFMAs are read one chunk ahead; the sched_barriers keep hipcc from
+        // sinking each read next to its MFMA (at this kernel's register pressure it otherwise
+        // does, and every MFMA waits out an LDS round trip: ~3.5x the MFMA time)
         const float* X = (w & 1) ? Xc : Xp;
         const int oc = (w >> 1) * 32 + pi;
-        float xa[2][8], da[2][8];
-        auto loadb = [&](int bt, int buf) {
+        float xa[2][16], da[2][16];
+        auto loadc = [&](int c, int buf) {
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const int p = 2 * (8 * bt + i) + h;
+          for (int i = 0; i < 16; ++i) {
+            const int p = 2 * (16 * c + i) + h;
             xa[buf][i] = X[p * XS + pi];
             da[buf][i] = DV[p * DS + oc];
           }
         };
-        loadb(0, 0);
+        loadc(0, 0);
 #pragma unroll
-        for (int bt = 0; bt < LP / 16; ++bt) {
-          const int cb = bt & 1;
-          if (bt + 1 < LP / 16) loadb(bt + 1, cb ^ 1);
+        for (int c = 0; c < LP / 32; ++c) {
+          const int cb = c & 1;
+          if (c + 1 < LP / 32) loadc(c + 1, cb ^ 1);
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) accW = mfma32(xa[cb][i], da[cb][i], accW);
+          for (int i = 0; i < 16; ++i) accW = mfma32(xa[cb][i], da[cb][i], accW);
+          __builtin_amdgcn_sched_barrier(0);
         }
       }
+      CSTAMP(7);
       __syncthreads();  // ZT visible; Xp/Xc free for RED
-      {  // dRES part over this wave's 32 positions
+      {  // dRES part over this wave's 32 positions (all operands read before the first MFMA)
         float za[16], ga[16];
 #pragma unroll
         for (int s2 = 0; s2 < 16; ++s2) {
@@ -839,9 +872,11 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
           za[s2] = ZT[p * XS + pi];
           ga[s2] = G[p * XS + pi];
         }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int s2 = 0; s2 < 16; ++s2) accR = mfma32(za[s2], ga[s2], accR);
       }
+      CSTAMP(8);
       float* slab = a.slab + ((long)l * ntiles + tile) * SLAB;
       {  // bias partials: column sums of DV (64) and G (32)
         float* part = RED + 4096;  // [8][96] after the dRES exchange area
@@ -873,6 +908,7 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
         for (int e = tid; e < 1024; e += 256)
           slab[4096 + e] = ((RED[e] + RED[1024 + e]) + RED[2048 + e]) + RED[3072 + e];
       }
+      CSTAMP(9);
       // 6. next layer's weight image (ZT is dead: every wave passed the barrier after dRES)
       if (l > 0) {
 #pragma unroll
@@ -882,7 +918,9 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
         }
       }
       __syncthreads();
+      CSTAMP(10);
     }
+#undef CSTAMP
   }
 }
 
@@ -949,8 +987,8 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(BwdK a) {
     if (a.Cd == 32) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        floatx4 v = {0.f, 0.f, 0.f, 0.f};
-        if (valid) v = *(const floatx4*)(a.dz_skip + m * a.lddz + 8 * q + 4 * h);
+        floatx4 v = *(const floatx4*)(a.dz_skip + (mb + min(t, a.T - 1)) * a.lddz + 8 * q + 4 * h);
+        if (!valid) v = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < 4; ++j) dz[4 * q + j] = v[j];
       }
@@ -1225,6 +1263,7 @@ int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   k.gc_tab = c.gc_tab; k.gc_ld = c.gc_ld; k.ids = c.ids; k.cond = c.cond; k.ldcond = c.ldcond;
   k.flags = c.flags; k.status = c.status;
   k.B = c.B; k.T = c.T; k.H = c.H; k.L = c.L; k.nbl = c.nbl; k.Cd = c.Cd;
+  k.trace = c.trace; k.trace_blk = c.trace_blk;
   const int tps = (c.T + LP - 1) / LP;
   LBWN_REQUIRE((unsigned*)c.status + 4 == c.flags, "chain: status word must head the flag block");
   LBWN_HIP(hipMemsetAsync(c.status, 0, (16 + (size_t)c.B * tps * 4 + 15) / 16 * 16, st));
@@ -1244,6 +1283,7 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   k.dv_out = c.dv_out; k.lddv = c.lddv; k.gc_dtab = c.gc_dtab;
   k.flags = c.flags; k.status = c.status;
   k.B = c.B; k.T = c.T; k.H = c.H; k.L = c.L; k.nbl = c.nbl; k.Cd = c.Cd;
+  k.trace = c.trace ? c.trace + 16L * c.L : nullptr; k.trace_blk = c.trace_blk;
   const int tps = (c.T + LP - 1) / LP;
   LBWN_REQUIRE((unsigned*)c.status + 4 == c.flags, "chain: status word must head the flag block");
   LBWN_HIP(hipMemsetAsync(c.status, 0, (16 + (size_t)c.B * tps * 4 + 15) / 16 * 16, st));

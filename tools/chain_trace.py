@@ -1,0 +1,41 @@
+"""Cycle-stamp trace of the backward layer chain for one block's tile (arch3, B=8, T=4096):
+per layer, the segments between the stamps in chain_bwd_kernel.  LBWN_CHAIN_TRACE=<block>
+(set here; block k runs tile ntiles-1-k).  Usage: python tools/chain_trace.py [block]"""
+import os
+import sys
+
+BLK = sys.argv[1] if len(sys.argv) > 1 else '1'
+os.environ['LBWN_CHAIN_TRACE'] = BLK
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'lb-wavenet_amd'))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from lbwn.arch import load_arch, n_layers  # noqa: E402
+from lbwn.tmodel import WaveNetTrain  # noqa: E402
+
+arch = load_arch(os.path.join(ROOT, 'par', 'arch3.json'))
+B, T = 8, 4096
+L = n_layers(arch)
+net = WaveNetTrain(**arch, batch_sz=B, l2_factor=0.0, print_interval=0, seed=0)
+g = torch.Generator().manual_seed(0)
+q = torch.randint(0, 256, (B, T), generator=g, dtype=torch.int32).cuda()
+ids = torch.ones(B, T, dtype=torch.int32).cuda()
+runs = []
+for i in range(6):
+    net.forward(q, None, ids, backward=True)
+    torch.cuda.synchronize()
+    if i >= 2:
+        runs.append(net.plan_tensor(T, 'ctrace').view(torch.int64).cpu().numpy().reshape(2, L, 16).copy())
+tr = np.median(np.array(runs), axis=0)[1].astype(np.int64)   # backward
+names = ['stage x/dz + bar', 'gate recompute', 'G wait+build', 'dz,dv,DV', 'dx MFMA+OC', 'publish bar',
+         'dSIG MFMA', 'bar+dRES', 'bias+slab+bar', 'image+bar']
+seg = np.diff(tr[:, :11], axis=1)          # [L][10]
+order = list(range(L - 1, -1, -1))         # execution order: top layer first
+seg = seg[order]
+med = np.median(seg[1:-1], axis=0)
+tot = np.median(tr[:, 10] - tr[:, 0])
+print('chain_bwd block %s, per layer (median cycles over layers):' % BLK)
+for n, m in zip(names, med):
+    print('  %-18s %6d  (%4.1f %%)' % (n, m, 100.0 * m / tot))
+print('  layer total        %6d  = %.2f us at 2.4 GHz;  whole tile %d cycles = %.0f us' %
+      (tot, tot / 2400.0, tr[0, 10] - tr[L - 1, 0], (tr[0, 10] - tr[L - 1, 0]) / 2400.0))
