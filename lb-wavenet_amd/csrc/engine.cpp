@@ -36,9 +36,10 @@ struct lbwn_plan {
   // layer chain, which keeps the MFMA pipes ~1/3 busy at one wave per SIMD, so they run on
   // a low-priority stream in lean-LDS form (21 KB beside the chain's 131 KB block).
   bool overlap = false;
+  bool dskip_main = false;       // dSKIP after the chain on the main stream at full rate (else aux, lean)
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  size_t oSPLIT_AUX = 0, oCOLS_AUX = 0;
+  size_t oSPLIT_AUX = 0;
   ~lbwn_plan() {
     if (aux) (void)hipStreamDestroy(aux);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
@@ -213,9 +214,10 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->oOCG = p->chain ? carve(cur, sizeof(float) * (size_t)L * M * 32) : 0;
   const char* ov = getenv("LBWN_OVERLAP");
   p->overlap = p->chain && !(ov && ov[0] == '0');
+  const char* dm = getenv("LBWN_DSKIP_MAIN");
+  p->dskip_main = p->overlap && dm && dm[0] == '1';
   if (p->overlap) {
     p->oSPLIT_AUX = carve(cur, sizeof(float) * (size_t)p->split_floats);
-    p->oCOLS_AUX = carve(cur, sizeof(float) * (size_t)lbwn_colsum_ws_floats((int)M, std::max({p->Cs, p->Cp, p->Q})));
   }
   {  // conditioning
     const size_t f = sizeof(float);
@@ -560,17 +562,24 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   Probe(p, st, "dz");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
   Probe::end(p, st, "dz");
+  // bias gradients (column sums of dlogits, dH1, dS; every layer's SKIP_BIAS gets the same Σ dS):
+  // here on the main stream, before the fork (small kernels on the least-priority stream beside a
+  // resident chain can wait hundreds of µs for a CU)
+  if (G->post2_b && (e = lbwn_colsum_launch(LOG, Q, (int)M, Q, G->post2_b, 0, COLS, st))) return e;
+  if (G->post1_b && (e = lbwn_colsum_launch(DH, Cp, (int)M, Cp, G->post1_b, 0, COLS, st))) return e;
+  if (G->skip_b) {
+    if ((e = lbwn_colsum_launch(DS, Cs, (int)M, Cs, G->skip_b, 0, COLS, st))) return e;
+    if ((e = lbwn_bcast_rows_launch(G->skip_b, L, Cs, st))) return e;
+  }
   // weight gradients of the head and skip GEMMs: beside the layer chain (aux stream) or here
   hipStream_t ws_st = st;
   float* WSPL = SPL;
-  float* WCOLS = COLS;
   auto wgemm = [&](const lbwn_gemm_args& a, int split) {
     return p->overlap ? lbwn_gemm_launch_lean(a, 0, 0, split, WSPL, ws_st) : lbwn_gemm_launch(a, 0, 0, split, WSPL, ws_st);
   };
   if (p->overlap) {
     ws_st = p->aux;
     WSPL = at<float>(ws, p->oSPLIT_AUX);
-    WCOLS = at<float>(ws, p->oCOLS_AUX);
     LBWN_HIP(hipEventRecord(p->ev_fork, st));
     LBWN_HIP(hipStreamWaitEvent(ws_st, p->ev_fork, 0));
   }
@@ -582,7 +591,6 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   Probe(p, ws_st, "dpost2");
   if ((e = wgemm(g, p->split_post2))) return e;
   Probe::end(p, ws_st, "dpost2");
-  if (G->post2_b && (e = lbwn_colsum_launch(LOG, Q, (int)M, Q, G->post2_b, 0, WCOLS, ws_st))) return e;
   // dPOST1 = relu(S)ᵀ·dH1, db1 = Σ dH1
   g = gemm0();
   g.A = S; g.lda = Cs; g.relu_a = 1; g.B = DH; g.ldb = Cp; g.C = G->post1; g.ldc = Cp; g.M = Cs; g.N = Cp;
@@ -590,17 +598,18 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   Probe(p, ws_st, "dpost1");
   if ((e = wgemm(g, p->split_post1))) return e;
   Probe::end(p, ws_st, "dpost1");
-  if (G->post1_b && (e = lbwn_colsum_launch(DH, Cp, (int)M, Cp, G->post1_b, 0, WCOLS, ws_st))) return e;
   // dSKIPcat = Zcatᵀ·dS; every layer's SKIP_BIAS gets the same Σ dS
-  g = gemm0();
-  g.A = Z; g.lda = ldz; g.B = DS; g.ldb = Cs; g.C = G->skip; g.ldc = Cs; g.M = (int)ldz; g.N = Cs; g.K = (int)M;
-  Probe(p, ws_st, "dskip");
-  if ((e = wgemm(g, p->split_skip))) return e;
-  Probe::end(p, ws_st, "dskip");
-  if (G->skip_b) {
-    if ((e = lbwn_colsum_launch(DS, Cs, (int)M, Cs, G->skip_b, 0, WCOLS, ws_st))) return e;
-    if ((e = lbwn_bcast_rows_launch(G->skip_b, L, Cs, ws_st))) return e;
-  }
+  auto dskip = [&](hipStream_t s2, bool lean, float* spl) -> int {
+    int e2;
+    g = gemm0();
+    g.A = Z; g.lda = ldz; g.B = DS; g.ldb = Cs; g.C = G->skip; g.ldc = Cs; g.M = (int)ldz; g.N = Cs; g.K = (int)M;
+    Probe(p, s2, "dskip");
+    if ((e2 = lean ? lbwn_gemm_launch_lean(g, 0, 0, p->split_skip, spl, s2)
+                   : lbwn_gemm_launch(g, 0, 0, p->split_skip, spl, s2))) return e2;
+    Probe::end(p, s2, "dskip");
+    return 0;
+  };
+  if (!p->dskip_main && (e = dskip(ws_st, p->overlap, WSPL))) return e;
   if (p->overlap) LBWN_HIP(hipEventRecord(p->ev_join, ws_st));
   // residual stack in reverse (conditioning recomputed from the forward's GCTAB / COND)
   Cond cd;
@@ -667,6 +676,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     if ((e = lbwn_layer_reduce_all_launch(r, L, (long)p->nblk * sstr, st))) return e;
   }
   if ((e = cond_backward(p, P, G, ws, mel, st))) return e;
+  if (p->dskip_main && (e = dskip(st, false, SPL))) return e;
   // dx_0 = (g + dcur) + shift(dprev) formed inside the scatter; dPRE = onehot(q)ᵀ·dx_0, dPRE_BIAS = Σ dx_0
   if ((e = lbwn_pre_grad_launch(wav_q, at<float>(ws, p->oGA[0]), at<float>(ws, p->oGC0[0]), 1, B, T, Cr, Q, G->pre,
                                 G->pre_b, at<float>(ws, p->oSPLIT2), st)))

@@ -259,21 +259,21 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __rest
     *(floatx4*)(part + (long)blockIdx.x * N + 4 * t) = tot;
   }
 }
-__global__ __launch_bounds__(1024) void colsum_final_kernel(const float* part, int nparts, int N, float* out,
-                                                            int accumulate) {
-  __shared__ float red[1024];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), lane = threadIdx.x >> 6;  // 16 part lanes
+// 256 threads (4 part lanes × 64 columns): a 1024-thread block needs 16 free wave slots on one
+// CU, which beside a resident layer chain and the aux-stream GEMMs it waited ~430 µs for
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* part, int nparts, int N, float* out,
+                                                           int accumulate) {
+  __shared__ float red[256];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), lane = threadIdx.x >> 6;  // 4 part lanes
   float s = 0.f;
   if (c < N) {
 #pragma unroll 8
-    for (int p = lane; p < nparts; p += 16) s += part[(long)p * N + c];
+    for (int p = lane; p < nparts; p += 4) s += part[(long)p * N + c];
   }
   red[threadIdx.x] = s;
   __syncthreads();
   if (threadIdx.x < 64 && c < N) {
-    float tot = 0.f;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) tot += red[k * 64 + threadIdx.x];
+    const float tot = ((red[threadIdx.x] + red[64 + threadIdx.x]) + red[128 + threadIdx.x]) + red[192 + threadIdx.x];
     out[c] = accumulate ? out[c] + tot : tot;
   }
 }
@@ -425,7 +425,7 @@ int lbwn_colsum_launch(const float* X, long ldx, int M, int N, float* out, int a
   LBWN_REQUIRE(N % 4 == 0 && N <= 1024 && ldx % 4 == 0, "colsum: N %% 4 / N <= 1024 / ldx %% 4 required");
   const int np = (M + CS_ROWS - 1) / CS_ROWS;
   colsum_partial_kernel<<<np, 256, 0, st>>>(X, ldx, M, N, ws);
-  colsum_final_kernel<<<(N + 63) / 64, 1024, 0, st>>>(ws, np, N, out, accumulate);
+  colsum_final_kernel<<<(N + 63) / 64, 256, 0, st>>>(ws, np, N, out, accumulate);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
