@@ -87,6 +87,14 @@ __global__ void pack_layers_kernel(const float* sig, const float* gate, const fl
 // ---- LDS staging ---------------------------------------------------------------------
 
 // dst[r][0..31] = x row (t0 + r + shift) of the halo buffer xb, zero if t0+r >= T.
+// orders this wave's LDS writes before its later LDS reads of another lane's data (LDS ops of
+// one wave are performed in issue order; this stops hipcc from reordering them) — no barrier
+LBWN_DEV void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 LBWN_DEV void stage_rows(float* dst, const float* __restrict__ xb, int t0, int shift, int T, int H, int C,
                          int tid) {
   if (C == 32) {
@@ -383,17 +391,24 @@ LBWN_DEV void conv_half(const float* xrow, const float* Wk, int pi, int h, float
 }
 
 static_assert(4096 + 768 <= 2 * LP * XS, "RED + bias partials must fit in Xp and Xc");
-constexpr int CF_LDS = 3 * LP * XS + WIMG;          // Xc[2] | HALO | IMG  (77.7 KB)
+constexpr int CF_LDS = 3 * LP * XS + 2 * WIMG;      // Xc[2] | HALO | IMG[2]  (99.8 KB)
 constexpr int IMG_PF = (WIMG / 4 + 255) / 256;      // float4 per thread to prefetch an image
 
+// Per layer l (weight image IMG[l&1]):
+//   wait for the producer tile's x_l, halo rows (sc1 loads), barrier;
+//   dilated tap W0·x[t-d] onto the accumulators that already hold W1·x[t] (done last layer);
+//   gate; residual → x_{l+1} to LDS and (sc1) to HBM;
+//   the NEXT layer's own tap W1'·x_{l+1}[t]: it reads only rows this wave just wrote, so it needs
+//   no barrier and runs while the x stores drain; then drain, barrier, publish, z store, and
+//   the image of layer l+2 into IMG[l&1] (dead after that barrier; first read after the next
+//   layer's halo barrier).  Double-buffered images are what let the own tap move: one image
+//   forced a barrier between this layer's last read and the next layer's first.
 __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
   __shared__ __attribute__((aligned(16))) float sm[CF_LDS];
   __shared__ int s_fail;
   float* HALO = sm + 2 * LP * XS;
-  float* Ws = HALO + LP * XS;
-  float* Rs = Ws + 64 * WS;
-  float* bs = Rs + 32 * XS;
-  float* br = bs + 64;
+  float* IMG0 = HALO + LP * XS;
+  auto img = [&](int l) { return IMG0 + (l & 1) * WIMG; };   // [W 64×WS | R 32×XS | bs 64 | br 32]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int pi = lane & 31, h = lane >> 5;
   const int r = 32 * w + pi;  // this lane's row of the tile
@@ -410,30 +425,35 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
     floatx4 cv[8];
     load_cond(a, 0, myid, m, valid && has_cond, h, cv);
     __syncthreads();  // previous tile's LDS use done
-    stage_image(Ws, a.wpack, tid);
+    stage_image(img(0), a.wpack, tid);
+    if (a.L > 1) stage_image(img(1), a.wpack + WIMG, tid);
     stage_rows(sm, a.X + sb, t0, 0, a.T, a.H, 32, tid);  // x_0 (embed output, pre-launch)
     __syncthreads();
+    // layer 0's own tap W1·x_0[t]
+    floatx16 acc_s, acc_g;
+    conv_init(img(0) + 64 * WS + 32 * XS, cv, h, acc_s, acc_g);
+    if (has_cond && a.L > 1) load_cond(a, 1, myid, m, valid, h, cv);
+    conv_half(sm + r * XS, img(0) + 32 * WS, pi, h, acc_s, acc_g);
+    const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && tile == (int)blockIdx.x;
+#define FSTAMP(i) if (trc) a.trace[16 * l + (i)] = clock64()
     for (int l = 0; l < a.L; ++l) {
+      FSTAMP(0);
       const int d = 1 << (l % a.nbl);
       float* cur = sm + (l & 1) * LP * XS;
       float* nxt = sm + ((l + 1) & 1) * LP * XS;
       float* xl = a.X + (long)l * a.xls + sb;
-      // 1. prefetch the next layer's weight image (pre-launch data: plain loads)
+      const float* Wl = img(l);
+      const float* Rs = Wl + 64 * WS;
+      const float* br = Rs + 32 * XS + 64;
+      // 1. prefetch the image of layer l+2 (pre-launch data: plain loads, clamped: no branch)
       floatx4 pf[IMG_PF];
-      if (l + 1 < a.L) {
-        const floatx4* src = (const floatx4*)(a.wpack + (long)(l + 1) * WIMG);
+      if (l + 2 < a.L) {
+        const floatx4* src = (const floatx4*)(a.wpack + (long)(l + 2) * WIMG);
 #pragma unroll
-        for (int i = 0; i < IMG_PF; ++i) {
-          const int e = tid + 256 * i;
-          pf[i] = src[min(e, WIMG / 4 - 1)];   // clamped: no load behind a branch
-        }
+        for (int i = 0; i < IMG_PF; ++i) pf[i] = src[min(tid + 256 * i, WIMG / 4 - 1)];
       }
-      // 2. own tap first: W1·x[t]
-      floatx16 acc_s, acc_g;
-      conv_init(bs, cv, h, acc_s, acc_g);
-      if (has_cond && l + 1 < a.L) load_cond(a, l + 1, myid, m, valid, h, cv);
-      conv_half(cur + r * XS, Ws + 32 * WS, pi, h, acc_s, acc_g);
-      // 3. wait for the producer of the halo rows (x_l is layer l-1's output)
+      FSTAMP(1);
+      // 2. wait for the producer of the halo rows (x_l is layer l-1's output)
       const int ptt = tt - max(1, d / LP);
       if (l > 0 && ptt >= 0) {
         if (tid == 0 && !s_fail) {
@@ -441,7 +461,8 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
         }
         __syncthreads();
       }
-      // 4. halo rows [0, min(d,LP)): x_l rows t0-d+row (SAVE rows when < 0), sc1 loads
+      FSTAMP(2);
+      // 3. halo rows [0, min(d,LP)): x_l rows t0-d+row (SAVE rows when < 0), sc1 loads
       {
         const int nh = min(d, LP);
         const __amdgpu_buffer_rsrc_t rs =
@@ -459,13 +480,21 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
         }
       }
       __syncthreads();
-      // 5. dilated tap W0·x[t-d], gate, residual
+      FSTAMP(3);
+      // 4. residual weights read now (they wait behind the conv, not in front of the residual)
+      float ra[16];
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) ra[s2] = Rs[acc_row(s2, h) * XS + pi];
+      __builtin_amdgcn_sched_barrier(0);
+      // 5. dilated tap W0·x[t-d], gate
       const float* xp = (r >= d) ? cur + (r - d) * XS : HALO + r * XS;
-      conv_half(xp, Ws, pi, h, acc_s, acc_g);
+      conv_half(xp, Wl, pi, h, acc_s, acc_g);
       floatx16 z;
 #pragma unroll
       for (int q = 0; q < 16; ++q) z[q] = tanhf_(acc_s[q]) * sigmoidf_(acc_g[q]);
+      FSTAMP(4);
       if (l + 1 < a.L) {
+        // 6. residual: x_{l+1} = x_l + br + RES·z → LDS (next layer's rows) and HBM (sc1)
         floatx16 acc_r;
         const float* xc = cur + r * XS;
 #pragma unroll
@@ -475,9 +504,6 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc_r[4 * q + j] = xv[j] + bv[j];
         }
-        float ra[16];
-#pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) ra[s2] = Rs[acc_row(s2, h) * XS + pi];
 #pragma unroll
         for (int s2 = 0; s2 < 16; ++s2) acc_r = mfma32(ra[s2], z[s2], acc_r);
         float* xn = a.X + (long)(l + 1) * a.xls + sb;
@@ -490,22 +516,33 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
           *(floatx4*)(nrow + 8 * q + 4 * h) = v;
           if (valid) __builtin_amdgcn_raw_buffer_store_b128(v, rn, ((a.H + t) * 32 + 8 * q + 4 * h) * 4, 0, 16);
         }
+        // 7. the next layer's own tap from the row this wave just wrote (wave-local: no barrier)
+        //    while the x stores drain; its image IMG[(l+1)&1] landed before this layer's barriers
+        wave_lds_fence();
+        const float* Wn = img(l + 1);
+        conv_init(Wn + 64 * WS + 32 * XS, cv, h, acc_s, acc_g);
+        if (has_cond && l + 2 < a.L) load_cond(a, l + 2, myid, m, valid, h, cv);
+        conv_half(nrow, Wn + 32 * WS, pi, h, acc_s, acc_g);
       }
-      // 6. publish x_{l+1}: every wave drains its sc1 stores, barrier, one lane signals
+      FSTAMP(5);
+      // 8. publish x_{l+1}: every wave drains its sc1 stores, barrier, one lane signals
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0 && l + 1 < a.L) publish_flag(a.flags + tile, (unsigned)(l + 1));
       if (valid) store_rows16(a.Z + m * a.ldz + (long)l * a.Cd, z, a.Cd, h);  // skip GEMM input
-      // 7. next weight image (everyone is past this layer's reads of IMG)
-      if (l + 1 < a.L) {
+      FSTAMP(6);
+      // 9. image of layer l+2 into IMG[l&1] (everyone is past this layer's reads of it)
+      if (l + 2 < a.L) {
+        float* dst = IMG0 + (l & 1) * WIMG;
 #pragma unroll
         for (int i = 0; i < IMG_PF; ++i) {
           const int e = tid + 256 * i;
-          if (e < WIMG / 4) *(floatx4*)(Ws + 4 * e) = pf[i];
+          if (e < WIMG / 4) *(floatx4*)(dst + 4 * e) = pf[i];
         }
-        __syncthreads();
       }
+      FSTAMP(7);
     }
+#undef FSTAMP
   }
 }
 

@@ -26,7 +26,18 @@ for i in range(6):
     torch.cuda.synchronize()
     if i >= 2:
         runs.append(net.plan_tensor(T, 'ctrace').view(torch.int64).cpu().numpy().reshape(2, L, 16).copy())
-tr = np.median(np.array(runs), axis=0)[1].astype(np.int64)   # backward
+allr = np.median(np.array(runs), axis=0).astype(np.int64)
+fw = allr[0]
+fnames = ['image prefetch issue', 'producer wait', 'halo loads + bar', 'dilated conv + gate',
+          'residual + next own tap', 'drain + bar + publish + z', 'image write']
+fseg = np.diff(fw[:, :8], axis=1)
+fmed = np.median(fseg[1:-1], axis=0)
+ftot = np.median(fw[:, 7] - fw[:, 0])
+print('chain_fwd block %s, per layer (median cycles over layers):' % BLK)
+for n, m in zip(fnames, fmed):
+    print('  %-26s %6d  (%4.1f %%)' % (n, m, 100.0 * m / ftot))
+print('  layer total                %6d  = %.2f us at 2.4 GHz' % (ftot, ftot / 2400.0))
+tr = allr[1]   # backward
 names = ['stage x/dz + bar', 'gate recompute', 'G wait+build', 'dz,dv,DV', 'dx MFMA+OC', 'publish bar',
          'dSIG MFMA', 'bar+dRES', 'bias+slab+bar', 'image+bar']
 seg = np.diff(tr[:, :11], axis=1)          # [L][10]
