@@ -366,28 +366,28 @@ LBWN_DEV void conv_init(const float* bs, const floatx4 (&cv)[8], int h, floatx16
 // acc += Wkᵀ·x over one tap: Wk = the 32 weight-image rows of that tap, xrow = this lane's
 // 32-channel input row (LDS)
 LBWN_DEV void conv_half(const float* xrow, const float* Wk, int pi, int h, floatx16& acc_s, floatx16& acc_g) {
-  floatx4 bx[2];
-  float ws_[2][4], wg_[2][4];
-  auto load = [&](int g, int buf) {
-    bx[buf] = *(const floatx4*)(xrow + 8 * g + 4 * h);
+  // every operand of the 32 MFMAs read first; the sched_barrier stops hipcc from sinking each
+  // weight pair next to its MFMA (it did, with an LDS round trip per MFMA pair)
+  floatx4 bx[4];
+  float ws_[4][4], wg_[4][4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    bx[g] = *(const floatx4*)(xrow + 8 * g + 4 * h);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int k = 8 * g + 4 * h + j;
-      ws_[buf][j] = Wk[k * WS + pi];
-      wg_[buf][j] = Wk[k * WS + 32 + pi];
-    }
-  };
-  load(0, 0);
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int cb = g & 1;
-    if (g + 1 < 4) load(g + 1, cb ^ 1);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      acc_s = mfma32(ws_[cb][j], bx[cb][j], acc_s);
-      acc_g = mfma32(wg_[cb][j], bx[cb][j], acc_g);
+      ws_[g][j] = Wk[k * WS + pi];
+      wg_[g][j] = Wk[k * WS + 32 + pi];
     }
   }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc_s = mfma32(ws_[g][j], bx[g][j], acc_s);
+      acc_g = mfma32(wg_[g][j], bx[g][j], acc_g);
+    }
 }
 
 static_assert(4096 + 768 <= 2 * LP * XS, "RED + bias partials must fit in Xp and Xc");
@@ -516,6 +516,7 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
           *(floatx4*)(nrow + 8 * q + 4 * h) = v;
           if (valid) __builtin_amdgcn_raw_buffer_store_b128(v, rn, ((a.H + t) * 32 + 8 * q + 4 * h) * 4, 0, 16);
         }
+        FSTAMP(8);
         // 7. the next layer's own tap from the row this wave just wrote (wave-local: no barrier)
         //    while the x stores drain; its image IMG[(l+1)&1] landed before this layer's barriers
         wave_lds_fence();

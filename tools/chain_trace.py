@@ -37,6 +37,7 @@ print('chain_fwd block %s, per layer (median cycles over layers):' % BLK)
 for n, m in zip(fnames, fmed):
     print('  %-26s %6d  (%4.1f %%)' % (n, m, 100.0 * m / ftot))
 print('  layer total                %6d  = %.2f us at 2.4 GHz' % (ftot, ftot / 2400.0))
+print('    of which residual + stores %6d, next own tap %6d' % (np.median(fw[1:-2, 8] - fw[1:-2, 4]), np.median(fw[1:-2, 5] - fw[1:-2, 8])))
 tr = allr[1]   # backward
 names = ['stage x/dz + bar', 'gate recompute', 'G wait+build', 'dz,dv,DV', 'dx MFMA+OC', 'publish bar',
          'dSIG MFMA', 'bar+dRES', 'bias+slab+bar', 'image+bar']
