@@ -36,7 +36,7 @@ struct lbwn_plan {
   // layer chain, which keeps the MFMA pipes ~1/3 busy at one wave per SIMD, so they run on
   // a low-priority stream in lean-LDS form (21 KB beside the chain's 131 KB block).
   bool overlap = false;
-  bool dskip_main = false;       // dSKIP after the chain on the main stream at full rate (else aux, lean)
+  bool dskip_main = true;        // dSKIP after the chain on the main stream at full rate (else aux, lean)
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   size_t oSPLIT_AUX = 0;
@@ -214,8 +214,11 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->oOCG = p->chain ? carve(cur, sizeof(float) * (size_t)L * M * 32) : 0;
   const char* ov = getenv("LBWN_OVERLAP");
   p->overlap = p->chain && !(ov && ov[0] == '0');
+  // dSKIP after the chain on the main stream at full rate (default): with the backward chain at
+  // ~850 µs, dPOST2 + dPOST1 alone fill the overlap window, and a lean dSKIP on the aux stream
+  // after it ran at ~70 TF (3.57 vs 3.47 ms per step).  LBWN_DSKIP_MAIN=0: the aux stream.
   const char* dm = getenv("LBWN_DSKIP_MAIN");
-  p->dskip_main = p->overlap && dm && dm[0] == '1';
+  p->dskip_main = p->overlap && !(dm && dm[0] == '0');
   if (p->overlap) {
     p->oSPLIT_AUX = carve(cur, sizeof(float) * (size_t)p->split_floats);
   }

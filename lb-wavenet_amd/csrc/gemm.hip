@@ -85,8 +85,10 @@ LBWN_DEV int xcd_remap(int bid, int nwg) {
 }
 
 // Block tile BMT × BNT, 4 waves as 2 × 2, each wave (BMT/2) × (BNT/2) = MI × NI MFMA tiles.
+// 128×128 tiles: four blocks (16 waves) per CU, i.e. at most 128 VGPRs; every register
+// above that costs a wave per SIMD, and the k-loop needs that occupancy to hide its LDS reads
 template <bool A_KC, bool B_KC, int BK, int BMT, int BNT>
-__global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(lbwn_gemm_args g) {
+__global__ __launch_bounds__(NT, (BMT * BNT > 128 * 128) ? 2 : 4) void gemm_f32_kernel(lbwn_gemm_args g) {
   constexpr int BM = BMT, BN = BNT, MI = BMT / 64, NI = BNT / 64;
   using SA = Stage<A_KC, BM, BK>;
   using SB = Stage<B_KC, BN, BK>;
@@ -148,7 +150,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(lbwn_gemm_args g) {
     __syncthreads();
   }
 
-  // epilogue
+  // epilogue.  A 32×32 tile's mask values are loaded unconditionally at clamped indices before
+  // any is used (a load under a per-row branch is waited for on its own: one memory round trip
+  // per element, from HBM in the training step), then out-of-range rows / columns are skipped.
   const int h = lane >> 5, ci = lane & 31;
   float* C = g.C + (long)blockIdx.z * g.split_stride;
   const bool raw = g.split_stride != 0;
@@ -156,22 +160,28 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(lbwn_gemm_args g) {
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
-      const int col = n0 + wn * (BN / 2) + ni * 32 + ci;
+      const int col = n0 + wn * (BN / 2) + ni * 32 + ci, colc = min(col, g.N - 1);
+      const int rbase = m0 + wm * (BM / 2) + mi * 32;
+      float mv[16];
+      if (!raw && g.mask) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mv[r] = g.mask[(long)min(rbase + acc_row(r, h), g.M - 1) * g.ldm + colc];
+      }
+      const float bv = (!raw && g.bias) ? g.bias[colc] : 0.f;
       if (col >= g.N) continue;
-      const float bv = (!raw && g.bias) ? g.bias[col] : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * (BM / 2) + mi * 32 + acc_row(r, h);
-        if (row >= g.M) continue;
+        const int row = rbase + acc_row(r, h);
         float v = acc[mi][ni][r];
-        const long o = (long)row * g.ldc + col;
         if (!raw) {
           v += bv;
           if (g.relu_out) v = fmaxf(v, 0.f);
-          if (g.mask && !(g.mask[(long)row * g.ldm + col] > 0.f)) v = 0.f;
-          if (g.accumulate) v += C[o];
+          if (g.mask && !(mv[r] > 0.f)) v = 0.f;
         }
-        C[o] = v;
+        if (row < g.M) {
+          if (!raw && g.accumulate) v += C[(long)row * g.ldc + col];
+          C[(long)row * g.ldc + col] = v;
+        }
       }
     }
 }
