@@ -651,7 +651,40 @@ LBWN_DEV void gc_scatter(float* gtab, long ld, const int* ids_b, const float* DV
   }
 }
 
-constexpr int CB_LDS = 2 * LP * XS + WIMG + LP * DS + 2 * LP * XS;  // Xp Xc | IMG | DV | G | OC (131 KB)
+// Xp Xc | IMG | DV | G | OC | XpN XcN (the next layer's rows, DMA-staged, unpadded): 163,712 B
+constexpr int CB_LDS = 2 * LP * XS + WIMG + LP * DS + 2 * LP * XS + 2 * LP * 32;
+static_assert(CB_LDS * 4 + 16 <= 160 * 1024, "chain bwd LDS");
+
+// next-layer rows by LDS-DMA: wave w moves rows [32w, 32w+32) of the dilated-tap and own-row
+// blocks, 8 rows (1 KiB) per global_load_lds_dwordx4; rows past T are clamped here and zeroed
+// by the copy
+LBWN_DEV void dma_rows(float* XpN, float* XcN, const float* xl, int t0, int d, int T, int H, int w, int lane,
+                       int j0, int j1) {
+#pragma unroll
+  for (int j = j0; j < j1; ++j) {
+    const int row = 32 * w + 8 * j + (lane >> 3), c4 = (lane & 7) * 4;
+    const int trow = min(t0 + row, T - 1);
+    __builtin_amdgcn_global_load_lds(xl + (long)(H + trow - d) * 32 + c4,
+                                     (__attribute__((address_space(3))) void*)(XpN + (32 * w + 8 * j) * 32), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(xl + (long)(H + trow) * 32 + c4,
+                                     (__attribute__((address_space(3))) void*)(XcN + (32 * w + 8 * j) * 32), 16, 0, 0);
+  }
+}
+// unpadded staged rows -> padded tile rows (zero past T)
+LBWN_DEV void copy_rows(float* dst, const float* src, int t0, int T, int tid) {
+  floatx4 v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = tid + 256 * i;
+    v[i] = *(const floatx4*)(src + (e >> 3) * 32 + (e & 7) * 4);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = tid + 256 * i;
+    if (t0 + (e >> 3) >= T) v[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    *(floatx4*)(dst + (e >> 3) * XS + (e & 7) * 4) = v[i];
+  }
+}
 
 __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
   __shared__ __attribute__((aligned(16))) float sm[CB_LDS];
@@ -664,6 +697,8 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
   float* DV = Ws + WIMG;
   float* G = DV + LP * DS;
   float* OC = G + LP * XS;
+  float* XpN = OC + LP * XS;    // next layer's rows, DMA-staged during this layer
+  float* XcN = XpN + LP * 32;
   float* ZT = Ws;   // after dx
   float* RED = Xp;  // after dSIG
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -698,9 +733,16 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
       const int d = 1 << (l % a.nbl);
       const int dn = (l + 1 < a.L) ? 1 << ((l + 1) % a.nbl) : 0;
       const float* xl = a.X + (long)l * a.xls + sb;
-      // 0. this layer's inputs (pre-launch data): x_l taps, dZ rows; next image prefetch
-      stage_rows(Xp, xl, t0, -d, a.T, a.H, 32, tid);
-      stage_rows(Xc, xl, t0, 0, a.T, a.H, 32, tid);
+      // 0. this layer's inputs: x_l taps / own rows (the tile's first layer: from HBM; later
+      //    layers: DMA-staged during the previous layer, landed by its publish drain + barrier),
+      //    dZ rows (first used after the gate recompute and G build); next image prefetch
+      if (l == a.L - 1) {
+        stage_rows(Xp, xl, t0, -d, a.T, a.H, 32, tid);
+        stage_rows(Xc, xl, t0, 0, a.T, a.H, 32, tid);
+      } else {
+        copy_rows(Xp, XpN, t0, a.T, tid);
+        copy_rows(Xc, XcN, t0, a.T, tid);
+      }
       floatx16 dz;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -720,11 +762,17 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
       }
       __syncthreads();
       CSTAMP(1);
+      // the next layer's rows into XpN / XcN (everyone has copied them out: the barrier above),
+      // half before each conv half so the DMA issue overlaps in-flight MFMAs
+      const float* xnext = a.X + (long)(l > 0 ? l - 1 : 0) * a.xls + sb;
+      const int dnext = 1 << ((l > 0 ? l - 1 : 0) % a.nbl);
+      if (l > 0) dma_rows(XpN, XcN, xnext, t0, dnext, a.T, a.H, w, lane, 0, 2);
       // 1. recompute the gate (no cross-tile dependency)
       floatx16 acc_s, acc_g;
       conv_init(bs, cv, h, acc_s, acc_g);
       if (has_cond && l > 0) load_cond(a, l - 1, myid, m, valid, h, cv);
       conv_half(Xc + r * XS, Ws + 32 * WS, pi, h, acc_s, acc_g);
+      if (l > 0) dma_rows(XpN, XcN, xnext, t0, dnext, a.T, a.H, w, lane, 2, 4);
       conv_half(Xp + r * XS, Ws, pi, h, acc_s, acc_g);
       floatx16 th, sg;
 #pragma unroll
