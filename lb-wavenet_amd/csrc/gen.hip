@@ -283,55 +283,72 @@ struct GemvK {
   float* out_part;                              // [ceil(K/KSL)][B][N]
   int B, K, N, KSL;
   long long* step_advance;                      // non-null: block (0,0) advances the step counter
+  long long* trace;                             // debug (LBWN_GEN_TRACE): [8] stamps of this launch
 };
 
 __global__ __launch_bounds__(256) void gen_gemv_kernel(GemvK a) {
-  __shared__ __attribute__((aligned(16))) float xs[16][GV_KSL_MAX];
+  // staged inputs per wave: xs[w][i][j] = x[j][k0 + w + 4i], so a wave reads the 16 stream
+  // values of one of its rows with 4 broadcast ds_read_b128 (not 16 ds_read_b32)
+  __shared__ __attribute__((aligned(16))) float xs[4][GV_KSL_MAX / 4][16];
   __shared__ float red[4][16][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int n = blockIdx.x * 64 + lane;
   const int KSL = a.KSL, ks = blockIdx.y, k0 = ks * KSL, k1 = min(a.K, k0 + KSL);
+  const bool first = blockIdx.x == 0 && blockIdx.y == 0, last = blockIdx.x == gridDim.x - 1 && blockIdx.y == gridDim.y - 1;
+  if (a.trace && tid == 0 && first) { a.trace[0] = wall_clock64(); a.trace[2] = clock64(); }
+  if (a.trace && tid == 0 && last) a.trace[6] = wall_clock64();
+  // weights: branch-free (clamped index, then select), so hipcc can count these loads and the
+  // input staging below does not wait for them (behind branches it lost the count and waited
+  // vmcnt(0): the weight fetch and the input fetch became two serial round trips)
   float wr[GV_KSL_MAX / 4];
 #pragma unroll
   for (int i = 0; i < GV_KSL_MAX / 4; ++i) {
     const int k = k0 + w + 4 * i;
-    wr[i] = (4 * i < KSL && k < k1 && n < a.N) ? a.W[(long)k * a.ldw + n] : 0.f;
+    wr[i] = a.W[(long)min(k, a.K - 1) * a.ldw + min(n, a.N - 1)];
+    if (!(4 * i < KSL && k < k1 && n < a.N)) wr[i] = 0.f;
   }
   if (a.step_advance && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0)   // no-return atomic: no wait
     __hip_atomic_fetch_add(a.step_advance, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  auto put = [&](int e, float x) {   // element e = j·KSL + kk of the slice
+    const int j = e / KSL, kk = e % KSL;
+    xs[kk & 3][kk >> 2][j] = x;
+  };
   for (int b0 = 0; b0 < a.B; b0 += 16) {
     const int nbb = min(16, a.B - b0);
     // stage the input slice: every load of this thread issued before the first is consumed
-    // (at most GV_EPT elements per thread; partial sums as in sum_parts, two elements at once)
     constexpr int GV_EPT = 16 * GV_KSL_MAX / 256;
     if (a.in_part) {
+      // the previous GEMV's partials (≤ 32 per element, all issued at once: one memory round
+      // trip) + bias, relu; two elements per pass
       for (int r0 = 0; r0 < GV_EPT; r0 += 2) {
-        float s2[2] = {0.f, 0.f};
-        for (int q0 = 0; q0 < a.in_parts; q0 += 16) {
-          float v[2][16];
+        if (tid + 256 * r0 >= 16 * KSL) break;
+        float s2[2] = {0.f, 0.f}, bb[2];
+        for (int q0 = 0; q0 < a.in_parts; q0 += 32) {
+          float v[2][32];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int e = tid + 256 * (r0 + h), j = min(e / KSL, nbb - 1), k = min(k0 + e % KSL, a.K - 1);
             const float* pp = a.in_part + (long)(b0 + j) * a.K + k;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) v[h][i] = pp[(long)min(q0 + i, a.in_parts - 1) * a.B * a.K];
+            for (int i = 0; i < 32; ++i) v[h][i] = pp[(long)min(q0 + i, a.in_parts - 1) * a.B * a.K];
+            if (q0 == 0) bb[h] = a.in_bias ? a.in_bias[k] : 0.f;
           }
 #pragma unroll
           for (int h = 0; h < 2; ++h)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) s2[h] += (q0 + i < a.in_parts) ? v[h][i] : 0.f;
+            for (int i = 0; i < 32; ++i) s2[h] += (q0 + i < a.in_parts) ? v[h][i] : 0.f;
         }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int e = tid + 256 * (r0 + h);
           if (e >= 16 * KSL) continue;
-          const int j = e / KSL, kk = e % KSL, k = k0 + kk;
+          const int j = e / KSL, k = k0 + e % KSL;
           float v = 0.f;
           if (j < nbb && k < a.K) {
-            v = s2[h] + (a.in_bias ? a.in_bias[k] : 0.f);
+            v = s2[h] + bb[h];
             if (a.relu_in) v = fmaxf(v, 0.f);
           }
-          xs[j][kk] = v;
+          put(e, v);
         }
       }
     } else {
@@ -348,18 +365,24 @@ __global__ __launch_bounds__(256) void gen_gemv_kernel(GemvK a) {
         const int j = e / KSL, kk = e % KSL;
         float x = (j < nbb && k0 + kk < a.K) ? v[r] : 0.f;
         if (a.relu_in) x = fmaxf(x, 0.f);
-        xs[j][kk] = x;
+        put(e, x);
       }
     }
     __syncthreads();
+    if (a.trace && tid == 0 && first && b0 == 0) a.trace[3] = clock64();
     float acc[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = 0.f;
 #pragma unroll
     for (int i = 0; i < GV_KSL_MAX / 4; ++i)
       if (4 * i < KSL) {
+        const floatx4* xr = (const floatx4*)&xs[w][i][0];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) acc[j] = fmaf(xs[j][w + 4 * i], wr[i], acc[j]);
+        for (int q = 0; q < 4; ++q) {
+          const floatx4 x = xr[q];
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) acc[4 * q + jj] = fmaf(x[jj], wr[i], acc[4 * q + jj]);
+        }
       }
 #pragma unroll
     for (int j = 0; j < 16; ++j) red[w][j][lane] = acc[j];
@@ -371,6 +394,8 @@ __global__ __launch_bounds__(256) void gen_gemv_kernel(GemvK a) {
     }
     __syncthreads();
   }
+  if (a.trace && tid == 0 && first) { a.trace[4] = clock64(); a.trace[1] = wall_clock64(); }
+  if (a.trace && tid == 0 && last) a.trace[7] = wall_clock64();
 }
 
 LBWN_DEV uint64_t splitmix(uint64_t seed, uint64_t stream, uint64_t step) {
@@ -539,7 +564,7 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
   p->oGCP = gcarve(cur, 4 * (size_t)p->L * B * 64);
   p->oBSUM = gcarve(cur, 4 * (size_t)p->Cs);
   p->oGIMG = gcarve(cur, 4 * (size_t)p->L * GIMG);
-  p->oTRACE = gcarve(cur, 8 * (size_t)(2 * p->L + 8));
+  p->oTRACE = gcarve(cur, 8 * (size_t)(2 * p->L + 8 + 32));
   p->trace = getenv("LBWN_GEN_TRACE") != nullptr;
   p->total = cur;
   *out = p;
@@ -557,7 +582,7 @@ extern "C" int lbwn_gen_tensor(const lbwn_gen_plan* p, const char* name, size_t*
   else if (!strcmp(name, "logits")) { *off = p->oLOG; *bytes = 4 * B * p->Q; }
   else if (!strcmp(name, "step")) { *off = p->oSTEP; *bytes = 8; }
   else if (!strcmp(name, "status")) { *off = p->oSTEP + 8; *bytes = 4; }   // reserved: 0 (the barrier-synchronised chain has no failure path)
-  else if (!strcmp(name, "trace")) { *off = p->oTRACE; *bytes = 8 * (size_t)(2 * p->L + 8); }
+  else if (!strcmp(name, "trace")) { *off = p->oTRACE; *bytes = 8 * (size_t)(2 * p->L + 8 + 32); }
   else if (!strcmp(name, "rings")) { *off = p->oRING; *bytes = 4 * (size_t)p->n_ring; }
   else if (!strcmp(name, "teacher")) { *off = p->oTEACH; *bytes = 4 * (size_t)std::max<long long>(1, p->n_teacher); }
   else LBWN_REQUIRE(false, "gen_tensor: unknown tensor '%s'", name);
@@ -633,6 +658,10 @@ extern "C" int lbwn_gen_run(lbwn_gen_plan* p, const lbwn_params* P, void* ws, in
   sm.wav = gat<float>(ws, p->oWAV); sm.max_steps = p->max_steps; sm.seed = p->seed;
   const dim3 gsk((sk.N + 63) / 64, p->ks_skip), gp1((p1.N + 63) / 64, (p1.K + 31) / 32), gp2((p2.N + 63) / 64, (p2.K + 31) / 32);
   const size_t sample_lds = 4 * (size_t)p->Q;
+  if (p->trace) {   // GEMV stamps after the wave kernel's: [skip | post1 | post2] × 8
+    long long* tb = gat<long long>(ws, p->oTRACE) + 2 * p->L + 8;
+    sk.trace = tb; p1.trace = tb + 8; p2.trace = tb + 16;
+  }
   for (int i = 0; i < n_steps; ++i) {
     gen_wave_kernel<<<p->B, 512, 0, st>>>(c);
     gen_gemv_kernel<<<gsk, 256, 0, st>>>(sk);

@@ -24,12 +24,14 @@ g.init_buffers(list(range(1, B + 1)) if arch['n_gc_embed'] else None)
 g.step(1000)
 torch.cuda.synchronize()
 L = arch['n_blocks'] * arch['n_block_layers']
-rows = []
+rows, gv = [], []
 for _ in range(5):
     g.step(1)
     torch.cuda.synchronize()
-    tr = g.tensor('trace', torch.int64).cpu().numpy()[:4 + 2 * L]
+    full = g.tensor('trace', torch.int64).cpu().numpy()
+    tr = full[:4 + 2 * L]
     rows.append(np.diff(np.concatenate([tr[:3], tr[4:4 + 2 * L]])))
+    gv.append(full[2 * L + 8:2 * L + 8 + 24].reshape(3, 8).astype(np.int64))
 d = np.median(np.array(rows), axis=0)
 print('cycles: input %d  wait for taps+layer 0 %d  first-conv %d' % (d[0], d[1], d[2]))
 conv, res = d[4::2], d[3::2][:L]
@@ -37,3 +39,8 @@ print('per layer (median over layers): conv+gate %.0f  residual %.0f   total %.0
       (np.median(conv), np.median(res), np.median(conv) + np.median(res)))
 print('layers:', ' '.join('%d/%d' % (c, r) for c, r in zip(d[2::2][:L], d[3::2][:L])))
 print('total kernel cycles (stamps): %d' % (np.sum(d)))
+gm = np.median(np.array(gv), axis=0)
+for name, s in zip(['skip', 'post1', 'post2'], gm):
+    print('gemv %-5s block0 %5.2f us (staged %d cyc, compute+store %d cyc); last block starts +%.2f us, ends +%.2f us'
+          % (name, (s[1] - s[0]) / 100.0, s[3] - s[2], s[4] - s[3], (s[6] - s[0]) / 100.0, (s[7] - s[0]) / 100.0))
+print('gaps: skip->post1 start %.2f us, post1->post2 %.2f us' % ((gm[1][0] - gm[0][0]) / 100.0, (gm[2][0] - gm[1][0]) / 100.0))
