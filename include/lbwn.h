@@ -137,6 +137,13 @@ int lbwn_mulaw_encode(const float* x, int* q, int64_t n, int n_quanta, int tf32,
 /* ops.mu_decode (ops.py:12-20) */
 int lbwn_mulaw_decode(const int* q, float* x, int64_t n, int n_quanta, void* stream);
 
+/* GEMM arithmetic for every lbwn 1x1 product (process-wide; not a reference interface).
+ * mode 1 (default): f32 operands split exactly into three bf16 terms, six cross products on
+ * the bf16 matrix cores, f32 accumulation (f32-class error, tests/test_gpu_parity.py
+ * ::test_gemm_split_accuracy).  mode 0: v_mfma_f32_32x32x2_f32.  Env LBWN_GEMM=f32 sets 0. */
+int lbwn_gemm_set_mode(int mode);
+int lbwn_gemm_get_mode(void);
+
 /* ops.conv1x1 and every 1x1 product (ops.py:41-55): C[M][N] = epi(A·B).
  * a_kcontig: A stored A[m*lda+k] (else A[k*lda+m]); b_kcontig: B stored B[n*ldb+k]
  * (else B[k*ldb+n]).  Epilogue: +bias[n], relu, zero where mask[m*ldm+n] <= 0, += C.

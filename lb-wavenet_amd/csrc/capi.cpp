@@ -57,6 +57,9 @@ int lbwn_gemm_f32(const float* A, int64_t lda, int a_kcontig, const float* B, in
   return lbwn_gemm_launch(g, a_kcontig, b_kcontig, split_k, slab_ws, (hipStream_t)stream);
 }
 
+int lbwn_gemm_set_mode(int mode) { return lbwn_gemm_set_mode_impl(mode); }
+int lbwn_gemm_get_mode(void) { return lbwn_gemm_mode(); }
+
 int lbwn_layer_image_floats_abi(void) { return lbwn_layer_image_floats(); }
 
 int lbwn_layer_forward(const float* x_in, float* x_out, float* z, int64_t ldz, const float* w_sig,

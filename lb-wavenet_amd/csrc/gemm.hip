@@ -8,6 +8,9 @@
 // MFMA k-order is permuted so a k-contiguous operand feeds four v_mfma_f32_32x32x2_f32
 // steps from one ds_read_b128: at step j of an 8-deep group, lane half h uses k = 8g+4h+j.
 #include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
 
 #include "common.h"
 #include "kernels.h"
@@ -207,12 +210,206 @@ __global__ void splitk_reduce_kernel(lbwn_gemm_args g, const float* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// f32 GEMM on the bf16 matrix cores by exact operand splitting.
+// Every f32 x splits EXACTLY into three bf16 terms x = x0 + x1 + x2: x0 = RN(x) keeps 8
+// significant bits, the f32 residual x - x0 is exact and holds ≤ 16 bits, x1 = RN(residual)
+// takes 8 of them and the ≤ 8 left are x2, exactly (normal range; the data here is O(1)).
+// a·b = Σ_{i,j} a_i·b_j; the six terms with i+j ≤ 2 are formed (each bf16 product is exact
+// in f32) and accumulated in f32; the three dropped terms are ≤ 2·2^-27·|a·b|, below the
+// 2^-24 rounding of every f32 accumulate.  So the result is an f32 GEMM (same operands,
+// f32 accumulation, error class of the f32 MFMA chain: tests/test_gpu_parity.py
+// ::test_gemm_split_accuracy) computed with 6 v_mfma_f32_32x32x16_bf16 (6 × 32 cycles) per
+// 32×32×16 block instead of 8 v_mfma_f32_32x32x2_f32 (8 × 64 cycles): 2.67× the MFMA rate.
+//
+// Tile 128×128×32, 4 waves as 2×2 (64×64 each: 2×2 accumulators).  The operands are staged
+// global f32 → registers (next k-step, issued before this step's MFMAs) → split → LDS as
+// three bf16 planes per row: [row][plane][32 k] with a 208-B row (conflict-free b128 fragment
+// reads: rows 52 dwords apart).  An mn-contiguous operand is transposed in registers (each
+// thread loads a 4(k)×4(mn) block), so both layouts give the same k-contiguous image.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef unsigned uintx2 __attribute__((ext_vector_type(2)));
+typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
+
+#ifndef X3_EXP
+#define X3_EXP 0
+#endif
+constexpr int X3_BK = 32;
+constexpr int X3_ROW = 104;               // bf16 per LDS row: 3 planes × 32 + 8 pad (208 B)
+
+LBWN_DEV unsigned pk_bf16(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((floatx2){a, b}, bf16x2));
+}
+LBWN_DEV float bf_lo(unsigned p) { return __uint_as_float(p << 16); }
+LBWN_DEV float bf_hi(unsigned p) { return __uint_as_float(p & 0xffff0000u); }
+
+// split 4 consecutive-k values into the three planes (2 packed dwords each) and store them
+LBWN_DEV void x3_store4(unsigned short* row, int k, floatx4 x, bool relu) {
+  if (relu) { x[0] = fmaxf(x[0], 0.f); x[1] = fmaxf(x[1], 0.f); x[2] = fmaxf(x[2], 0.f); x[3] = fmaxf(x[3], 0.f); }
+  uintx2 h, m, l;
+  h[0] = pk_bf16(x[0], x[1]); h[1] = pk_bf16(x[2], x[3]);
+#if X3_EXP == 1
+  *(uintx2*)(row + k) = h; *(uintx2*)(row + 32 + k) = h; *(uintx2*)(row + 64 + k) = h;
+  return;
+#endif
+  float r0 = x[0] - bf_lo(h[0]), r1 = x[1] - bf_hi(h[0]), r2 = x[2] - bf_lo(h[1]), r3 = x[3] - bf_hi(h[1]);
+  m[0] = pk_bf16(r0, r1); m[1] = pk_bf16(r2, r3);
+  r0 -= bf_lo(m[0]); r1 -= bf_hi(m[0]); r2 -= bf_lo(m[1]); r3 -= bf_hi(m[1]);
+  l[0] = pk_bf16(r0, r1); l[1] = pk_bf16(r2, r3);
+  *(uintx2*)(row + k) = h;
+  *(uintx2*)(row + 32 + k) = m;
+  *(uintx2*)(row + 64 + k) = l;
+}
+
+template <bool KC, int BMN>
+struct X3Stage {
+  // KC: float4 i covers row (tid/8 + 32 i), k = 4·(tid%8).  MN: one 4(k)×4(mn) block per
+  // 128-row operand, k = 4·(tid%8), mn = 4·(tid/8) (+ 128 per extra block for BMN = 256).
+  static constexpr int NV = BMN * X3_BK / (4 * NT);
+  floatx4 v[NV];
+  LBWN_DEV void load(const float* __restrict__ P, long ld, int mn0, int MN, int k0, int K, int tid) {
+    const int kq = tid & 7, c = 4 * kq, gk = k0 + c;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      floatx4 x = {0.f, 0.f, 0.f, 0.f};
+      if (KC) {
+        const int gr = mn0 + (tid >> 3) + 32 * i;
+        if (gr < MN && gk < K) x = *(const floatx4*)(P + (long)gr * ld + gk);
+      } else {
+        const int gr = mn0 + 4 * (tid >> 3) + 128 * (i >> 2), kk = gk + (i & 3);
+        if (kk < K && gr < MN) x = *(const floatx4*)(P + (long)kk * ld + gr);
+      }
+      v[i] = x;
+    }
+  }
+  LBWN_DEV void store(unsigned short* lds, int tid, bool relu) {
+    const int kq = tid & 7, c = 4 * kq;
+    if (KC) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) x3_store4(lds + ((tid >> 3) + 32 * i) * X3_ROW, c, v[i], relu);
+    } else {
+#pragma unroll
+      for (int b = 0; b < NV / 4; ++b)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          floatx4 t = {v[4 * b][j], v[4 * b + 1][j], v[4 * b + 2][j], v[4 * b + 3][j]};
+          x3_store4(lds + (4 * (tid >> 3) + 128 * b + j) * X3_ROW, c, t, relu);
+        }
+    }
+  }
+};
+
+template <bool A_KC, bool B_KC>
+__global__ __launch_bounds__(NT, 2) void gemm_x3_kernel(lbwn_gemm_args g) {
+  constexpr int BM = 128, BN = 128, MI = 2, NI = 2;
+  __shared__ __attribute__((aligned(16))) unsigned short sA[BM * X3_ROW];
+  __shared__ __attribute__((aligned(16))) unsigned short sB[BN * X3_ROW];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  const int kz0 = blockIdx.z * g.k_per_split;
+  const int kz1 = min(g.K, kz0 + g.k_per_split);
+  const int ntiles = (kz1 - kz0 + X3_BK - 1) / X3_BK;
+
+  floatx16 acc[MI][NI];
+#pragma unroll
+  for (int a = 0; a < MI; ++a)
+#pragma unroll
+    for (int b = 0; b < NI; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  X3Stage<A_KC, BM> sa;
+  X3Stage<B_KC, BN> sb;
+  if (ntiles > 0) {
+    sa.load(g.A, g.lda, m0, g.M, kz0, kz1, tid);
+    sb.load(g.B, g.ldb, n0, g.N, kz0, kz1, tid);
+    sa.store(sA, tid, g.relu_a);
+    sb.store(sB, tid, false);
+  }
+  __syncthreads();
+  const int fi = lane & 31, fh = lane >> 5;
+  const unsigned short* fa0 = sA + (wm * 64 + fi) * X3_ROW + 8 * fh;
+  const unsigned short* fb0 = sB + (wn * 64 + fi) * X3_ROW + 8 * fh;
+  for (int kt = 0; kt < ntiles; ++kt) {
+    if (kt + 1 < ntiles) {
+      const int k0 = kz0 + (kt + 1) * X3_BK;
+      sa.load(g.A, g.lda, m0, g.M, k0, kz1, tid);
+      sb.load(g.B, g.ldb, n0, g.N, k0, kz1, tid);
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      bf16x8 fa[MI][3], fb[NI][3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) fa[mi][p] = *(const bf16x8*)(fa0 + mi * 32 * X3_ROW + 32 * p + 16 * c);
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) fb[ni][p] = *(const bf16x8*)(fb0 + ni * 32 * X3_ROW + 32 * p + 16 * c);
+      }
+      // small terms first: a2b0, a1b1, a0b2, a1b0, a0b1, a0b0
+#pragma unroll
+      for (int s = 0; s < (X3_EXP == 2 ? 1 : 6); ++s) {
+        constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][PA[s]], fb[ni][PB[s]], acc[mi][ni], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < ntiles && X3_EXP != 3) {
+      __syncthreads();
+      sa.store(sA, tid, g.relu_a);
+      sb.store(sB, tid, false);
+    }
+    __syncthreads();
+  }
+
+  const int h = lane >> 5, ci = lane & 31;
+  float* C = g.C + (long)blockIdx.z * g.split_stride;
+  const bool raw = g.split_stride != 0;
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int col = n0 + wn * (BN / 2) + ni * 32 + ci, colc = min(col, g.N - 1);
+      const int rbase = m0 + wm * (BM / 2) + mi * 32;
+      float mv[16];
+      if (!raw && g.mask) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mv[r] = g.mask[(long)min(rbase + acc_row(r, h), g.M - 1) * g.ldm + colc];
+      }
+      const float bv = (!raw && g.bias) ? g.bias[colc] : 0.f;
+      if (col >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rbase + acc_row(r, h);
+        float v = acc[mi][ni][r];
+        if (!raw) {
+          v += bv;
+          if (g.relu_out) v = fmaxf(v, 0.f);
+          if (g.mask && !(mv[r] > 0.f)) v = 0.f;
+        }
+        if (row < g.M) {
+          if (!raw && g.accumulate) v += C[(long)row * g.ldc + col];
+          C[(long)row * g.ldc + col] = v;
+        }
+      }
+    }
+}
+
 }  // namespace
 
 namespace {
-template <int BK, int BMT, int BNT>
-int gemm_launch_t(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws, hipStream_t st) {
-  constexpr int BM = BMT, BN = BNT;
+// shape checks and split-K set-up shared by both GEMM forms
+int gemm_setup(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int& split_k, float* slab_ws, int BK,
+               int BM, int BN, lbwn_gemm_args& g, dim3& grid) {
   LBWN_REQUIRE(a.M > 0 && a.N > 0 && a.K > 0, "gemm: empty shape M=%d N=%d K=%d", a.M, a.N, a.K);
   LBWN_REQUIRE(a.K % 4 == 0 || !a_kcontig, "gemm: K %% 4 != 0 with k-contiguous A");
   LBWN_REQUIRE(a.K % 4 == 0 || !b_kcontig, "gemm: K %% 4 != 0 with k-contiguous B");
@@ -223,13 +420,13 @@ int gemm_launch_t(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int spl
   LBWN_REQUIRE((a.a_codes || (((uintptr_t)a.A) & 15) == 0) && (((uintptr_t)a.B) & 15) == 0,
                "gemm: A/B not 16-B aligned");
   if (split_k < 1) split_k = 1;
-  lbwn_gemm_args g = a;
+  g = a;
   int kps = (a.K + split_k - 1) / split_k;
   kps = (kps + BK - 1) / BK * BK;
   split_k = (a.K + kps - 1) / kps;
   g.k_per_split = kps;
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  dim3 grid(tiles, 1, split_k);
+  grid = dim3(tiles, 1, split_k);
   if (split_k > 1) {
     LBWN_REQUIRE(slab_ws != nullptr, "gemm: split-K needs a slab workspace");
     g.C = slab_ws;
@@ -238,11 +435,10 @@ int gemm_launch_t(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int spl
   } else {
     g.split_stride = 0;
   }
-  if (a_kcontig && b_kcontig) gemm_f32_kernel<true, true, BK, BMT, BNT><<<grid, NT, 0, st>>>(g);
-  else if (a_kcontig) gemm_f32_kernel<true, false, BK, BMT, BNT><<<grid, NT, 0, st>>>(g);
-  else if (b_kcontig) gemm_f32_kernel<false, true, BK, BMT, BNT><<<grid, NT, 0, st>>>(g);
-  else gemm_f32_kernel<false, false, BK, BMT, BNT><<<grid, NT, 0, st>>>(g);
-  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int splitk_finish(const lbwn_gemm_args& a, int split_k, const float* slab_ws, hipStream_t st) {
   if (split_k > 1) {
     const long total = (long)a.M * (a.N / 4);
     int blocks = (int)std::min<long>((total + 255) / 256, 4096);
@@ -251,10 +447,57 @@ int gemm_launch_t(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int spl
   }
   return 0;
 }
+
+int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
+                   hipStream_t st) {
+  LBWN_REQUIRE(a.a_codes == nullptr, "gemm (bf16x3 split): one-hot A not supported");
+  lbwn_gemm_args g;
+  dim3 grid;
+  int e = gemm_setup(a, a_kcontig, b_kcontig, split_k, slab_ws, X3_BK, 128, 128, g, grid);
+  if (e) return e;
+  if (a_kcontig && b_kcontig) gemm_x3_kernel<true, true><<<grid, NT, 0, st>>>(g);
+  else if (a_kcontig) gemm_x3_kernel<true, false><<<grid, NT, 0, st>>>(g);
+  else if (b_kcontig) gemm_x3_kernel<false, true><<<grid, NT, 0, st>>>(g);
+  else gemm_x3_kernel<false, false><<<grid, NT, 0, st>>>(g);
+  LBWN_CHECK_LAUNCH();
+  return splitk_finish(a, split_k, slab_ws, st);
+}
+
+template <int BK, int BMT, int BNT>
+int gemm_launch_t(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws, hipStream_t st) {
+  lbwn_gemm_args g;
+  dim3 grid;
+  int e = gemm_setup(a, a_kcontig, b_kcontig, split_k, slab_ws, BK, BMT, BNT, g, grid);
+  if (e) return e;
+  if (a_kcontig && b_kcontig) gemm_f32_kernel<true, true, BK, BMT, BNT><<<grid, NT, 0, st>>>(g);
+  else if (a_kcontig) gemm_f32_kernel<true, false, BK, BMT, BNT><<<grid, NT, 0, st>>>(g);
+  else if (b_kcontig) gemm_f32_kernel<false, true, BK, BMT, BNT><<<grid, NT, 0, st>>>(g);
+  else gemm_f32_kernel<false, false, BK, BMT, BNT><<<grid, NT, 0, st>>>(g);
+  LBWN_CHECK_LAUNCH();
+  return splitk_finish(a, split_k, slab_ws, st);
+}
 }  // namespace
+
+// GEMM arithmetic: 1 = f32 operands split exactly into bf16 terms on the bf16 matrix cores
+// (default), 0 = v_mfma_f32_32x32x2_f32.  LBWN_GEMM=f32 selects the latter at start-up.
+static int g_gemm_mode = -1;
+int lbwn_gemm_mode(void) {
+  if (g_gemm_mode < 0) {
+    const char* env = getenv("LBWN_GEMM");
+    g_gemm_mode = (env && !strcmp(env, "f32")) ? 0 : 1;
+  }
+  return g_gemm_mode;
+}
+int lbwn_gemm_set_mode_impl(int mode) {
+  LBWN_REQUIRE(mode == 0 || mode == 1, "gemm_set_mode: mode must be 0 (f32 MFMA) or 1 (bf16 split)");
+  g_gemm_mode = mode;
+  return 0;
+}
 
 int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                      hipStream_t st) {
+  if (lbwn_gemm_mode() == 1 && a.a_codes == nullptr)
+    return gemm_launch_x3(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
   // tall products (M = B·T positions): 256 × 128 block tiles, each wave 128 × 64
   static const char* env = getenv("LBWN_GEMM_TILE");
   const bool tall = (env && env[0] == '2') && a.M >= 8192 && split_k <= 1;   // measured slower: opt-in
@@ -264,5 +507,7 @@ int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int 
 
 int lbwn_gemm_launch_lean(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                           hipStream_t st) {
+  if (lbwn_gemm_mode() == 1 && a.a_codes == nullptr)
+    return gemm_launch_x3(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
   return gemm_launch_t<8, 128, 128>(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
 }

@@ -18,6 +18,9 @@ struct lbwn_gemm_args {
 };
 int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                      hipStream_t st);
+// 1: bf16-split (default), 0: f32 MFMA (gemm.hip)
+int lbwn_gemm_mode(void);
+int lbwn_gemm_set_mode_impl(int mode);
 // same product with a 21 KB LDS footprint (BK = 8) so it can co-reside with a chain block
 int lbwn_gemm_launch_lean(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                           hipStream_t st);

@@ -61,9 +61,19 @@ def close(a, b, rel, name=''):
 
 # ---- GEMM ------------------------------------------------------------------------------
 
+@pytest.fixture
+def gemm_mode(lib):
+    """Set the GEMM arithmetic for one test (1 = bf16 split, 0 = f32 MFMA), then restore it."""
+    old = lib.lbwn_gemm_get_mode()
+    yield lambda m: _lib.check(lib.lbwn_gemm_set_mode(m))
+    _lib.check(lib.lbwn_gemm_set_mode(old))
+
+
 @pytest.mark.parametrize('akc,bkc', [(1, 0), (1, 1), (0, 0), (0, 1)])
 @pytest.mark.parametrize('split', [1, 3])
-def test_gemm_layouts(lib, akc, bkc, split):
+@pytest.mark.parametrize('mode', [1, 0])
+def test_gemm_layouts(lib, gemm_mode, akc, bkc, split, mode):
+    gemm_mode(mode)
     M, N, K = 300, 136, 200
     g = torch.Generator().manual_seed(1)
     A = torch.randn(M, K, generator=g, dtype=torch.float64)
@@ -85,8 +95,10 @@ def test_gemm_layouts(lib, akc, bkc, split):
     close(Cd.cpu().numpy(), ref.numpy(), 1e-5, 'gemm')
 
 
-def test_gemm_large_skip_shape(lib):
+@pytest.mark.parametrize('mode', [1, 0])
+def test_gemm_large_skip_shape(lib, gemm_mode, mode):
     """The skip GEMM shape (K = 1600, N = 512) against torch fp64."""
+    gemm_mode(mode)
     M, N, K = 1024, 512, 1600
     g = torch.Generator().manual_seed(2)
     A = torch.rand(M, K, generator=g, dtype=torch.float64) * 2 - 1
@@ -97,6 +109,40 @@ def test_gemm_large_skip_shape(lib):
                                  None, 0, 0, 1, None, None))
     torch.cuda.synchronize()
     close(C.cpu().numpy(), (A @ Bm).numpy(), 1e-5, 'gemm_skip')
+
+
+def _gemm_err(lib, A, Bm, akc, bkc, split):
+    M, K = A.shape
+    N = Bm.shape[1]
+    Ad = (A if akc else A.t()).contiguous().float().to(DEV)
+    Bd = (Bm.t() if bkc else Bm).contiguous().float().to(DEV)
+    C = torch.empty(M, N, device=DEV)
+    ws = torch.empty(split * M * N, device=DEV)
+    _lib.check(lib.lbwn_gemm_f32(Ad.data_ptr(), K if akc else M, akc, Bd.data_ptr(), K if bkc else N, bkc,
+                                 C.data_ptr(), N, M, N, K, None, 0, 0, None, 0, 0, split, ws.data_ptr(), None))
+    torch.cuda.synchronize()
+    # reference on the f32-rounded operands: only the GEMM's own arithmetic is measured
+    ref = A.float().double() @ Bm.float().double()
+    scale = torch.abs(A.float().double()) @ torch.abs(Bm.float().double())
+    return float(torch.max(torch.abs(C.cpu().double() - ref) / scale))
+
+
+@pytest.mark.parametrize('shape', [('skip_fwd', 2048, 512, 1600, 1, 0, 1), ('dz', 1024, 1600, 512, 1, 1, 1),
+                                   ('dskip', 1600, 512, 32768, 0, 0, 8)])
+def test_gemm_split_accuracy(lib, gemm_mode, shape):
+    """The bf16-split GEMM is an f32 GEMM: its error against fp64 (relative to Σ|a·b|) is of the
+    f32 MFMA's class.  Operands carry a full 24-bit significand (uniform, random exponents over
+    2^±4) so that a 1- or 2-term split, or a bf16 product, would fail by orders of magnitude."""
+    name, M, N, K, akc, bkc, split = shape
+    g = torch.Generator().manual_seed(5)
+    A = (torch.rand(M, K, generator=g, dtype=torch.float64) * 2 - 1) * 2.0 ** torch.randint(-4, 5, (M, K), generator=g)
+    Bm = (torch.rand(K, N, generator=g, dtype=torch.float64) * 2 - 1) * 2.0 ** torch.randint(-4, 5, (K, N), generator=g)
+    gemm_mode(0)
+    e32 = _gemm_err(lib, A, Bm, akc, bkc, split)
+    gemm_mode(1)
+    ex3 = _gemm_err(lib, A, Bm, akc, bkc, split)
+    print('%s: max |err|/sum|ab|  f32 MFMA %.3g  bf16-split %.3g' % (name, e32, ex3))
+    assert ex3 <= max(2.0 * e32, 1e-7), (name, e32, ex3)
 
 
 # ---- one layer ---------------------------------------------------------------------------

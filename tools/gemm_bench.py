@@ -46,7 +46,12 @@ for name, m, n, k, akc, bkc, split in SHAPES:
 
     def ref():
         torch.matmul(Am, Bm, out=C)
-    t0, t1 = timeit(ours), timeit(ref)
     fl = 2.0 * m * n * k
-    print('%-10s M%6d N%5d K%6d  ours %7.1f us %6.1f TF | torch %7.1f us %6.1f TF' % (
-        name, m, n, k, t0 * 1e6, fl / t0 / 1e12, t1 * 1e6, fl / t1 / 1e12), flush=True)
+    res = []
+    for mode in (0, 1):
+        _lib.check(lib.lbwn_gemm_set_mode(mode))
+        t = timeit(ours)
+        res.append('%s %7.1f us %6.1f TF' % (('f32 ', 'x3  ')[mode], t * 1e6, fl / t / 1e12))
+    t1 = timeit(ref)
+    print('%-10s M%6d N%5d K%6d split %2d | %s | torch %7.1f us %6.1f TF' % (
+        name, m, n, k, split, ' | '.join(res), t1 * 1e6, fl / t1 / 1e12), flush=True)
