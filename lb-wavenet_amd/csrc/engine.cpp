@@ -40,6 +40,11 @@ struct lbwn_plan {
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   size_t oSPLIT_AUX = 0;
+  // Weights pre-split into bf16 planes once per step for the bf16-split GEMMs (gemm.hip):
+  // [W3_SKIP_F] SKIPcat as skip-fwd B, [W3_POST1_F] POST1 as post1-fwd B, [W3_POST2_F] POST2 as
+  // post2-fwd B, [W3_POST2_B] POST2ᵀ as dH1 B, [W3_POST1_B] POST1ᵀ as dS B, [W3_SKIP_B]
+  // SKIPcatᵀ as dZ B.  Offset 0 = not used (K % 32 != 0).
+  size_t oW3[6] = {0, 0, 0, 0, 0, 0};
   ~lbwn_plan() {
     if (aux) (void)hipStreamDestroy(aux);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
@@ -51,6 +56,21 @@ struct lbwn_plan {
 };
 
 namespace {
+enum { W3_SKIP_F, W3_POST1_F, W3_POST2_F, W3_POST2_B, W3_POST1_B, W3_SKIP_B };
+// (rows = N of the product, K, trans, W's row stride) of each pre-split weight
+struct W3Shape { int rows, K, trans, ldw; };
+W3Shape w3_shape(const lbwn_plan* p, int i) {
+  const int ldz = p->L * p->Cd;
+  switch (i) {
+    case W3_SKIP_F: return {p->Cs, ldz, 1, p->Cs};
+    case W3_POST1_F: return {p->Cp, p->Cs, 1, p->Cp};
+    case W3_POST2_F: return {p->Q, p->Cp, 1, p->Q};
+    case W3_POST2_B: return {p->Cp, p->Q, 0, p->Q};
+    case W3_POST1_B: return {p->Cs, p->Cp, 0, p->Cp};
+    default: return {ldz, p->Cs, 0, p->Cs};
+  }
+}
+
 struct Probe {
   lbwn_plan* p;
   hipStream_t st;
@@ -200,7 +220,8 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->oSLAB = carve(cur, sizeof(float) * (size_t)L * std::max(nblk, ntiles) * lbwn_layer_slab_stride());
   p->oSPLIT = carve(cur, sizeof(float) * (size_t)p->split_floats);
   p->oSPLIT2 = carve(cur, sizeof(float) * (size_t)lbwn_pre_grad_ws_floats(p->Q, p->Cr));   // dPRE partials
-  p->oCOLS = carve(cur, sizeof(float) * (size_t)lbwn_colsum_ws_floats((int)M, std::max({p->Cs, p->Cp, p->Q, p->Cr})));
+  // three column sums at once in the backward (dlogits, dH1, dS)
+  p->oCOLS = carve(cur, sizeof(float) * 3 * (size_t)lbwn_colsum_ws_floats((int)M, std::max({p->Cs, p->Cp, p->Q, p->Cr})));
   // [status (16 B) | hand-off flags], zeroed together before every chain launch
   p->oSTATUS = carve(cur, 16 + sizeof(unsigned) * (size_t)B * ((T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS));
   p->oFLAGS = p->oSTATUS + 16;
@@ -242,6 +263,10 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     p->oDLCCAT = p->Lo ? carve(cur, f * (size_t)p->Lo * ncond) : 0;
     for (int i = 0; i < 2; ++i) p->oDLC[i] = p->Lo ? carve(cur, f * (size_t)M * std::max(p->Lo, p->Li)) : 0;
   }
+  for (int i = 0; i < 6; ++i) {
+    const W3Shape w = w3_shape(p, i);
+    if (w.K % 32 == 0) p->oW3[i] = carve(cur, 2 * lbwn_split_planes_elems(w.rows, w.K));
+  }
   p->oHEADP = carve(cur, sizeof(float) * 3 * 2048);
   p->oBSUM = carve(cur, sizeof(float) * (size_t)p->Cs);
   p->oWPK = carve(cur, sizeof(float) * (size_t)L * lbwn_layer_image_floats());
@@ -273,6 +298,12 @@ int lbwn_plan_tensor(const lbwn_plan* p, const char* name, size_t* off, size_t* 
   return 0;
 }
 size_t lbwn_plan_workspace_bytes(const lbwn_plan* p) { return p ? p->total : 0; }
+
+// pre-split planes of weight i when the bf16-split GEMM is active, else null
+static const unsigned short* w3(const lbwn_plan* p, void* ws, int i) {
+  return (p->oW3[i] && lbwn_gemm_mode() == 1) ? reinterpret_cast<const unsigned short*>(static_cast<char*>(ws) + p->oW3[i])
+                                              : nullptr;
+}
 
 static lbwn_gemm_args gemm0() {
   lbwn_gemm_args g;
@@ -454,6 +485,22 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   float* WPK = at<float>(ws, p->oWPK);
   if ((e = lbwn_pack_layers_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b, WPK, L, Cr, Cd, st)))
     return e;
+  // skip/head weights -> bf16 planes for the split GEMMs, forward and backward (once per step)
+  if (lbwn_gemm_mode() == 1) {
+    const float* wsrc[6] = {P->skip, P->post1, P->post2, P->post2, P->post1, P->skip};
+    const float* jw[6];
+    long jld[6];
+    int jr[6], jk[6], jt[6], nj = 0;
+    unsigned short* jo[6];
+    for (int i = 0; i < 6; ++i) {
+      if (!p->oW3[i]) continue;
+      const W3Shape w = w3_shape(p, i);
+      jw[nj] = wsrc[i]; jld[nj] = w.ldw; jr[nj] = w.rows; jk[nj] = w.K; jt[nj] = w.trans;
+      jo[nj] = at<unsigned short>(ws, p->oW3[i]);
+      ++nj;
+    }
+    if (nj && (e = lbwn_split_planes_launch(nj, jw, jld, jr, jk, jt, jo, st))) return e;
+  }
   // one-hot·PRE + PRE_BIAS == row gather (tmodel.py:53-66, :86-102)
   if ((e = lbwn_embed_launch(wav_q, P->pre, P->pre_b, X, B, T, H, Cr, p->Q, st))) return e;
   Cond cd;
@@ -493,6 +540,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     lbwn_gemm_args g = gemm0();
     g.A = Z; g.lda = ldz; g.B = P->skip; g.ldb = p->Cs; g.C = S; g.ldc = p->Cs;
     g.M = (int)M; g.N = p->Cs; g.K = (int)ldz; g.bias = P->skip_b ? bsum : nullptr;
+    g.b3 = w3(p, ws, W3_SKIP_F);
     Probe(p, st, "skip_fwd");
     if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
     Probe::end(p, st, "skip_fwd");
@@ -501,6 +549,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   lbwn_gemm_args g = gemm0();
   g.A = S; g.lda = p->Cs; g.B = P->post1; g.ldb = p->Cp; g.C = R2; g.ldc = p->Cp;
   g.M = (int)M; g.N = p->Cp; g.K = p->Cs; g.bias = P->post1_b; g.relu_a = 1; g.relu_out = 1;
+  g.b3 = w3(p, ws, W3_POST1_F);
   Probe(p, st, "post1_fwd");
   if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
   Probe::end(p, st, "post1_fwd");
@@ -508,6 +557,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   g = gemm0();
   g.A = R2; g.lda = p->Cp; g.B = P->post2; g.ldb = p->Q; g.C = LOG; g.ldc = p->Q;
   g.M = (int)M; g.N = p->Q; g.K = p->Cp; g.bias = P->post2_b;
+  g.b3 = w3(p, ws, W3_POST2_F);
   Probe(p, st, "post2_fwd");
   if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
   Probe::end(p, st, "post2_fwd");
@@ -549,6 +599,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   g = gemm0();
   g.A = LOG; g.lda = Q; g.B = P->post2; g.ldb = Q; g.C = DH; g.ldc = Cp; g.M = (int)M; g.N = Cp; g.K = Q;
   g.mask = R2; g.ldm = Cp;
+  g.b3 = w3(p, ws, W3_POST2_B);
   Probe(p, st, "dh");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
   Probe::end(p, st, "dh");
@@ -556,23 +607,31 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   g = gemm0();
   g.A = DH; g.lda = Cp; g.B = P->post1; g.ldb = Cp; g.C = DS; g.ldc = Cs; g.M = (int)M; g.N = Cs; g.K = Cp;
   g.mask = S; g.ldm = Cs;
+  g.b3 = w3(p, ws, W3_POST1_B);
   Probe(p, st, "ds");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
   Probe::end(p, st, "ds");
   // dZ = dS·SKIPcatᵀ
   g = gemm0();
   g.A = DS; g.lda = Cs; g.B = P->skip; g.ldb = Cs; g.C = DZ; g.ldc = ldz; g.M = (int)M; g.N = (int)ldz; g.K = Cs;
+  g.b3 = w3(p, ws, W3_SKIP_B);
   Probe(p, st, "dz");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
   Probe::end(p, st, "dz");
   // bias gradients (column sums of dlogits, dH1, dS; every layer's SKIP_BIAS gets the same Σ dS):
   // here on the main stream, before the fork (small kernels on the least-priority stream beside a
   // resident chain can wait hundreds of µs for a CU)
-  if (G->post2_b && (e = lbwn_colsum_launch(LOG, Q, (int)M, Q, G->post2_b, 0, COLS, st))) return e;
-  if (G->post1_b && (e = lbwn_colsum_launch(DH, Cp, (int)M, Cp, G->post1_b, 0, COLS, st))) return e;
-  if (G->skip_b) {
-    if ((e = lbwn_colsum_launch(DS, Cs, (int)M, Cs, G->skip_b, 0, COLS, st))) return e;
-    if ((e = lbwn_bcast_rows_launch(G->skip_b, L, Cs, st))) return e;
+  {
+    const float* cx[3];
+    long cld[3];
+    int cn[3], cacc[3] = {0, 0, 0}, nj = 0;
+    float* cout[3];
+    auto job = [&](const float* x, int n, float* o) { cx[nj] = x; cld[nj] = n; cn[nj] = n; cout[nj] = o; ++nj; };
+    if (G->post2_b) job(LOG, Q, G->post2_b);
+    if (G->post1_b) job(DH, Cp, G->post1_b);
+    if (G->skip_b) job(DS, Cs, G->skip_b);
+    if (nj && (e = lbwn_colsum_multi_launch(nj, cx, cld, cn, cout, cacc, (int)M, COLS, st))) return e;
+    if (G->skip_b && (e = lbwn_bcast_rows_launch(G->skip_b, L, Cs, st))) return e;
   }
   // weight gradients of the head and skip GEMMs: beside the layer chain (aux stream) or here
   hipStream_t ws_st = st;

@@ -195,8 +195,19 @@ __global__ void splitk_reduce_kernel(lbwn_gemm_args g, const float* __restrict__
   const long total = (long)g.M * n4;
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const int row = (int)(e / n4), col = (int)(e % n4) * 4;
+    const float* src = slabs + (long)row * g.N + col;
+    const long zs = (long)g.M * g.N;
     floatx4 s = {0.f, 0.f, 0.f, 0.f};
-    for (int z = 0; z < splits; ++z) s += *(const floatx4*)(slabs + (long)z * g.M * g.N + (long)row * g.N + col);
+    // 8 slabs per round, all loads issued before the first add (clamped, not predicated), summed
+    // in slab order (deterministic)
+    for (int z0 = 0; z0 < splits; z0 += 8) {
+      floatx4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = *(const floatx4*)(src + (long)min(z0 + i, splits - 1) * zs);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (z0 + i < splits) s += v[i];
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float v = s[j];
@@ -222,87 +233,136 @@ __global__ void splitk_reduce_kernel(lbwn_gemm_args g, const float* __restrict__
 // ::test_gemm_split_accuracy) computed with 6 v_mfma_f32_32x32x16_bf16 (6 × 32 cycles) per
 // 32×32×16 block instead of 8 v_mfma_f32_32x32x2_f32 (8 × 64 cycles): 2.67× the MFMA rate.
 //
-// Tile 128×128×32, 4 waves as 2×2 (64×64 each: 2×2 accumulators).  The operands are staged
-// global f32 → registers (next k-step, issued before this step's MFMAs) → split → LDS as
-// three bf16 planes per row: [row][plane][32 k] with a 208-B row (conflict-free b128 fragment
-// reads: rows 52 dwords apart).  An mn-contiguous operand is transposed in registers (each
-// thread loads a 4(k)×4(mn) block), so both layouts give the same k-contiguous image.
+// Tile 128×128×32, 4 waves as 2×2 (64×64 each: 2×2 accumulators), two blocks per CU.  The
+// operands are staged global f32 → registers (next k-step, issued before this step's MFMAs)
+// → split → LDS as three bf16 planes per row: [row][plane][32 k] with a 208-B row
+// (conflict-free b128 fragment reads: rows 52 dwords apart).  An mn-contiguous operand is
+// transposed in registers (each thread loads a 4(k)×4(mn) block), so both layouts give the
+// same k-contiguous image.  A weight operand can come pre-split (lbwn_gemm_args::b3, packed
+// once per step by lbwn_split_planes_launch): its staging is a straight 16-B copy.
+// Rows (m or n) past the end are read at a clamped row and never zeroed: they only feed
+// output rows / columns that are discarded.  K past the end (K % 32 != 0) is zeroed.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float floatx2 __attribute__((ext_vector_type(2)));
 typedef unsigned uintx2 __attribute__((ext_vector_type(2)));
 typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
 
-#ifndef X3_EXP
-#define X3_EXP 0
-#endif
 constexpr int X3_BK = 32;
 constexpr int X3_ROW = 104;               // bf16 per LDS row: 3 planes × 32 + 8 pad (208 B)
+constexpr int X3_NT = 256;
 
-LBWN_DEV unsigned pk_bf16(float a, float b) {
-  return __builtin_bit_cast(unsigned, __builtin_convertvector((floatx2){a, b}, bf16x2));
+LBWN_DEV unsigned pk_bf16(floatx2 v) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
 }
-LBWN_DEV float bf_lo(unsigned p) { return __uint_as_float(p << 16); }
-LBWN_DEV float bf_hi(unsigned p) { return __uint_as_float(p & 0xffff0000u); }
+LBWN_DEV floatx2 unpk_bf16(unsigned p) { return (floatx2){__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)}; }
 
-// split 4 consecutive-k values into the three planes (2 packed dwords each) and store them
+// x → (hi, mid, lo) packed pairs, exact (see the header comment)
+LBWN_DEV void split2(floatx2 x, unsigned& h, unsigned& m, unsigned& l) {
+  h = pk_bf16(x);
+  x -= unpk_bf16(h);
+  m = pk_bf16(x);
+  x -= unpk_bf16(m);
+  l = pk_bf16(x);
+}
+
+// split 4 consecutive-k values into the three planes and store them
 LBWN_DEV void x3_store4(unsigned short* row, int k, floatx4 x, bool relu) {
   if (relu) { x[0] = fmaxf(x[0], 0.f); x[1] = fmaxf(x[1], 0.f); x[2] = fmaxf(x[2], 0.f); x[3] = fmaxf(x[3], 0.f); }
-  uintx2 h, m, l;
-  h[0] = pk_bf16(x[0], x[1]); h[1] = pk_bf16(x[2], x[3]);
-#if X3_EXP == 1
-  *(uintx2*)(row + k) = h; *(uintx2*)(row + 32 + k) = h; *(uintx2*)(row + 64 + k) = h;
-  return;
-#endif
-  float r0 = x[0] - bf_lo(h[0]), r1 = x[1] - bf_hi(h[0]), r2 = x[2] - bf_lo(h[1]), r3 = x[3] - bf_hi(h[1]);
-  m[0] = pk_bf16(r0, r1); m[1] = pk_bf16(r2, r3);
-  r0 -= bf_lo(m[0]); r1 -= bf_hi(m[0]); r2 -= bf_lo(m[1]); r3 -= bf_hi(m[1]);
-  l[0] = pk_bf16(r0, r1); l[1] = pk_bf16(r2, r3);
+  unsigned h0, m0, l0, h1, m1, l1;
+  split2((floatx2){x[0], x[1]}, h0, m0, l0);
+  split2((floatx2){x[2], x[3]}, h1, m1, l1);
+  const uintx2 h = {h0, h1}, m = {m0, m1}, l = {l0, l1};
   *(uintx2*)(row + k) = h;
   *(uintx2*)(row + 32 + k) = m;
   *(uintx2*)(row + 64 + k) = l;
 }
 
-template <bool KC, int BMN>
+// One f32 operand's k-step: 128 rows × 32 k, 256 threads.
+// KC (k-contiguous in HBM): float4 i covers row (tid/8 + 32 i), k = 4·(tid%8).
+// MN (mn-contiguous): one 4(k)×4(mn) block per thread at k = 4·(tid%8), mn = 4·(tid/8);
+// lanes with consecutive tid%8 write one row's 64 B and rows 4 apart (≡ 16 banks): conflict-free.
+// Row addresses are fixed per thread (set once); KFULL (K % 32 == 0): no per-step checks.
+template <bool KC, bool KFULL>
 struct X3Stage {
-  // KC: float4 i covers row (tid/8 + 32 i), k = 4·(tid%8).  MN: one 4(k)×4(mn) block per
-  // 128-row operand, k = 4·(tid%8), mn = 4·(tid/8) (+ 128 per extra block for BMN = 256).
-  static constexpr int NV = BMN * X3_BK / (4 * NT);
+  static constexpr int NV = 4;
   floatx4 v[NV];
-  LBWN_DEV void load(const float* __restrict__ P, long ld, int mn0, int MN, int k0, int K, int tid) {
-    const int kq = tid & 7, c = 4 * kq, gk = k0 + c;
+  const float* p[NV];   // KC: row pointers at the split's first k; MN: k-row pointers
+  long step;            // floats per k-step
+  int kq;               // 4·(tid%8): this thread's k offset in the step
+  int kz;               // the split's first k
+  unsigned okm;         // !KFULL: bit i = k in range (zeroed at store time, not at load)
+  LBWN_DEV void init(const float* __restrict__ P, long ld, int mn0, int MN, int kz0, int tid) {
+    kq = 4 * (tid & 7);
+    kz = kz0;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      floatx4 x = {0.f, 0.f, 0.f, 0.f};
-      if (KC) {
-        const int gr = mn0 + (tid >> 3) + 32 * i;
-        if (gr < MN && gk < K) x = *(const floatx4*)(P + (long)gr * ld + gk);
+      if (KC) p[i] = P + (long)min(mn0 + (tid >> 3) + 32 * i, MN - 1) * ld + kz0 + kq;
+      else    p[i] = P + (long)(kz0 + kq + i) * ld + min(mn0 + 4 * (tid >> 3), MN - 4);
+    }
+    step = KC ? X3_BK : X3_BK * ld;
+  }
+  // k-step t of the split ending at kend (kend read only when !KFULL); a clamped index keeps
+  // every load unconditional
+  LBWN_DEV void load(int t, int kend) {
+    okm = 0xf;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      if (KFULL) {
+        v[i] = *(const floatx4*)(p[i] + t * step);
       } else {
-        const int gr = mn0 + 4 * (tid >> 3) + 128 * (i >> 2), kk = gk + (i & 3);
-        if (kk < K && gr < MN) x = *(const floatx4*)(P + (long)kk * ld + gr);
+        const int k = kz + t * X3_BK + kq + (KC ? 0 : i);             // this value's first k
+        const int kc = KC ? min(k, kend - 4) : min(k, kend - 1);
+        const long dk = kc - (kz + kq + (KC ? 0 : i));                 // k offset from p[i]
+        v[i] = *(const floatx4*)(p[i] + (KC ? dk : dk * (step / X3_BK)));
+        if (k >= kend) okm &= ~(1u << i);
       }
-      v[i] = x;
     }
   }
+  LBWN_DEV floatx4 val(int i) const {
+    return (KFULL || ((okm >> i) & 1)) ? v[i] : (floatx4){0.f, 0.f, 0.f, 0.f};
+  }
   LBWN_DEV void store(unsigned short* lds, int tid, bool relu) {
-    const int kq = tid & 7, c = 4 * kq;
     if (KC) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) x3_store4(lds + ((tid >> 3) + 32 * i) * X3_ROW, c, v[i], relu);
+      for (int i = 0; i < NV; ++i) x3_store4(lds + ((tid >> 3) + 32 * i) * X3_ROW, kq, val(i), relu);
     } else {
+      const floatx4 r0 = val(0), r1 = val(1), r2 = val(2), r3 = val(3);
 #pragma unroll
-      for (int b = 0; b < NV / 4; ++b)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          floatx4 t = {v[4 * b][j], v[4 * b + 1][j], v[4 * b + 2][j], v[4 * b + 3][j]};
-          x3_store4(lds + (4 * (tid >> 3) + 128 * b + j) * X3_ROW, c, t, relu);
-        }
+      for (int j = 0; j < 4; ++j) {
+        floatx4 t = {r0[j], r1[j], r2[j], r3[j]};
+        x3_store4(lds + (4 * (tid >> 3) + j) * X3_ROW, kq, t, relu);
+      }
     }
   }
 };
 
-template <bool A_KC, bool B_KC>
-__global__ __launch_bounds__(NT, 2) void gemm_x3_kernel(lbwn_gemm_args g) {
+// Pre-split operand [rows][K/32][3][32] bf16: 128 rows × 12 granules of 16 B per k-step.
+struct X3Pre {
+  static constexpr int NV = 6;
+  uintx4 v[NV];
+  const unsigned short* p[NV];
+  int ldst[NV];
+  LBWN_DEV void init(const unsigned short* __restrict__ P3, int kchunks, int mn0, int MN, int kz0, int tid) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int gi = tid + X3_NT * i, r = gi / 12, part = gi % 12;
+      p[i] = P3 + ((long)min(mn0 + r, MN - 1) * kchunks + kz0 / X3_BK) * (3 * X3_BK) + 8 * part;
+      ldst[i] = r * X3_ROW + 8 * part;
+    }
+  }
+  LBWN_DEV void load(int t) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = *(const uintx4*)(p[i] + t * (3 * X3_BK));
+  }
+  LBWN_DEV void store(unsigned short* lds) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) *(uintx4*)(lds + ldst[i]) = v[i];
+  }
+};
+
+template <bool A_KC, bool B_KC, bool KFULL, bool BPRE>
+__global__ __launch_bounds__(X3_NT, 2) void gemm_x3_kernel(lbwn_gemm_args g) {
   constexpr int BM = 128, BN = 128, MI = 2, NI = 2;
   __shared__ __attribute__((aligned(16))) unsigned short sA[BM * X3_ROW];
   __shared__ __attribute__((aligned(16))) unsigned short sB[BN * X3_ROW];
@@ -324,23 +384,27 @@ __global__ __launch_bounds__(NT, 2) void gemm_x3_kernel(lbwn_gemm_args g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
-  X3Stage<A_KC, BM> sa;
-  X3Stage<B_KC, BN> sb;
+  X3Stage<A_KC, KFULL> sa;
+  X3Stage<B_KC, KFULL> sb;
+  X3Pre sp;
+  sa.init(g.A, g.lda, m0, g.M, kz0, tid);
+  if (BPRE) sp.init(g.b3, g.K / X3_BK, n0, g.N, kz0, tid);
+  else sb.init(g.B, g.ldb, n0, g.N, kz0, tid);
+  const bool relu_a = g.relu_a;
   if (ntiles > 0) {
-    sa.load(g.A, g.lda, m0, g.M, kz0, kz1, tid);
-    sb.load(g.B, g.ldb, n0, g.N, kz0, kz1, tid);
-    sa.store(sA, tid, g.relu_a);
-    sb.store(sB, tid, false);
+    sa.load(0, kz1);
+    if (BPRE) sp.load(0); else sb.load(0, kz1);
+    sa.store(sA, tid, relu_a);
+    if (BPRE) sp.store(sB); else sb.store(sB, tid, false);
   }
   __syncthreads();
   const int fi = lane & 31, fh = lane >> 5;
-  const unsigned short* fa0 = sA + (wm * 64 + fi) * X3_ROW + 8 * fh;
-  const unsigned short* fb0 = sB + (wn * 64 + fi) * X3_ROW + 8 * fh;
+  const int fa_off = (wm * 64 + fi) * X3_ROW + 8 * fh, fb_off = (wn * 64 + fi) * X3_ROW + 8 * fh;
+
   for (int kt = 0; kt < ntiles; ++kt) {
     if (kt + 1 < ntiles) {
-      const int k0 = kz0 + (kt + 1) * X3_BK;
-      sa.load(g.A, g.lda, m0, g.M, k0, kz1, tid);
-      sb.load(g.B, g.ldb, n0, g.N, k0, kz1, tid);
+      sa.load(kt + 1, kz1);
+      if (BPRE) sp.load(kt + 1); else sb.load(kt + 1, kz1);
     }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -348,13 +412,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_x3_kernel(lbwn_gemm_args g) {
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
 #pragma unroll
-        for (int mi = 0; mi < MI; ++mi) fa[mi][p] = *(const bf16x8*)(fa0 + mi * 32 * X3_ROW + 32 * p + 16 * c);
+        for (int mi = 0; mi < MI; ++mi) fa[mi][p] = *(const bf16x8*)(sA + fa_off + mi * 32 * X3_ROW + 32 * p + 16 * c);
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni) fb[ni][p] = *(const bf16x8*)(fb0 + ni * 32 * X3_ROW + 32 * p + 16 * c);
+        for (int ni = 0; ni < NI; ++ni) fb[ni][p] = *(const bf16x8*)(sB + fb_off + ni * 32 * X3_ROW + 32 * p + 16 * c);
       }
       // small terms first: a2b0, a1b1, a0b2, a1b0, a0b1, a0b0
 #pragma unroll
-      for (int s = 0; s < (X3_EXP == 2 ? 1 : 6); ++s) {
+      for (int s = 0; s < 6; ++s) {
         constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi)
@@ -363,14 +427,15 @@ __global__ __launch_bounds__(NT, 2) void gemm_x3_kernel(lbwn_gemm_args g) {
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][PA[s]], fb[ni][PB[s]], acc[mi][ni], 0, 0, 0);
       }
     }
-    if (kt + 1 < ntiles && X3_EXP != 3) {
+    if (kt + 1 < ntiles) {
       __syncthreads();
-      sa.store(sA, tid, g.relu_a);
-      sb.store(sB, tid, false);
+      sa.store(sA, tid, relu_a);
+      if (BPRE) sp.store(sB); else sb.store(sB, tid, false);
     }
     __syncthreads();
   }
 
+  // epilogue: mask and C (accumulate) values loaded unconditionally at clamped indices before use
   const int h = lane >> 5, ci = lane & 31;
   float* C = g.C + (long)blockIdx.z * g.split_stride;
   const bool raw = g.split_stride != 0;
@@ -378,12 +443,16 @@ __global__ __launch_bounds__(NT, 2) void gemm_x3_kernel(lbwn_gemm_args g) {
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
-      const int col = n0 + wn * (BN / 2) + ni * 32 + ci, colc = min(col, g.N - 1);
-      const int rbase = m0 + wm * (BM / 2) + mi * 32;
-      float mv[16];
+      const int col = n0 + wn * 64 + ni * 32 + ci, colc = min(col, g.N - 1);
+      const int rbase = m0 + wm * 64 + mi * 32;
+      float mv[16], cv[16];
       if (!raw && g.mask) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) mv[r] = g.mask[(long)min(rbase + acc_row(r, h), g.M - 1) * g.ldm + colc];
+      }
+      if (!raw && g.accumulate) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cv[r] = C[(long)min(rbase + acc_row(r, h), g.M - 1) * g.ldc + colc];
       }
       const float bv = (!raw && g.bias) ? g.bias[colc] : 0.f;
       if (col >= g.N) continue;
@@ -395,13 +464,45 @@ __global__ __launch_bounds__(NT, 2) void gemm_x3_kernel(lbwn_gemm_args g) {
           v += bv;
           if (g.relu_out) v = fmaxf(v, 0.f);
           if (g.mask && !(mv[r] > 0.f)) v = 0.f;
+          if (g.accumulate) v += cv[r];
         }
-        if (row < g.M) {
-          if (!raw && g.accumulate) v += C[(long)row * g.ldc + col];
-          C[(long)row * g.ldc + col] = v;
-        }
+        if (row < g.M) C[(long)row * g.ldc + col] = v;
       }
     }
+}
+
+// Pre-split planes of weights W (f32, row stride ldw): out[r][kc][plane][32] = split of
+// W[r][32·kc + j] (k-contiguous, trans = 0) or W[32·kc + j][r] (trans = 1); k ≥ K is zero.
+// Up to 6 weights per launch (blockIdx.y = job).
+struct SplitJobs {
+  const float* W[6];
+  long ldw[6];
+  int rows[6], K[6], trans[6];
+  unsigned short* out[6];
+};
+__global__ void split_planes_kernel(SplitJobs jb) {
+  const int jj = blockIdx.y;
+  const float* __restrict__ W = jb.W[jj];
+  const long ldw = jb.ldw[jj];
+  const int rows = jb.rows[jj], K = jb.K[jj], trans = jb.trans[jj];
+  unsigned short* __restrict__ out = jb.out[jj];
+  const int kch = (K + X3_BK - 1) / X3_BK;
+  const long total = (long)rows * kch * (X3_BK / 2);   // pairs
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int j2 = (int)(e % (X3_BK / 2)) * 2;
+    const long rc = e / (X3_BK / 2);
+    const int kc = (int)(rc % kch), r = (int)(rc / kch);
+    const int k = kc * X3_BK + j2;
+    floatx2 x;
+    x[0] = k < K ? (trans ? W[(long)k * ldw + r] : W[(long)r * ldw + k]) : 0.f;
+    x[1] = k + 1 < K ? (trans ? W[(long)(k + 1) * ldw + r] : W[(long)r * ldw + k + 1]) : 0.f;
+    unsigned h, m, l;
+    split2(x, h, m, l);
+    unsigned* o = (unsigned*)(out + rc * (3 * X3_BK) + j2);
+    o[0] = h;
+    o[X3_BK / 2] = m;
+    o[X3_BK] = l;
+  }
 }
 
 }  // namespace
@@ -448,18 +549,33 @@ int splitk_finish(const lbwn_gemm_args& a, int split_k, const float* slab_ws, hi
   return 0;
 }
 
+template <bool KFULL, bool BPRE>
+int gemm_launch_x3_t(const lbwn_gemm_args& g, const dim3& grid, int a_kcontig, int b_kcontig, hipStream_t st) {
+  if (BPRE) {
+    if (a_kcontig) gemm_x3_kernel<true, true, KFULL, true><<<grid, X3_NT, 0, st>>>(g);
+    else gemm_x3_kernel<false, true, KFULL, true><<<grid, X3_NT, 0, st>>>(g);
+  } else if (a_kcontig && b_kcontig) gemm_x3_kernel<true, true, KFULL, false><<<grid, X3_NT, 0, st>>>(g);
+  else if (a_kcontig) gemm_x3_kernel<true, false, KFULL, false><<<grid, X3_NT, 0, st>>>(g);
+  else if (b_kcontig) gemm_x3_kernel<false, true, KFULL, false><<<grid, X3_NT, 0, st>>>(g);
+  else gemm_x3_kernel<false, false, KFULL, false><<<grid, X3_NT, 0, st>>>(g);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
 int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                    hipStream_t st) {
-  LBWN_REQUIRE(a.a_codes == nullptr, "gemm (bf16x3 split): one-hot A not supported");
+  LBWN_REQUIRE(a.a_codes == nullptr, "gemm (bf16 split): one-hot A not supported");
+  LBWN_REQUIRE(a.b3 == nullptr || (a.K % X3_BK == 0 && (((uintptr_t)a.b3) & 15) == 0),
+               "gemm (bf16 split): pre-split B needs K %% 32 == 0 and 16-B alignment");
   lbwn_gemm_args g;
   dim3 grid;
   int e = gemm_setup(a, a_kcontig, b_kcontig, split_k, slab_ws, X3_BK, 128, 128, g, grid);
   if (e) return e;
-  if (a_kcontig && b_kcontig) gemm_x3_kernel<true, true><<<grid, NT, 0, st>>>(g);
-  else if (a_kcontig) gemm_x3_kernel<true, false><<<grid, NT, 0, st>>>(g);
-  else if (b_kcontig) gemm_x3_kernel<false, true><<<grid, NT, 0, st>>>(g);
-  else gemm_x3_kernel<false, false><<<grid, NT, 0, st>>>(g);
-  LBWN_CHECK_LAUNCH();
+  const bool kfull = a.K % X3_BK == 0, pre = a.b3 != nullptr;
+  if (kfull && pre) e = gemm_launch_x3_t<true, true>(g, grid, a_kcontig, b_kcontig, st);
+  else if (kfull) e = gemm_launch_x3_t<true, false>(g, grid, a_kcontig, b_kcontig, st);
+  else e = gemm_launch_x3_t<false, false>(g, grid, a_kcontig, b_kcontig, st);
+  if (e) return e;
   return splitk_finish(a, split_k, slab_ws, st);
 }
 
@@ -496,7 +612,7 @@ int lbwn_gemm_set_mode_impl(int mode) {
 
 int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                      hipStream_t st) {
-  if (lbwn_gemm_mode() == 1 && a.a_codes == nullptr)
+  if (lbwn_gemm_mode() == 1 && a.a_codes == nullptr && a.K >= 4 && a.M >= 4 && a.N >= 4)
     return gemm_launch_x3(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
   // tall products (M = B·T positions): 256 × 128 block tiles, each wave 128 × 64
   static const char* env = getenv("LBWN_GEMM_TILE");
@@ -507,7 +623,26 @@ int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int 
 
 int lbwn_gemm_launch_lean(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                           hipStream_t st) {
-  if (lbwn_gemm_mode() == 1 && a.a_codes == nullptr)
+  if (lbwn_gemm_mode() == 1 && a.a_codes == nullptr && a.K >= 4 && a.M >= 4 && a.N >= 4)
     return gemm_launch_x3(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
   return gemm_launch_t<8, 128, 128>(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
+}
+
+size_t lbwn_split_planes_elems(int rows, int K) { return (size_t)rows * ((K + X3_BK - 1) / X3_BK) * 3 * X3_BK; }
+
+int lbwn_split_planes_launch(int njobs, const float* const* W, const long* ldw, const int* rows, const int* K,
+                             const int* trans, unsigned short* const* out, hipStream_t st) {
+  LBWN_REQUIRE(njobs >= 1 && njobs <= 6, "split_planes: 1..6 jobs");
+  SplitJobs jb;
+  memset(&jb, 0, sizeof(jb));
+  long most = 0;
+  for (int j = 0; j < njobs; ++j) {
+    LBWN_REQUIRE(W[j] && out[j] && rows[j] > 0 && K[j] > 0, "split_planes: bad arguments");
+    jb.W[j] = W[j]; jb.ldw[j] = ldw[j]; jb.rows[j] = rows[j]; jb.K[j] = K[j]; jb.trans[j] = trans[j]; jb.out[j] = out[j];
+    most = std::max(most, (long)rows[j] * ((K[j] + X3_BK - 1) / X3_BK) * (X3_BK / 2));
+  }
+  const int blocks = (int)std::min<long>((most + 255) / 256, 1024);
+  split_planes_kernel<<<dim3(blocks, njobs), 256, 0, st>>>(jb);
+  LBWN_CHECK_LAUNCH();
+  return 0;
 }

@@ -12,12 +12,19 @@ struct lbwn_gemm_args {
   const float* mask;   // mask[m*ldm+n] > 0 keeps the value; nullable
   long ldm;
   int relu_a, relu_out, accumulate;
+  const unsigned short* b3;  // nullable: B pre-split into bf16 planes [N][K/32][3][32] (lbwn_split_planes_launch)
   const int* a_codes;  // m-contiguous A only: A[k][m] = (a_codes[k] == m)  (one-hot, tmodel.py:64-65)
   int k_per_split;     // set by the launcher
   long split_stride;   // set by the launcher
 };
 int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                      hipStream_t st);
+// Pre-split planes of a weight for lbwn_gemm_args::b3: rows = N of the product it feeds,
+// W[r][k] (trans = 0) or W[k][r] (trans = 1), row stride ldw; up to 6 weights per launch.
+// Element count of one output:
+size_t lbwn_split_planes_elems(int rows, int K);
+int lbwn_split_planes_launch(int njobs, const float* const* W, const long* ldw, const int* rows, const int* K,
+                             const int* trans, unsigned short* const* out, hipStream_t st);
 // 1: bf16-split (default), 0: f32 MFMA (gemm.hip)
 int lbwn_gemm_mode(void);
 int lbwn_gemm_set_mode_impl(int mode);
@@ -114,6 +121,9 @@ struct lbwn_head_args {
 int lbwn_head_launch(const lbwn_head_args& a, int* nblocks_out, hipStream_t st);
 int lbwn_stats_reduce_launch(const float* partial, int nparts, float* stats, hipStream_t st);
 
+// several column sums in one launch pair; ws holds Σ_j lbwn_colsum_ws_floats(M, N[j]) floats
+int lbwn_colsum_multi_launch(int njobs, const float* const* X, const long* ldx, const int* N, float* const* out,
+                             const int* accumulate, int M, float* ws, hipStream_t st);
 int lbwn_colsum_launch(const float* X, long ldx, int M, int N, float* out, int accumulate, float* ws,
                        hipStream_t st);
 int lbwn_colsum_ws_floats(int M, int N);

@@ -5,6 +5,10 @@
 //   (ops.py:4-39).
 #include <math.h>
 
+#include <string.h>
+
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -239,9 +243,22 @@ __global__ void stats_reduce_kernel(const float* partial, int nparts, float* sta
 // threads per 64 columns sum the chunk partials.  N % 4 == 0, N <= 1024.
 
 constexpr int CS_ROWS = 64;
-__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ X, long ldx, int M, int N,
-                                                             float* part) {
+// up to 4 column sums of M-row matrices in one launch pair (blockIdx.y = job)
+struct ColsumJobs {
+  const float* X[4];
+  long ldx[4];
+  int N[4];
+  float* out[4];
+  int accumulate[4];
+  float* ws[4];
+};
+__global__ __launch_bounds__(256) void colsum_partial_kernel(ColsumJobs jb, int M) {
   __shared__ floatx4 red[256];
+  const int j = blockIdx.y;
+  const float* X = jb.X[j];
+  const long ldx = jb.ldx[j];
+  const int N = jb.N[j];
+  float* part = jb.ws[j];
   const int ng = N / 4, RL = max(1, 256 / ng);
   const int t = threadIdx.x, g = t % ng, rl = t / ng;
   const int r0 = blockIdx.x * CS_ROWS;
@@ -261,10 +278,12 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __rest
 }
 // 256 threads (4 part lanes × 64 columns): a 1024-thread block needs 16 free wave slots on one
 // CU, which beside a resident layer chain and the aux-stream GEMMs it waited ~430 µs for
-__global__ __launch_bounds__(256) void colsum_final_kernel(const float* part, int nparts, int N, float* out,
-                                                           int accumulate) {
+__global__ __launch_bounds__(256) void colsum_final_kernel(ColsumJobs jb, int nparts) {
   __shared__ float red[256];
+  const int j = blockIdx.y, N = jb.N[j];
+  const float* part = jb.ws[j];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), lane = threadIdx.x >> 6;  // 4 part lanes
+  if (blockIdx.x * 64 >= N) return;   // block-uniform
   float s = 0.f;
   if (c < N) {
 #pragma unroll 8
@@ -274,7 +293,8 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(const float* part, in
   __syncthreads();
   if (threadIdx.x < 64 && c < N) {
     const float tot = ((red[threadIdx.x] + red[64 + threadIdx.x]) + red[128 + threadIdx.x]) + red[192 + threadIdx.x];
-    out[c] = accumulate ? out[c] + tot : tot;
+    float* out = jb.out[j];
+    out[c] = jb.accumulate[j] ? out[c] + tot : tot;
   }
 }
 
@@ -420,14 +440,30 @@ int lbwn_stats_reduce_launch(const float* partial, int nparts, float* stats, hip
 
 int lbwn_colsum_ws_floats(int M, int N) { return ((M + CS_ROWS - 1) / CS_ROWS) * N; }
 
-int lbwn_colsum_launch(const float* X, long ldx, int M, int N, float* out, int accumulate, float* ws,
-                       hipStream_t st) {
-  LBWN_REQUIRE(N % 4 == 0 && N <= 1024 && ldx % 4 == 0, "colsum: N %% 4 / N <= 1024 / ldx %% 4 required");
+int lbwn_colsum_multi_launch(int njobs, const float* const* X, const long* ldx, const int* N, float* const* out,
+                             const int* accumulate, int M, float* ws, hipStream_t st) {
+  LBWN_REQUIRE(njobs >= 1 && njobs <= 4, "colsum: 1..4 jobs");
+  ColsumJobs jb;
+  memset(&jb, 0, sizeof(jb));
   const int np = (M + CS_ROWS - 1) / CS_ROWS;
-  colsum_partial_kernel<<<np, 256, 0, st>>>(X, ldx, M, N, ws);
-  colsum_final_kernel<<<(N + 63) / 64, 256, 0, st>>>(ws, np, N, out, accumulate);
+  int nmax = 0;
+  float* w = ws;
+  for (int j = 0; j < njobs; ++j) {
+    LBWN_REQUIRE(N[j] % 4 == 0 && N[j] <= 1024 && ldx[j] % 4 == 0, "colsum: N %% 4 / N <= 1024 / ldx %% 4 required");
+    jb.X[j] = X[j]; jb.ldx[j] = ldx[j]; jb.N[j] = N[j]; jb.out[j] = out[j]; jb.accumulate[j] = accumulate[j];
+    jb.ws[j] = w;
+    w += (long)np * N[j];
+    nmax = std::max(nmax, N[j]);
+  }
+  colsum_partial_kernel<<<dim3(np, njobs), 256, 0, st>>>(jb, M);
+  colsum_final_kernel<<<dim3((nmax + 63) / 64, njobs), 256, 0, st>>>(jb, np);
   LBWN_CHECK_LAUNCH();
   return 0;
+}
+
+int lbwn_colsum_launch(const float* X, long ldx, int M, int N, float* out, int accumulate, float* ws,
+                       hipStream_t st) {
+  return lbwn_colsum_multi_launch(1, &X, &ldx, &N, &out, &accumulate, M, ws, st);
 }
 
 int lbwn_sum_bias_launch(const float* b, int L, int N, float* out, hipStream_t st) {
