@@ -251,6 +251,9 @@ typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
 constexpr int X3_BK = 32;
 constexpr int X3_ROW = 104;               // bf16 per LDS row: 3 planes × 32 + 8 pad (208 B)
 constexpr int X3_NT = 256;
+#ifndef X3_OCC
+#define X3_OCC 2
+#endif
 
 LBWN_DEV unsigned pk_bf16(floatx2 v) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
@@ -278,42 +281,50 @@ LBWN_DEV void x3_store4(unsigned short* row, int k, floatx4 x, bool relu) {
   *(uintx2*)(row + 64 + k) = l;
 }
 
-// One f32 operand's k-step: 128 rows × 32 k, 256 threads.
-// KC (k-contiguous in HBM): float4 i covers row (tid/8 + 32 i), k = 4·(tid%8).
-// MN (mn-contiguous): one 4(k)×4(mn) block per thread at k = 4·(tid%8), mn = 4·(tid/8);
-// lanes with consecutive tid%8 write one row's 64 B and rows 4 apart (≡ 16 banks): conflict-free.
+// One f32 operand's k-step: ROWS rows × 32 k, NTHR threads.
+// KC (k-contiguous in HBM): float4 i covers row (tid/8 + (NTHR/8)·i), k = 4·(tid%8).
+// MN (mn-contiguous): 4(k)×4(mn) blocks b = tid + NTHR·q at k = 4·(b%8), mn = 4·(b/8); lanes
+// with consecutive b%8 write one row's 64 B and rows 4 apart (≡ 16 banks): conflict-free.  When
+// there are fewer blocks than threads (2·ROWS < NTHR), the extra waves load a duplicate and
+// skip the store (wave-uniform).
 // Row addresses are fixed per thread (set once); KFULL (K % 32 == 0): no per-step checks.
-template <bool KC, bool KFULL>
+template <bool KC, bool KFULL, int ROWS, int NTHR>
 struct X3Stage {
-  static constexpr int NV = 4;
+  static constexpr int NQ = (2 * ROWS + NTHR - 1) / NTHR;          // MN: 4×4 blocks per thread
+  static constexpr int NV = KC ? ROWS * 8 / NTHR : 4 * NQ;
   floatx4 v[NV];
   const float* p[NV];   // KC: row pointers at the split's first k; MN: k-row pointers
   long step;            // floats per k-step
   int kq;               // 4·(tid%8): this thread's k offset in the step
   int kz;               // the split's first k
   unsigned okm;         // !KFULL: bit i = k in range (zeroed at store time, not at load)
+  LBWN_DEV static bool mine(int tid, int q) { return KC || tid + NTHR * q < 2 * ROWS; }
   LBWN_DEV void init(const float* __restrict__ P, long ld, int mn0, int MN, int kz0, int tid) {
     kq = 4 * (tid & 7);
     kz = kz0;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      if (KC) p[i] = P + (long)min(mn0 + (tid >> 3) + 32 * i, MN - 1) * ld + kz0 + kq;
-      else    p[i] = P + (long)(kz0 + kq + i) * ld + min(mn0 + 4 * (tid >> 3), MN - 4);
+      if (KC) {
+        p[i] = P + (long)min(mn0 + (tid >> 3) + (NTHR / 8) * i, MN - 1) * ld + kz0 + kq;
+      } else {
+        const int b = (tid + NTHR * (i >> 2)) % (2 * ROWS);
+        p[i] = P + (long)(kz0 + kq + (i & 3)) * ld + min(mn0 + 4 * (b >> 3), MN - 4);
+      }
     }
     step = KC ? X3_BK : X3_BK * ld;
   }
   // k-step t of the split ending at kend (kend read only when !KFULL); a clamped index keeps
   // every load unconditional
   LBWN_DEV void load(int t, int kend) {
-    okm = 0xf;
+    okm = ~0u;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       if (KFULL) {
         v[i] = *(const floatx4*)(p[i] + t * step);
       } else {
-        const int k = kz + t * X3_BK + kq + (KC ? 0 : i);             // this value's first k
+        const int k = kz + t * X3_BK + kq + (KC ? 0 : (i & 3));       // this value's first k
         const int kc = KC ? min(k, kend - 4) : min(k, kend - 1);
-        const long dk = kc - (kz + kq + (KC ? 0 : i));                 // k offset from p[i]
+        const long dk = kc - (kz + kq + (KC ? 0 : (i & 3)));           // k offset from p[i]
         v[i] = *(const floatx4*)(p[i] + (KC ? dk : dk * (step / X3_BK)));
         if (k >= kend) okm &= ~(1u << i);
       }
@@ -325,28 +336,34 @@ struct X3Stage {
   LBWN_DEV void store(unsigned short* lds, int tid, bool relu) {
     if (KC) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) x3_store4(lds + ((tid >> 3) + 32 * i) * X3_ROW, kq, val(i), relu);
+      for (int i = 0; i < NV; ++i) x3_store4(lds + ((tid >> 3) + (NTHR / 8) * i) * X3_ROW, kq, val(i), relu);
     } else {
-      const floatx4 r0 = val(0), r1 = val(1), r2 = val(2), r3 = val(3);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        floatx4 t = {r0[j], r1[j], r2[j], r3[j]};
-        x3_store4(lds + (4 * (tid >> 3) + j) * X3_ROW, kq, t, relu);
+      for (int q = 0; q < NQ; ++q) {
+        if (!mine(tid, q)) continue;
+        const int b = tid + NTHR * q;
+        const floatx4 r0 = val(4 * q), r1 = val(4 * q + 1), r2 = val(4 * q + 2), r3 = val(4 * q + 3);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          floatx4 t = {r0[j], r1[j], r2[j], r3[j]};
+          x3_store4(lds + (4 * (b >> 3) + j) * X3_ROW, kq, t, relu);
+        }
       }
     }
   }
 };
 
-// Pre-split operand [rows][K/32][3][32] bf16: 128 rows × 12 granules of 16 B per k-step.
+// Pre-split operand [rows][K/32][3][32] bf16: ROWS rows × 12 granules of 16 B per k-step.
+template <int ROWS, int NTHR>
 struct X3Pre {
-  static constexpr int NV = 6;
+  static constexpr int NV = ROWS * 12 / NTHR;
   uintx4 v[NV];
   const unsigned short* p[NV];
   int ldst[NV];
   LBWN_DEV void init(const unsigned short* __restrict__ P3, int kchunks, int mn0, int MN, int kz0, int tid) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      const int gi = tid + X3_NT * i, r = gi / 12, part = gi % 12;
+      const int gi = tid + NTHR * i, r = gi / 12, part = gi % 12;
       p[i] = P3 + ((long)min(mn0 + r, MN - 1) * kchunks + kz0 / X3_BK) * (3 * X3_BK) + 8 * part;
       ldst[i] = r * X3_ROW + 8 * part;
     }
@@ -361,9 +378,10 @@ struct X3Pre {
   }
 };
 
-template <bool A_KC, bool B_KC, bool KFULL, bool BPRE>
-__global__ __launch_bounds__(X3_NT, 2) void gemm_x3_kernel(lbwn_gemm_args g) {
-  constexpr int BM = 128, BN = 128, MI = 2, NI = 2;
+// Block tile (64·WM) × 128, WM × 2 waves of 64 × 64 (2 × 2 accumulators of 32 × 32).
+template <bool A_KC, bool B_KC, bool KFULL, bool BPRE, int WM>
+__global__ __launch_bounds__(128 * WM, WM == 2 ? X3_OCC : 1) void gemm_x3_kernel(lbwn_gemm_args g) {
+  constexpr int NTHR = 128 * WM, BM = 64 * WM, BN = 128, MI = 2, NI = 2;
   __shared__ __attribute__((aligned(16))) unsigned short sA[BM * X3_ROW];
   __shared__ __attribute__((aligned(16))) unsigned short sB[BN * X3_ROW];
 
@@ -384,9 +402,9 @@ __global__ __launch_bounds__(X3_NT, 2) void gemm_x3_kernel(lbwn_gemm_args g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
-  X3Stage<A_KC, KFULL> sa;
-  X3Stage<B_KC, KFULL> sb;
-  X3Pre sp;
+  X3Stage<A_KC, KFULL, BM, NTHR> sa;
+  X3Stage<B_KC, KFULL, BN, NTHR> sb;
+  X3Pre<BN, NTHR> sp;
   sa.init(g.A, g.lda, m0, g.M, kz0, tid);
   if (BPRE) sp.init(g.b3, g.K / X3_BK, n0, g.N, kz0, tid);
   else sb.init(g.B, g.ldb, n0, g.N, kz0, tid);
@@ -549,15 +567,16 @@ int splitk_finish(const lbwn_gemm_args& a, int split_k, const float* slab_ws, hi
   return 0;
 }
 
-template <bool KFULL, bool BPRE>
+template <bool KFULL, bool BPRE, int WM>
 int gemm_launch_x3_t(const lbwn_gemm_args& g, const dim3& grid, int a_kcontig, int b_kcontig, hipStream_t st) {
+  constexpr int NTHR = 128 * WM;
   if (BPRE) {
-    if (a_kcontig) gemm_x3_kernel<true, true, KFULL, true><<<grid, X3_NT, 0, st>>>(g);
-    else gemm_x3_kernel<false, true, KFULL, true><<<grid, X3_NT, 0, st>>>(g);
-  } else if (a_kcontig && b_kcontig) gemm_x3_kernel<true, true, KFULL, false><<<grid, X3_NT, 0, st>>>(g);
-  else if (a_kcontig) gemm_x3_kernel<true, false, KFULL, false><<<grid, X3_NT, 0, st>>>(g);
-  else if (b_kcontig) gemm_x3_kernel<false, true, KFULL, false><<<grid, X3_NT, 0, st>>>(g);
-  else gemm_x3_kernel<false, false, KFULL, false><<<grid, X3_NT, 0, st>>>(g);
+    if (a_kcontig) gemm_x3_kernel<true, true, KFULL, true, WM><<<grid, NTHR, 0, st>>>(g);
+    else gemm_x3_kernel<false, true, KFULL, true, WM><<<grid, NTHR, 0, st>>>(g);
+  } else if (a_kcontig && b_kcontig) gemm_x3_kernel<true, true, KFULL, false, WM><<<grid, NTHR, 0, st>>>(g);
+  else if (a_kcontig) gemm_x3_kernel<true, false, KFULL, false, WM><<<grid, NTHR, 0, st>>>(g);
+  else if (b_kcontig) gemm_x3_kernel<false, true, KFULL, false, WM><<<grid, NTHR, 0, st>>>(g);
+  else gemm_x3_kernel<false, false, KFULL, false, WM><<<grid, NTHR, 0, st>>>(g);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
@@ -567,14 +586,22 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
   LBWN_REQUIRE(a.a_codes == nullptr, "gemm (bf16 split): one-hot A not supported");
   LBWN_REQUIRE(a.b3 == nullptr || (a.K % X3_BK == 0 && (((uintptr_t)a.b3) & 15) == 0),
                "gemm (bf16 split): pre-split B needs K %% 32 == 0 and 16-B alignment");
+  static const char* env = getenv("LBWN_X3_WM");
+  const int wm = (env && env[0] == '4') ? 4 : 2;   // 256-row tiles (8 waves): opt-in
   lbwn_gemm_args g;
   dim3 grid;
-  int e = gemm_setup(a, a_kcontig, b_kcontig, split_k, slab_ws, X3_BK, 128, 128, g, grid);
+  int e = gemm_setup(a, a_kcontig, b_kcontig, split_k, slab_ws, X3_BK, 64 * wm, 128, g, grid);
   if (e) return e;
   const bool kfull = a.K % X3_BK == 0, pre = a.b3 != nullptr;
-  if (kfull && pre) e = gemm_launch_x3_t<true, true>(g, grid, a_kcontig, b_kcontig, st);
-  else if (kfull) e = gemm_launch_x3_t<true, false>(g, grid, a_kcontig, b_kcontig, st);
-  else e = gemm_launch_x3_t<false, false>(g, grid, a_kcontig, b_kcontig, st);
+  if (wm == 4) {
+    if (kfull && pre) e = gemm_launch_x3_t<true, true, 4>(g, grid, a_kcontig, b_kcontig, st);
+    else if (kfull) e = gemm_launch_x3_t<true, false, 4>(g, grid, a_kcontig, b_kcontig, st);
+    else e = gemm_launch_x3_t<false, false, 4>(g, grid, a_kcontig, b_kcontig, st);
+  } else {
+    if (kfull && pre) e = gemm_launch_x3_t<true, true, 2>(g, grid, a_kcontig, b_kcontig, st);
+    else if (kfull) e = gemm_launch_x3_t<true, false, 2>(g, grid, a_kcontig, b_kcontig, st);
+    else e = gemm_launch_x3_t<false, false, 2>(g, grid, a_kcontig, b_kcontig, st);
+  }
   if (e) return e;
   return splitk_finish(a, split_k, slab_ws, st);
 }
