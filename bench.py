@@ -246,6 +246,9 @@ def main():
         'metric': 'audio samples/sec: train fwd+bwd & cached autoregressive gen, 1/2/4/8 GPU',
         'value': value, 'unit': 'audio samples/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': ms, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'gemm_arith': ('f32 operands split exactly into 3 bf16 terms, 6 products on bf16 MFMA, f32 accumulation '
+                       '(error vs fp64 <= the f32 MFMA: tests/test_gpu_parity.py::test_gemm_split_accuracy)'
+                       if net.lib.lbwn_gemm_get_mode() == 1 else 'f32 MFMA (v_mfma_f32_32x32x2_f32)'),
         'data': 'synthetic 16 kHz harmonic tones, mu-law 256, dealt with the reference slicing/mask semantics',
         'config': {'workload': 'train step fwd+xent+bwd+TF1-Adam, par/arch3.json (5x10 layers, res/dil 32, '
                                'skip/post 512, Q 256), B=%d streams x T=%d per GPU' % (B, T),
