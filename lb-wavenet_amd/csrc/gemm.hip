@@ -1,12 +1,14 @@
-// fp32 MFMA GEMM for every 1x1 channel-mixing product of the WaveNet step:
+// GEMMs for every 1x1 channel-mixing product of the WaveNet step:
 //   skip    S  = Zcat·SKIPcat        (tmodel.py:171-184 summed over layers, tmodel.py:316-320)
 //   head    H1 = relu(S)·POST1, logits = relu(H1)·POST2   (tmodel.py:187-215)
 //   and their backward products (weight grads are split-K over the M = B·T positions).
 // C[M][N] = epi( Σ_k A[m][k]·B[k][n] ).  A is stored either k-contiguous (A[m*lda+k]) or
-// m-contiguous (A[k*lda+m]); B either n-contiguous (B[k*ldb+n]) or k-contiguous
-// (B[n*ldb+k]).  The LDS image follows the global layout (no transposing stage), and the
-// MFMA k-order is permuted so a k-contiguous operand feeds four v_mfma_f32_32x32x2_f32
-// steps from one ds_read_b128: at step j of an 8-deep group, lane half h uses k = 8g+4h+j.
+// m-contiguous (A[k*lda+m]); B either n-contiguous (B[k*ldb+n]) or k-contiguous (B[n*ldb+k]).
+// Two arithmetic forms (lbwn_gemm_set_mode): the default gemm_x3_kernel computes the f32
+// products on the bf16 matrix cores by exact operand splitting (below); gemm_f32_kernel uses
+// v_mfma_f32_32x32x2_f32.  In the latter the LDS image follows the global layout (no
+// transposing stage), and the MFMA k-order is permuted so a k-contiguous operand feeds four
+// MFMA steps from one ds_read_b128: at step j of an 8-deep group, lane half h uses k = 8g+4h+j.
 #include <stdlib.h>
 #include <string.h>
 
@@ -251,6 +253,9 @@ typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
 constexpr int X3_BK = 32;
 constexpr int X3_ROW = 104;               // bf16 per LDS row: 3 planes × 32 + 8 pad (208 B)
 constexpr int X3_NT = 256;
+#ifndef X3_EXP
+#define X3_EXP 0   // timing experiments only: 2 = one product per block, 4 = no in-loop global loads
+#endif
 #ifndef X3_OCC
 #define X3_OCC 2
 #endif
@@ -378,6 +383,44 @@ struct X3Pre {
   }
 };
 
+// Epilogue of a wave's 64×64 (2×2 accumulators) at (m0 + 64·wm, n0 + 64·wn): bias, relu, mask,
+// accumulate; mask and C values loaded unconditionally at clamped indices before use.
+LBWN_DEV void x3_epilogue(const lbwn_gemm_args& g, floatx16 (&acc)[2][2], int m0, int n0, int wm, int wn, int lane) {
+  const int h = lane >> 5, ci = lane & 31;
+  float* C = g.C + (long)blockIdx.z * g.split_stride;
+  const bool raw = g.split_stride != 0;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int col = n0 + wn * 64 + ni * 32 + ci, colc = min(col, g.N - 1);
+      const int rbase = m0 + wm * 64 + mi * 32;
+      float mv[16], cv[16];
+      if (!raw && g.mask) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mv[r] = g.mask[(long)min(rbase + acc_row(r, h), g.M - 1) * g.ldm + colc];
+      }
+      if (!raw && g.accumulate) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cv[r] = C[(long)min(rbase + acc_row(r, h), g.M - 1) * g.ldc + colc];
+      }
+      const float bv = (!raw && g.bias) ? g.bias[colc] : 0.f;
+      if (col >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rbase + acc_row(r, h);
+        float v = acc[mi][ni][r];
+        if (!raw) {
+          v += bv;
+          if (g.relu_out) v = fmaxf(v, 0.f);
+          if (g.mask && !(mv[r] > 0.f)) v = 0.f;
+          if (g.accumulate) v += cv[r];
+        }
+        if (row < g.M) C[(long)row * g.ldc + col] = v;
+      }
+    }
+}
+
 // Block tile (64·WM) × 128, WM × 2 waves of 64 × 64 (2 × 2 accumulators of 32 × 32).
 template <bool A_KC, bool B_KC, bool KFULL, bool BPRE, int WM>
 __global__ __launch_bounds__(128 * WM, WM == 2 ? X3_OCC : 1) void gemm_x3_kernel(lbwn_gemm_args g) {
@@ -420,7 +463,7 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? X3_OCC : 1) void gemm_x3_kernel
   const int fa_off = (wm * 64 + fi) * X3_ROW + 8 * fh, fb_off = (wn * 64 + fi) * X3_ROW + 8 * fh;
 
   for (int kt = 0; kt < ntiles; ++kt) {
-    if (kt + 1 < ntiles) {
+    if (kt + 1 < ntiles && X3_EXP != 4) {
       sa.load(kt + 1, kz1);
       if (BPRE) sp.load(kt + 1); else sb.load(kt + 1, kz1);
     }
@@ -436,7 +479,7 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? X3_OCC : 1) void gemm_x3_kernel
       }
       // small terms first: a2b0, a1b1, a0b2, a1b0, a0b1, a0b0
 #pragma unroll
-      for (int s = 0; s < 6; ++s) {
+      for (int s = (X3_EXP == 2 ? 5 : 0); s < 6; ++s) {
         constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi)
@@ -453,40 +496,7 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? X3_OCC : 1) void gemm_x3_kernel
     __syncthreads();
   }
 
-  // epilogue: mask and C (accumulate) values loaded unconditionally at clamped indices before use
-  const int h = lane >> 5, ci = lane & 31;
-  float* C = g.C + (long)blockIdx.z * g.split_stride;
-  const bool raw = g.split_stride != 0;
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      const int col = n0 + wn * 64 + ni * 32 + ci, colc = min(col, g.N - 1);
-      const int rbase = m0 + wm * 64 + mi * 32;
-      float mv[16], cv[16];
-      if (!raw && g.mask) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mv[r] = g.mask[(long)min(rbase + acc_row(r, h), g.M - 1) * g.ldm + colc];
-      }
-      if (!raw && g.accumulate) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) cv[r] = C[(long)min(rbase + acc_row(r, h), g.M - 1) * g.ldc + colc];
-      }
-      const float bv = (!raw && g.bias) ? g.bias[colc] : 0.f;
-      if (col >= g.N) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = rbase + acc_row(r, h);
-        float v = acc[mi][ni][r];
-        if (!raw) {
-          v += bv;
-          if (g.relu_out) v = fmaxf(v, 0.f);
-          if (g.mask && !(mv[r] > 0.f)) v = 0.f;
-          if (g.accumulate) v += cv[r];
-        }
-        if (row < g.M) C[(long)row * g.ldc + col] = v;
-      }
-    }
+  x3_epilogue(g, acc, m0, n0, wm, wn, lane);
 }
 
 // Pre-split planes of weights W (f32, row stride ldw): out[r][kc][plane][32] = split of
