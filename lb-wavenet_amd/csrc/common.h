@@ -6,7 +6,49 @@
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef unsigned uintx2 __attribute__((ext_vector_type(2)));
+typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
+
 #define LBWN_DEV __device__ __forceinline__
+
+// ---- f32 products on the bf16 matrix cores (gemm.hip header) ----------------
+// x = hi + mid + lo exactly, each a bf16 (RN at every step; O(1) data, no subnormal terms).
+LBWN_DEV unsigned pk_bf16(floatx2 v) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
+}
+LBWN_DEV floatx2 unpk_bf16(unsigned p) { return (floatx2){__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)}; }
+LBWN_DEV void split2(floatx2 x, unsigned& h, unsigned& m, unsigned& l) {
+  h = pk_bf16(x);
+  x -= unpk_bf16(h);
+  m = pk_bf16(x);
+  x -= unpk_bf16(m);
+  l = pk_bf16(x);
+}
+// 8 consecutive-k values (a = k 0..3, b = k 4..7) -> the three bf16x8 MFMA fragments
+LBWN_DEV void split8(floatx4 a, floatx4 b, bf16x8 (&f)[3]) {
+  unsigned h0, m0, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
+  split2((floatx2){a[0], a[1]}, h0, m0, l0);
+  split2((floatx2){a[2], a[3]}, h1, m1, l1);
+  split2((floatx2){b[0], b[1]}, h2, m2, l2);
+  split2((floatx2){b[2], b[3]}, h3, m3, l3);
+  f[0] = __builtin_bit_cast(bf16x8, (uintx4){h0, h1, h2, h3});
+  f[1] = __builtin_bit_cast(bf16x8, (uintx4){m0, m1, m2, m3});
+  f[2] = __builtin_bit_cast(bf16x8, (uintx4){l0, l1, l2, l3});
+}
+// acc += A·B over one 16-deep k-step from split fragments: the six products with i + j <= 2,
+// small terms first
+LBWN_DEV floatx16 mfma_x3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+  return acc;
+}
 
 // v_mfma_f32_32x32x2_f32: lane l supplies A[i=l&31][k=l>>5] and B[k=l>>5][j=l&31];
 // D[row=(r&3)+8*(r>>2)+4*(l>>5)][col=l&31] in accumulator register r (cdna_hip_programming §3).

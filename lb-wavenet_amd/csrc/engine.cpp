@@ -21,7 +21,7 @@ struct lbwn_plan {
   long M;
   // workspace carving (byte offsets)
   size_t oX, oZ, oS, oR2, oLOG, oDH, oDS, oDZ, oGA[2], oGC0[2], oSLAB, oSPLIT, oSPLIT2, oCOLS,
-      oHEADP, oBSUM, oWPK, oFLAGS, oSTATUS, oOCG, oCTRACE;
+      oHEADP, oBSUM, oWPK, oWPKX, oFLAGS, oSTATUS, oOCG, oCTRACE;
   int ctrace_blk = -1;            // LBWN_CHAIN_TRACE=<block>: chain cycle stamps (debug)
   size_t oGCTAB, oGCD, oGCPART, oLCACT[8], oCOND, oDVALL, oLCCAT, oDLCCAT, oDLC[2];
   int split_dlc, split_up[8];
@@ -270,6 +270,7 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->oHEADP = carve(cur, sizeof(float) * 3 * 2048);
   p->oBSUM = carve(cur, sizeof(float) * (size_t)p->Cs);
   p->oWPK = carve(cur, sizeof(float) * (size_t)L * lbwn_layer_image_floats());
+  p->oWPKX = carve(cur, 2 * (size_t)L * lbwn_layer_image_x3_elems());
   p->total = cur;
   *out = p;
   return 0;
@@ -485,8 +486,14 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   float* WPK = at<float>(ws, p->oWPK);
   if ((e = lbwn_pack_layers_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b, WPK, L, Cr, Cd, st)))
     return e;
-  // skip/head weights -> bf16 planes for the split GEMMs, forward and backward (once per step)
-  if (lbwn_gemm_mode() == 1) {
+  // skip/head weights -> bf16 planes for the split GEMMs, forward and backward, and the split
+  // per-layer images of the forward chain (once per step)
+  const bool x3 = lbwn_gemm_mode() == 1;
+  if (x3 && p->chain &&
+      (e = lbwn_pack_layers_x3_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b,
+                                      at<unsigned short>(ws, p->oWPKX), L, Cr, Cd, st)))
+    return e;
+  if (x3) {
     const float* wsrc[6] = {P->skip, P->post1, P->post2, P->post2, P->post1, P->skip};
     const float* jw[6];
     long jld[6];
@@ -512,6 +519,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     lbwn_chain_args c;
     memset(&c, 0, sizeof(c));
     c.X = X; c.xls = p->x_layer_stride; c.Z = Z; c.ldz = ldz; c.wpack = WPK; c.ids = ids;
+    c.wpack_x3 = x3 ? at<unsigned short>(ws, p->oWPKX) : nullptr;
     c.gc_tab = cd.gc_tab; c.gc_ld = cd.gc_ld; c.cond = cd.cond; c.ldcond = cd.ldcond;
     c.flags = at<unsigned>(ws, p->oFLAGS); c.status = at<unsigned>(ws, p->oSTATUS);
     if (p->ctrace_blk >= 0) { c.trace = at<long long>(ws, p->oCTRACE); c.trace_blk = p->ctrace_blk; }

@@ -244,11 +244,6 @@ __global__ void splitk_reduce_kernel(lbwn_gemm_args g, const float* __restrict__
 // once per step by lbwn_split_planes_launch): its staging is a straight 16-B copy.
 // Rows (m or n) past the end are read at a clamped row and never zeroed: they only feed
 // output rows / columns that are discarded.  K past the end (K % 32 != 0) is zeroed.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float floatx2 __attribute__((ext_vector_type(2)));
-typedef unsigned uintx2 __attribute__((ext_vector_type(2)));
-typedef unsigned uintx4 __attribute__((ext_vector_type(4)));
 
 constexpr int X3_BK = 32;
 constexpr int X3_ROW = 104;               // bf16 per LDS row: 3 planes × 32 + 8 pad (208 B)
@@ -259,20 +254,6 @@ constexpr int X3_NT = 256;
 #ifndef X3_OCC
 #define X3_OCC 2
 #endif
-
-LBWN_DEV unsigned pk_bf16(floatx2 v) {
-  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
-}
-LBWN_DEV floatx2 unpk_bf16(unsigned p) { return (floatx2){__uint_as_float(p << 16), __uint_as_float(p & 0xffff0000u)}; }
-
-// x → (hi, mid, lo) packed pairs, exact (see the header comment)
-LBWN_DEV void split2(floatx2 x, unsigned& h, unsigned& m, unsigned& l) {
-  h = pk_bf16(x);
-  x -= unpk_bf16(h);
-  m = pk_bf16(x);
-  x -= unpk_bf16(m);
-  l = pk_bf16(x);
-}
 
 // split 4 consecutive-k values into the three planes and store them
 LBWN_DEV void x3_store4(unsigned short* row, int k, floatx4 x, bool relu) {

@@ -67,6 +67,11 @@ constexpr int LBWN_LAYER_POS = 128;   // positions per layer-kernel block
 int lbwn_layer_fwd_launch(const lbwn_layer_args& a, hipStream_t st);
 int lbwn_layer_bwd_launch(const lbwn_layer_args& a, hipStream_t st);
 int lbwn_layer_slab_stride();
+// split weight images for the forward chain's bf16-split products (bf16 elements per layer)
+int lbwn_layer_image_x3_elems();
+int lbwn_pack_layers_x3_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
+                               const float* res, const float* res_b, unsigned short* out, int L, int Cr, int Cd,
+                               hipStream_t st);
 int lbwn_layer_image_floats();
 int lbwn_layer_nblocks(int B, int T);
 int lbwn_layer_bwd_grid(int B, int T);   // = number of slab partials per layer
@@ -79,6 +84,7 @@ struct lbwn_chain_args {
   float* X; long xls;          // x_l buffers of all layers, layer stride in floats
   float* Z; long ldz;
   const float* wpack;
+  const unsigned short* wpack_x3;   // forward: split images (bf16-split conv/residual) or null
   const float* gc_tab; long gc_ld; const int* ids;   // GC table [ncat+1][L·2Cd] or null
   const float* cond; long ldcond;                     // LC term [M][L·2Cd] or null
   float* dv_out; long lddv; float* gc_dtab;           // backward: LC dv export, GC grad table

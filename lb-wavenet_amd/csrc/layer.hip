@@ -84,6 +84,72 @@ __global__ void pack_layers_kernel(const float* sig, const float* gate, const fl
   }
 }
 
+// Split image for the forward chain's bf16-split conv / residual, bf16 units:
+//   WT[o (sig 0..31 | gate 32..63)][tap][plane][in 0..31]  (row XW_ROW = 192 + 8 pad: rows 100
+//     dwords apart, conflict-free b128 fragment reads)
+//   RT[out][plane][kk]  (row XR_ROW = 96 + 8 pad), kk = 16s + 8h + j holds z channel
+//     16s + 8(j>>2) + 4h + (j&3): the k order of a 32x32 accumulator used as the B operand
+//     (registers 8s..8s+7 of lane half h), cdna_hip_programming §3
+//   then bs[64], br[32] as f32.
+constexpr int XW_ROW = 200, XR_ROW = 104;
+constexpr int XB_OFF = 64 * XW_ROW + 32 * XR_ROW;             // bf16 offset of the f32 biases
+constexpr int XIMG_US = XB_OFF + 2 * 96;                       // bf16 elements per layer image
+constexpr int XIMG_F = XIMG_US / 2;                            // = 8160 floats, multiple of 4
+static_assert(XIMG_F % 4 == 0 && XB_OFF % 8 == 0, "x3 image alignment");
+
+__global__ void pack_layers_x3_kernel(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
+                                      const float* res, const float* res_b, unsigned short* out, int Cr, int Cd) {
+  const int l = blockIdx.x;
+  const float* ws = sig + (long)l * 2 * Cr * Cd;
+  const float* wg = gate + (long)l * 2 * Cr * Cd;
+  const float* wr = res + (long)l * Cd * Cr;
+  unsigned short* img = out + (long)l * XIMG_US;
+  // WT: pairs of consecutive input channels
+  for (int e = threadIdx.x; e < 64 * 2 * 16; e += blockDim.x) {
+    const int o = e >> 5, tap = (e >> 4) & 1, in = 2 * (e & 15), oc = o & 31;
+    const float* w = o < 32 ? ws : wg;
+    floatx2 x = {0.f, 0.f};
+    if (oc < Cd) {
+      if (in < Cr) x[0] = w[(tap * Cr + in) * Cd + oc];
+      if (in + 1 < Cr) x[1] = w[(tap * Cr + in + 1) * Cd + oc];
+    }
+    unsigned h, m, lo;
+    split2(x, h, m, lo);
+    unsigned short* row = img + o * XW_ROW + tap * 96 + in;
+    *(unsigned*)(row) = h;
+    *(unsigned*)(row + 32) = m;
+    *(unsigned*)(row + 64) = lo;
+  }
+  // RT: kk pairs (kk, kk+1) hold z channels c, c+1 (same j>>2 group)
+  for (int e = threadIdx.x; e < 32 * 16; e += blockDim.x) {
+    const int o = e >> 4, kk = 2 * (e & 15);
+    const int s2 = kk >> 4, hh = (kk >> 3) & 1, j = kk & 7;
+    const int c = 16 * s2 + 8 * (j >> 2) + 4 * hh + (j & 3);
+    floatx2 x = {0.f, 0.f};
+    if (o < Cr) {
+      if (c < Cd) x[0] = wr[c * Cr + o];
+      if (c + 1 < Cd) x[1] = wr[(c + 1) * Cr + o];
+    }
+    unsigned h, m, lo;
+    split2(x, h, m, lo);
+    unsigned short* row = img + 64 * XW_ROW + o * XR_ROW + kk;
+    *(unsigned*)(row) = h;
+    *(unsigned*)(row + 32) = m;
+    *(unsigned*)(row + 64) = lo;
+  }
+  if (threadIdx.x < 96) {
+    const int i = threadIdx.x;
+    float v = 0.f;
+    if (i < 64) {
+      const float* bb = i < 32 ? sig_b : gate_b;
+      if (bb && (i & 31) < Cd) v = bb[(long)l * Cd + (i & 31)];
+    } else if (res_b && i - 64 < Cr) {
+      v = res_b[(long)l * Cr + (i - 64)];
+    }
+    ((float*)(img + XB_OFF))[i] = v;
+  }
+}
+
 // ---- LDS staging ---------------------------------------------------------------------
 
 // dst[r][0..31] = x row (t0 + r + shift) of the halo buffer xb, zero if t0+r >= T.
@@ -309,6 +375,7 @@ struct ChainFK {
   unsigned* flags; unsigned* status;
   int B, T, H, L, nbl, Cd;
   long long* trace; int trace_blk;   // debug stamps (null in production)
+  const unsigned short* ximg;        // L split images (XIMG_US bf16 each): the bf16-split form
 };
 
 // GC + LC term of layer l for this lane's position, in acc layout: cv[q] = sig channels
@@ -390,9 +457,35 @@ LBWN_DEV void conv_half(const float* xrow, const float* Wk, int pi, int h, float
     }
 }
 
+// conv_half on the bf16 cores: acc += Wkᵀ·x over one tap (2 k-steps of 16 channels, sig and
+// gate), Wt = the split image's WT at this tap (bf16, rows XW_ROW), x split on the fly
+LBWN_DEV void conv_half_x3(const float* xrow, const unsigned short* Wt, int pi, int h, floatx16& acc_s, floatx16& acc_g) {
+  floatx4 xv[4];
+  bf16x8 ws_[2][3], wg_[2][3];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    xv[2 * c] = *(const floatx4*)(xrow + 16 * c + 8 * h);
+    xv[2 * c + 1] = *(const floatx4*)(xrow + 16 * c + 8 * h + 4);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      ws_[c][p] = *(const bf16x8*)(Wt + pi * XW_ROW + 32 * p + 16 * c + 8 * h);
+      wg_[c][p] = *(const bf16x8*)(Wt + (32 + pi) * XW_ROW + 32 * p + 16 * c + 8 * h);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    bf16x8 xb[3];
+    split8(xv[2 * c], xv[2 * c + 1], xb);
+    acc_s = mfma_x3(ws_[c], xb, acc_s);
+    acc_g = mfma_x3(wg_[c], xb, acc_g);
+  }
+}
+
 static_assert(4096 + 768 <= 2 * LP * XS, "RED + bias partials must fit in Xp and Xc");
 constexpr int CF_LDS = 3 * LP * XS + 2 * WIMG;      // Xc[2] | HALO | IMG[2]  (99.8 KB)
 constexpr int IMG_PF = (WIMG / 4 + 255) / 256;      // float4 per thread to prefetch an image
+constexpr int CF_LDS_X3 = 3 * LP * XS + 2 * XIMG_F;  // with split images (120.6 KB)
 
 // Per layer l (weight image IMG[l&1]):
 //   wait for the producer tile's x_l, halo rows (sc1 loads), barrier;
@@ -403,12 +496,21 @@ constexpr int IMG_PF = (WIMG / 4 + 255) / 256;      // float4 per thread to pref
 //   the image of layer l+2 into IMG[l&1] (dead after that barrier; first read after the next
 //   layer's halo barrier).  Double-buffered images are what let the own tap move: one image
 //   forced a barrier between this layer's last read and the next layer's first.
+// X3: the conv and residual products on the bf16 cores from split images (ChainFK::ximg);
+// otherwise v_mfma_f32_32x32x2_f32 from the f32 images.
+template <bool X3>
 __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
-  __shared__ __attribute__((aligned(16))) float sm[CF_LDS];
+  constexpr int IMGF = X3 ? XIMG_F : WIMG;              // floats per layer image
+  constexpr int PF = (IMGF / 4 + 255) / 256;            // float4 per thread to prefetch one
+  __shared__ __attribute__((aligned(16))) float sm[X3 ? CF_LDS_X3 : CF_LDS];
   __shared__ int s_fail;
   float* HALO = sm + 2 * LP * XS;
   float* IMG0 = HALO + LP * XS;
-  auto img = [&](int l) { return IMG0 + (l & 1) * WIMG; };   // [W 64×WS | R 32×XS | bs 64 | br 32]
+  // f32: [W 64×WS | R 32×XS | bs 64 | br 32]; X3: [WT | RT | bs 64 | br 32] (bf16 + f32)
+  auto img = [&](int l) { return IMG0 + (l & 1) * IMGF; };
+  const float* wsrc = X3 ? (const float*)a.ximg : a.wpack;
+  auto bias_of = [&](const float* im) { return X3 ? im + XB_OFF / 2 : im + 64 * WS + 32 * XS; };
+
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int pi = lane & 31, h = lane >> 5;
   const int r = 32 * w + pi;  // this lane's row of the tile
@@ -425,15 +527,17 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
     floatx4 cv[8];
     load_cond(a, 0, myid, m, valid && has_cond, h, cv);
     __syncthreads();  // previous tile's LDS use done
-    stage_image(img(0), a.wpack, tid);
-    if (a.L > 1) stage_image(img(1), a.wpack + WIMG, tid);
+    for (int e = tid; e < IMGF / 4; e += 256) *(floatx4*)(img(0) + 4 * e) = *(const floatx4*)(wsrc + 4 * e);
+    if (a.L > 1)
+      for (int e = tid; e < IMGF / 4; e += 256) *(floatx4*)(img(1) + 4 * e) = *(const floatx4*)(wsrc + IMGF + 4 * e);
     stage_rows(sm, a.X + sb, t0, 0, a.T, a.H, 32, tid);  // x_0 (embed output, pre-launch)
     __syncthreads();
     // layer 0's own tap W1·x_0[t]
     floatx16 acc_s, acc_g;
-    conv_init(img(0) + 64 * WS + 32 * XS, cv, h, acc_s, acc_g);
+    conv_init(bias_of(img(0)), cv, h, acc_s, acc_g);
     if (has_cond && a.L > 1) load_cond(a, 1, myid, m, valid, h, cv);
-    conv_half(sm + r * XS, img(0) + 32 * WS, pi, h, acc_s, acc_g);
+    if (X3) conv_half_x3(sm + r * XS, (const unsigned short*)img(0) + 96, pi, h, acc_s, acc_g);
+    else conv_half(sm + r * XS, img(0) + 32 * WS, pi, h, acc_s, acc_g);
     const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && tile == (int)blockIdx.x;
 #define FSTAMP(i) if (trc) a.trace[16 * l + (i)] = clock64()
     for (int l = 0; l < a.L; ++l) {
@@ -444,13 +548,13 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
       float* xl = a.X + (long)l * a.xls + sb;
       const float* Wl = img(l);
       const float* Rs = Wl + 64 * WS;
-      const float* br = Rs + 32 * XS + 64;
+      const float* br = bias_of(Wl) + 64;
       // 1. prefetch the image of layer l+2 (pre-launch data: plain loads, clamped: no branch)
-      floatx4 pf[IMG_PF];
+      floatx4 pf[PF];
       if (l + 2 < a.L) {
-        const floatx4* src = (const floatx4*)(a.wpack + (long)(l + 2) * WIMG);
+        const floatx4* src = (const floatx4*)(wsrc + (long)(l + 2) * IMGF);
 #pragma unroll
-        for (int i = 0; i < IMG_PF; ++i) pf[i] = src[min(tid + 256 * i, WIMG / 4 - 1)];
+        for (int i = 0; i < PF; ++i) pf[i] = src[min(tid + 256 * i, IMGF / 4 - 1)];
       }
       FSTAMP(1);
       // 2. wait for the producer of the halo rows (x_l is layer l-1's output)
@@ -483,12 +587,22 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
       FSTAMP(3);
       // 4. residual weights read now (they wait behind the conv, not in front of the residual)
       float ra[16];
+      bf16x8 rf[2][3];   // X3: RT fragments of the two 16-channel k-steps
+      if (X3) {
+        const unsigned short* rt = (const unsigned short*)Wl + 64 * XW_ROW + pi * XR_ROW + 8 * h;
 #pragma unroll
-      for (int s2 = 0; s2 < 16; ++s2) ra[s2] = Rs[acc_row(s2, h) * XS + pi];
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) rf[s2][p] = *(const bf16x8*)(rt + 32 * p + 16 * s2);
+      } else {
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) ra[s2] = Rs[acc_row(s2, h) * XS + pi];
+      }
       __builtin_amdgcn_sched_barrier(0);
       // 5. dilated tap W0·x[t-d], gate
       const float* xp = (r >= d) ? cur + (r - d) * XS : HALO + r * XS;
-      conv_half(xp, Wl, pi, h, acc_s, acc_g);
+      if (X3) conv_half_x3(xp, (const unsigned short*)Wl, pi, h, acc_s, acc_g);
+      else conv_half(xp, Wl, pi, h, acc_s, acc_g);
       floatx16 z;
 #pragma unroll
       for (int q = 0; q < 16; ++q) z[q] = tanhf_(acc_s[q]) * sigmoidf_(acc_g[q]);
@@ -504,8 +618,20 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc_r[4 * q + j] = xv[j] + bv[j];
         }
+        if (X3) {
+          // z (acc layout) is the B operand: registers 8s..8s+7 form k-step s (RT holds the
+          // matching permuted channel order)
 #pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) acc_r = mfma32(ra[s2], z[s2], acc_r);
+          for (int s2 = 0; s2 < 2; ++s2) {
+            bf16x8 zb[3];
+            split8(floatx4{z[8 * s2], z[8 * s2 + 1], z[8 * s2 + 2], z[8 * s2 + 3]},
+                   floatx4{z[8 * s2 + 4], z[8 * s2 + 5], z[8 * s2 + 6], z[8 * s2 + 7]}, zb);
+            acc_r = mfma_x3(rf[s2], zb, acc_r);
+          }
+        } else {
+#pragma unroll
+          for (int s2 = 0; s2 < 16; ++s2) acc_r = mfma32(ra[s2], z[s2], acc_r);
+        }
         float* xn = a.X + (long)(l + 1) * a.xls + sb;
         const __amdgpu_buffer_rsrc_t rn =
             __builtin_amdgcn_make_buffer_rsrc(xn, (short)0, (int)((long)(a.H + a.T) * 32 * 4), BUF_DW3);
@@ -521,9 +647,10 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
         //    while the x stores drain; its image IMG[(l+1)&1] landed before this layer's barriers
         wave_lds_fence();
         const float* Wn = img(l + 1);
-        conv_init(Wn + 64 * WS + 32 * XS, cv, h, acc_s, acc_g);
+        conv_init(bias_of(Wn), cv, h, acc_s, acc_g);
         if (has_cond && l + 2 < a.L) load_cond(a, l + 2, myid, m, valid, h, cv);
-        conv_half(nrow, Wn + 32 * WS, pi, h, acc_s, acc_g);
+        if (X3) conv_half_x3(nrow, (const unsigned short*)Wn + 96, pi, h, acc_s, acc_g);
+        else conv_half(nrow, Wn + 32 * WS, pi, h, acc_s, acc_g);
       }
       FSTAMP(5);
       // 8. publish x_{l+1}: every wave drains its sc1 stores, barrier, one lane signals
@@ -534,11 +661,11 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
       FSTAMP(6);
       // 9. image of layer l+2 into IMG[l&1] (everyone is past this layer's reads of it)
       if (l + 2 < a.L) {
-        float* dst = IMG0 + (l & 1) * WIMG;
+        float* dst = IMG0 + (l & 1) * IMGF;
 #pragma unroll
-        for (int i = 0; i < IMG_PF; ++i) {
+        for (int i = 0; i < PF; ++i) {
           const int e = tid + 256 * i;
-          if (e < WIMG / 4) *(floatx4*)(dst + 4 * e) = pf[i];
+          if (e < IMGF / 4) *(floatx4*)(dst + 4 * e) = pf[i];
         }
       }
       FSTAMP(7);
@@ -1293,6 +1420,16 @@ BwdK to_bwd(const lbwn_layer_args& a) {
 
 int lbwn_layer_slab_stride() { return SLAB; }
 int lbwn_layer_image_floats() { return WIMG; }
+int lbwn_layer_image_x3_elems() { return XIMG_US; }
+
+int lbwn_pack_layers_x3_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
+                               const float* res, const float* res_b, unsigned short* out, int L, int Cr, int Cd,
+                               hipStream_t st) {
+  LBWN_REQUIRE(Cr <= 32 && Cd <= 32 && (((uintptr_t)out) & 15) == 0, "pack_layers_x3: bad arguments");
+  pack_layers_x3_kernel<<<L, 256, 0, st>>>(sig, gate, sig_b, gate_b, res, res_b, out, Cr, Cd);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
 int lbwn_layer_nblocks(int B, int T) { return B * ((T + LP - 1) / LP); }
 int lbwn_layer_bwd_grid(int B, int T) { return std::min(lbwn_layer_nblocks(B, T), 256); }
 
@@ -1350,10 +1487,13 @@ int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   k.flags = c.flags; k.status = c.status;
   k.B = c.B; k.T = c.T; k.H = c.H; k.L = c.L; k.nbl = c.nbl; k.Cd = c.Cd;
   k.trace = c.trace; k.trace_blk = c.trace_blk;
+  k.ximg = c.wpack_x3;
+  LBWN_REQUIRE(!c.wpack_x3 || (((uintptr_t)c.wpack_x3) & 15) == 0, "chain fwd: split images not 16-B aligned");
   const int tps = (c.T + LP - 1) / LP;
   LBWN_REQUIRE((unsigned*)c.status + 4 == c.flags, "chain: status word must head the flag block");
   LBWN_HIP(hipMemsetAsync(c.status, 0, (16 + (size_t)c.B * tps * 4 + 15) / 16 * 16, st));
-  chain_fwd_kernel<<<c.grid, 256, 0, st>>>(k);
+  if (c.wpack_x3) chain_fwd_kernel<true><<<c.grid, 256, 0, st>>>(k);
+  else chain_fwd_kernel<false><<<c.grid, 256, 0, st>>>(k);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
