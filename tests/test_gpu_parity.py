@@ -220,8 +220,12 @@ def _run_oracle(arch, net, q, ids):
     return P, S, lg, cache, new_save, st, dlog
 
 
-@pytest.mark.parametrize('which,B,T', [('small', 2, 256), ('small', 3, 200), ('arch3', 2, 512)])
-def test_plan_forward_backward(which, B, T):
+@pytest.mark.parametrize('which,B,T,mode', [('small', 2, 256, 1), ('small', 3, 200, 1), ('arch3', 2, 512, 1),
+                                            ('arch3', 2, 512, 0)])
+def test_plan_forward_backward(lib, gemm_mode, which, B, T, mode):
+    """mode 1: GEMMs and the forward chain's conv/residual on the bf16 cores by exact splitting;
+    mode 0: every product on the f32 MFMA.  Same bars for both."""
+    gemm_mode(mode)
     arch = arch3() if which == 'arch3' else small_arch()
     net = make_net(arch, B)
     q, ids = rand_batch(arch, B, T)
