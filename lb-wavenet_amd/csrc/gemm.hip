@@ -403,11 +403,16 @@ LBWN_DEV void x3_epilogue(const lbwn_gemm_args& g, floatx16 (&acc)[2][2], int m0
 }
 
 // Block tile (64·WM) × 128, WM × 2 waves of 64 × 64 (2 × 2 accumulators of 32 × 32).
-template <bool A_KC, bool B_KC, bool KFULL, bool BPRE, int WM>
-__global__ __launch_bounds__(128 * WM, WM == 2 ? X3_OCC : 1) void gemm_x3_kernel(lbwn_gemm_args g) {
+// STAGES = 2: two LDS slots, one barrier per k-step; the next k-step's registers are split
+// into the other slot between this step's two MFMA chunks, and the loads of the step after it
+// are issued right behind (one k-step of load lead).
+template <bool A_KC, bool B_KC, bool KFULL, bool BPRE, int WM, int STAGES>
+__global__ __launch_bounds__(128 * WM, (WM == 2 && STAGES == 1) ? X3_OCC : 1) void gemm_x3_kernel(lbwn_gemm_args g) {
   constexpr int NTHR = 128 * WM, BM = 64 * WM, BN = 128, MI = 2, NI = 2;
-  __shared__ __attribute__((aligned(16))) unsigned short sA[BM * X3_ROW];
-  __shared__ __attribute__((aligned(16))) unsigned short sB[BN * X3_ROW];
+  constexpr int SLOT = (BM + BN) * X3_ROW;
+  __shared__ __attribute__((aligned(16))) unsigned short smem[STAGES * SLOT];
+  unsigned short* sA = smem;
+  unsigned short* sB = smem + BM * X3_ROW;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -443,38 +448,59 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? X3_OCC : 1) void gemm_x3_kernel
   const int fi = lane & 31, fh = lane >> 5;
   const int fa_off = (wm * 64 + fi) * X3_ROW + 8 * fh, fb_off = (wn * 64 + fi) * X3_ROW + 8 * fh;
 
-  for (int kt = 0; kt < ntiles; ++kt) {
-    if (kt + 1 < ntiles && X3_EXP != 4) {
-      sa.load(kt + 1, kz1);
-      if (BPRE) sp.load(kt + 1); else sb.load(kt + 1, kz1);
+  // one 16-deep chunk c of the k-step held in slot `base`: 12 fragment reads, 24 MFMAs
+  auto chunk = [&](const unsigned short* base, int c) {
+    bf16x8 fa[MI][3], fb[NI][3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) fa[mi][p] = *(const bf16x8*)(base + fa_off + mi * 32 * X3_ROW + 32 * p + 16 * c);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+        fb[ni][p] = *(const bf16x8*)(base + BM * X3_ROW + fb_off + ni * 32 * X3_ROW + 32 * p + 16 * c);
     }
+    // small terms first: a2b0, a1b1, a0b2, a1b0, a0b1, a0b0
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      bf16x8 fa[MI][3], fb[NI][3];
+    for (int q = (X3_EXP == 2 ? 5 : 0); q < 6; ++q) {
+      constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-        for (int mi = 0; mi < MI; ++mi) fa[mi][p] = *(const bf16x8*)(sA + fa_off + mi * 32 * X3_ROW + 32 * p + 16 * c);
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) fb[ni][p] = *(const bf16x8*)(sB + fb_off + ni * 32 * X3_ROW + 32 * p + 16 * c);
-      }
-      // small terms first: a2b0, a1b1, a0b2, a1b0, a0b1, a0b0
-#pragma unroll
-      for (int s = (X3_EXP == 2 ? 5 : 0); s < 6; ++s) {
-        constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < NI; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][PA[s]], fb[ni][PB[s]], acc[mi][ni], 0, 0, 0);
-      }
+        for (int ni = 0; ni < NI; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][PA[q]], fb[ni][PB[q]], acc[mi][ni], 0, 0, 0);
     }
-    if (kt + 1 < ntiles) {
+  };
+  auto stage_store = [&](unsigned short* base) {
+    sa.store(base, tid, relu_a);
+    if (BPRE) sp.store(base + BM * X3_ROW); else sb.store(base + BM * X3_ROW, tid, false);
+  };
+  auto stage_load = [&](int k) {
+    sa.load(k, kz1);
+    if (BPRE) sp.load(k); else sb.load(k, kz1);
+  };
+
+  if (STAGES == 1) {
+    for (int kt = 0; kt < ntiles; ++kt) {
+      if (kt + 1 < ntiles && X3_EXP != 4) stage_load(kt + 1);
+      chunk(smem, 0);
+      chunk(smem, 1);
+      if (kt + 1 < ntiles) {
+        __syncthreads();
+        stage_store(smem);
+      }
       __syncthreads();
-      sa.store(sA, tid, relu_a);
-      if (BPRE) sp.store(sB); else sb.store(sB, tid, false);
     }
-    __syncthreads();
+  } else {
+    // the prologue stored k-step 0 into slot 0; the registers now take k-step 1
+    if (ntiles > 1) stage_load(1);
+    for (int kt = 0; kt < ntiles; ++kt) {
+      const unsigned short* cur = smem + (kt & 1) * SLOT;
+      chunk(cur, 0);
+      if (kt + 1 < ntiles) stage_store(smem + ((kt + 1) & 1) * SLOT);
+      if (kt + 2 < ntiles) stage_load(kt + 2);
+      chunk(cur, 1);
+      __syncthreads();
+    }
   }
 
   x3_epilogue(g, acc, m0, n0, wm, wn, lane);
@@ -560,14 +586,14 @@ int splitk_finish(const lbwn_gemm_args& a, int split_k, const float* slab_ws, hi
 
 template <bool KFULL, bool BPRE, int WM>
 int gemm_launch_x3_t(const lbwn_gemm_args& g, const dim3& grid, int a_kcontig, int b_kcontig, hipStream_t st) {
-  constexpr int NTHR = 128 * WM;
+  constexpr int NTHR = 128 * WM, S = WM == 4 ? 2 : 1;
   if (BPRE) {
-    if (a_kcontig) gemm_x3_kernel<true, true, KFULL, true, WM><<<grid, NTHR, 0, st>>>(g);
-    else gemm_x3_kernel<false, true, KFULL, true, WM><<<grid, NTHR, 0, st>>>(g);
-  } else if (a_kcontig && b_kcontig) gemm_x3_kernel<true, true, KFULL, false, WM><<<grid, NTHR, 0, st>>>(g);
-  else if (a_kcontig) gemm_x3_kernel<true, false, KFULL, false, WM><<<grid, NTHR, 0, st>>>(g);
-  else if (b_kcontig) gemm_x3_kernel<false, true, KFULL, false, WM><<<grid, NTHR, 0, st>>>(g);
-  else gemm_x3_kernel<false, false, KFULL, false, WM><<<grid, NTHR, 0, st>>>(g);
+    if (a_kcontig) gemm_x3_kernel<true, true, KFULL, true, WM, S><<<grid, NTHR, 0, st>>>(g);
+    else gemm_x3_kernel<false, true, KFULL, true, WM, S><<<grid, NTHR, 0, st>>>(g);
+  } else if (a_kcontig && b_kcontig) gemm_x3_kernel<true, true, KFULL, false, WM, S><<<grid, NTHR, 0, st>>>(g);
+  else if (a_kcontig) gemm_x3_kernel<true, false, KFULL, false, WM, S><<<grid, NTHR, 0, st>>>(g);
+  else if (b_kcontig) gemm_x3_kernel<false, true, KFULL, false, WM, S><<<grid, NTHR, 0, st>>>(g);
+  else gemm_x3_kernel<false, false, KFULL, false, WM, S><<<grid, NTHR, 0, st>>>(g);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
@@ -577,8 +603,12 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
   LBWN_REQUIRE(a.a_codes == nullptr, "gemm (bf16 split): one-hot A not supported");
   LBWN_REQUIRE(a.b3 == nullptr || (a.K % X3_BK == 0 && (((uintptr_t)a.b3) & 15) == 0),
                "gemm (bf16 split): pre-split B needs K %% 32 == 0 and 16-B alignment");
+  // 256-row tiles (8 waves, 2-stage pipeline) for the tall k-contiguous products with N <= 512
+  // (skip fwd, post1/post2 fwd, dH1, dS: 3-8 % faster); 128-row tiles at 2 blocks per CU for
+  // the rest (the mn-contiguous weight gradients: 1.3-1.5x slower on 256-row tiles; dZ, N =
+  // 1600).  LBWN_X3_WM=2|4 forces one.
   static const char* env = getenv("LBWN_X3_WM");
-  const int wm = (env && env[0] == '4') ? 4 : 2;   // 256-row tiles (8 waves): opt-in
+  const int wm = env ? (env[0] == '4' ? 4 : 2) : (a_kcontig && a.N <= 512 && a.M >= 8192 ? 4 : 2);
   lbwn_gemm_args g;
   dim3 grid;
   int e = gemm_setup(a, a_kcontig, b_kcontig, split_k, slab_ws, X3_BK, 64 * wm, 128, g, grid);
