@@ -366,12 +366,15 @@ struct X3Pre {
 
 // Epilogue of a wave's 64×64 (2×2 accumulators) at (m0 + 64·wm, n0 + 64·wn): bias, relu, mask,
 // accumulate; mask and C values loaded unconditionally at clamped indices before use.
-LBWN_DEV void x3_epilogue(const lbwn_gemm_args& g, floatx16 (&acc)[2][2], int m0, int n0, int wm, int wn, int lane) {
+// MI = 1 writes one 32-row band (rows m0 + 64·wm … +31) × 64 columns.
+template <int MI>
+LBWN_DEV void x3_epilogue_rows(const lbwn_gemm_args& g, floatx16 (&acc)[MI][2], int m0, int n0, int wm, int wn,
+                               int lane) {
   const int h = lane >> 5, ci = lane & 31;
   float* C = g.C + (long)blockIdx.z * g.split_stride;
   const bool raw = g.split_stride != 0;
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
+  for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
       const int col = n0 + wn * 64 + ni * 32 + ci, colc = min(col, g.N - 1);
@@ -400,6 +403,9 @@ LBWN_DEV void x3_epilogue(const lbwn_gemm_args& g, floatx16 (&acc)[2][2], int m0
         if (row < g.M) C[(long)row * g.ldc + col] = v;
       }
     }
+}
+LBWN_DEV void x3_epilogue(const lbwn_gemm_args& g, floatx16 (&acc)[2][2], int m0, int n0, int wm, int wn, int lane) {
+  x3_epilogue_rows<2>(g, acc, m0, n0, wm, wn, lane);
 }
 
 // Block tile (64·WM) × 128, WM × 2 waves of 64 × 64 (2 × 2 accumulators of 32 × 32).
