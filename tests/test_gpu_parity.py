@@ -211,6 +211,34 @@ def test_mulaw_gpu_golden(lib):
     np.testing.assert_allclose(out.cpu().numpy(), R.mu_decode_tf32(np.arange(256), 256), rtol=2e-6, atol=1e-7)
 
 
+@pytest.mark.parametrize('nq', [256, 64])
+def test_mulaw_tf32_encode(lib, nq):
+    """ops.mu_encode (ops.py:4-9, TF float32 graph) on the golden inputs against the oracle's
+    float32 restatement.  Bit-exact, except where the exact (float64) pre-truncation value
+    (amp+1)·mu/2+0.5 lies within 4 float32 ulps of an integer: there the truncation depends on
+    the last bit of log1pf, which TF (Eigen's plog1p), glibc and ROCm's ocml each round
+    differently, so either neighbour is the reference's answer.  Such points are counted and
+    must be rare."""
+    g = np.load(os.path.join(GOLDEN, 'mulaw.npz'))
+    xs = np.concatenate([g['mu_x32'], np.linspace(-1, 1, 20001, dtype=np.float32),
+                         np.random.default_rng(3).uniform(-1, 1, 20000).astype(np.float32)])
+    x = torch.tensor(xs, device=DEV)
+    q = torch.empty(x.numel(), dtype=torch.int32, device=DEV)
+    _lib.check(lib.lbwn_mulaw_encode(x.data_ptr(), q.data_ptr(), x.numel(), nq, 1, None))
+    got = q.cpu().numpy()
+    want = R.mu_encode_tf32(xs, nq)
+    mu = nq - 1
+    x64 = xs.astype(np.float64)
+    exact = (np.sign(x64) * np.log1p(mu * np.abs(x64)) / np.log1p(mu) + 1) * 0.5 * mu + 0.5
+    frac = exact - np.round(exact)
+    tie = np.abs(frac) <= 4 * np.spacing(np.float32(nq), dtype=np.float32)
+    bad = (got != want) & ~tie
+    assert not bad.any(), 'tf32 encode differs off-boundary at x=%s' % xs[bad][:8]
+    assert np.all(np.abs(got.astype(np.int64) - want) <= 1)
+    assert int(tie.sum()) <= 0.01 * xs.size, int(tie.sum())
+    assert got.min() >= 0 and got.max() <= mu
+
+
 # ---- full plan -------------------------------------------------------------------------------
 
 def _run_oracle(arch, net, q, ids):
