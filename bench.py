@@ -1,9 +1,16 @@
 #!/usr/bin/env python
 """Benchmark: WaveNet training step (forward + masked xent + backward + TF1 Adam) on
-MI355X, arch3 (par/arch3.json) with B = 8 streams x T = 4096 samples per GPU (BASELINE.json
-configs[1]), synthetic 16 kHz µ-law input dealt by the reference's slicing
-semantics.  Data-parallel over N GPUs (one process per GPU, RCCL all-reduce of the flat
-gradient bucket + loss stats): per-GPU work is fixed, so scaling is weak.
+MI355X with synthetic 16 kHz µ-law input dealt by the reference's slicing semantics.
+
+* N = 1: arch3 (par/arch3.json), B = 8 streams x T = 4096 (BASELINE.json configs[1], SURVEY
+  §8 C2) is the headline line; the same run adds C4 (arch5, B = 32), the per-GPU share of C5
+  (arch5, B = 8, one GPU), C1 (arch1, B = 2, T = 512, forward + loss) and C3 (cached
+  generation, arch3, B = 10) as sub-objects, each with its CPU baseline where one applies.
+* N > 1: C5 -- arch5 at 8 streams per GPU, data-parallel (one process per GPU, RCCL
+  all-reduce of the flat gradient bucket + loss stats): per-GPU work is fixed, so scaling is
+  weak.  ``python bench.py --gpus N`` without torch.distributed.run spawns the N ranks
+  itself (before anything touches the GPU; no exec); under torch.distributed.run it reads
+  RANK / LOCAL_RANK / WORLD_SIZE like any worker.
 
 Prints ONE JSON line (rank 0).  `value` = audio samples/s for the whole job (all ranks):
 N·B·T / step time.  `roofline` is for the dominant kernel, timed live with HIP events
@@ -15,6 +22,8 @@ cannot run here: TensorFlow 1.x is not installable) on a bounded sample on rank 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -22,16 +31,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, 'lb-wavenet_amd'))
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
-from lbwn import _lib  # noqa: E402
-from lbwn import dist as lbdist  # noqa: E402
-from lbwn.arch import load_arch, mel_hop_sz, n_layers, recep_field_sz  # noqa: E402
-from lbwn.data import SliceDealer, SyntheticSource  # noqa: E402
-from lbwn.imodel import WaveNetGen  # noqa: E402
-from lbwn.optim import AdamOptimizer  # noqa: E402
-from lbwn.tmodel import WaveNetTrain  # noqa: E402
 
 HBM_PEAK = 8.0e12        # B/s, MI355X_MICROARCH.md chip table
 FP32_MFMA_PEAK = 157.3e12  # FLOP/s dense fp32 MFMA
@@ -39,6 +38,7 @@ FP32_MFMA_PEAK = 157.3e12  # FLOP/s dense fp32 MFMA
 
 def kernel_work(name, arch, M):
     """Algorithmic work per launch."""
+    from lbwn.arch import n_layers
     L, Cr, Cd, Cs, Cp, Q = (n_layers(arch), arch['n_res'], arch['n_dil'], arch['n_skip'], arch['n_post'],
                             arch['n_quant'])
     flops = {
@@ -66,7 +66,7 @@ def kernel_work(name, arch, M):
 def gen_bytes_per_step(arch, B):
     """every weight read once per step (PRE table excluded: one row per stream)
     + per stream 50 lookback reads/writes of n_res floats + PRE row, skip/head vectors."""
-    from lbwn.arch import ParamLayout
+    from lbwn.arch import ParamLayout, n_layers
     lay = ParamLayout(arch)
     w = sum(e.numel for n, e in lay.entries.items() if n != 'PRE') * 4
     L, Cr = n_layers(arch), arch['n_res']
@@ -77,13 +77,15 @@ def gen_bytes_per_step(arch, B):
 def bench_gen(net, arch, B=10, seconds=3.0, sr=16000, chunk=1000):
     """imodel.py cached generation, arch3, B=10, 3 s @ 16 kHz (BASELINE configs[2]), graph
     replay of chunk-sized step sequences; weights = the benchmark net's."""
+    import torch
+    from lbwn.imodel import WaveNetGen
     g = WaveNetGen(arch['n_blocks'], arch['n_block_layers'], arch['n_quant'], arch['n_res'], arch['n_dil'],
                    arch['n_skip'], arch['n_post'], arch['n_gc_embed'], arch['n_gc_category'], arch['use_bias'],
                    B, chunk, None, seed=1, graph=True)
     g.load_params(net)
     n = int(seconds * sr)
     g.build_graph(n)
-    gc = list(range(1, B + 1)) if arch['n_gc_embed'] else None
+    gc = [1 + b % max(1, arch['n_gc_category']) for b in range(B)] if arch['n_gc_embed'] else None
     g.init_buffers(gc)
     g.step(chunk)   # capture + warm
     torch.cuda.synchronize()
@@ -103,137 +105,165 @@ def bench_gen(net, arch, B=10, seconds=3.0, sr=16000, chunk=1000):
                                  'chain, latency- not bandwidth-bound'}}
 
 
-def cpu_baseline(arch, seconds):
-    """Oracle (numpy fp32) fwd+loss+bwd+Adam at B=1, T=512 for ~`seconds`."""
-    sys.path.insert(0, ROOT)
-    from oracle import wavenet_ref as R
+def _cores():
     try:
         from threadpoolctl import threadpool_info
-        cores = max([x.get('num_threads', 1) for x in threadpool_info()] or [1])
+        return int(max([x.get('num_threads', 1) for x in threadpool_info()] or [1]))
     except Exception:
-        cores = os.cpu_count() or 1
+        return os.cpu_count() or 1
+
+
+def _oracle():
+    sys.path.insert(0, ROOT)
+    from oracle import wavenet_ref as R
+    return R
+
+
+def _timed(fn, seconds):
+    fn()    # warm-up (BLAS init)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        fn()
+        n += 1
+    return n, time.perf_counter() - t0
+
+
+def cpu_baseline(arch, seconds, B=1, T=512, backward=True, label='arch3'):
+    """Oracle (numpy fp32) train step (fwd+xent+bwd+TF1 Adam), or fwd+loss only, for
+    ~`seconds` on the host cores (the TF-CPU reference cannot run: TF is not installable)."""
+    R = _oracle()
     rng = np.random.default_rng(0)
     P = R.init_params(arch, rng, dtype=np.float32)
-    S = R.init_save(arch, 1, rng, dtype=np.float32)
-    B, T = 1, 512
+    S = R.init_save(arch, B, rng, dtype=np.float32)
     q = rng.integers(0, arch['n_quant'], (B, T))
-    ids = np.ones((B, T), np.int32)
+    ids = rng.integers(1, max(1, arch['n_gc_category']) + 1, (B, T)).astype(np.int32)
+    hop = 1
+    for u in arch['lc_upsample'] if arch['n_lc_out'] else []:
+        hop *= u
+    mel = rng.standard_normal((B, T // hop, arch['n_lc_in'])).astype(np.float32) if arch['n_lc_out'] else None
     opt = R.AdamTF1(1e-3)
 
     def step():
         nonlocal S
-        lg, cache, S = R.forward(arch, P, q, ids, S)
+        lg, cache, S = R.forward(arch, P, q, ids, S, mel)
         st, dlog = R.loss_fcn(arch, P, lg, q, ids, 1e-3)
-        G = R.backward(arch, P, cache, dlog, 1e-3)
-        opt.step(P, G)
+        if backward:
+            G = R.backward(arch, P, cache, dlog, 1e-3)
+            opt.step(P, G)
 
-    step()  # warm-up (BLAS init)
-    n, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        step()
-        n += 1
+    n, dt = _timed(step, seconds)
+    what = 'train step (fwd+xent+bwd+TF1 Adam)' if backward else 'forward + loss'
+    return {'value': B * T * n / dt, 'unit': 'audio samples/s', 'cores': _cores(), 'kind': 'port',
+            'sample': 'oracle/wavenet_ref.py numpy fp32 %s, %s, B=%d, T=%d, %d steps in %.1f s on the GPU box '
+                      'host (TF-CPU reference not installable)' % (what, label, B, T, n, dt)}
+
+
+def cpu_baseline_gen(arch, seconds, B=10):
+    """Oracle cached generation (imodel.py:214-272 restated) at C3's B for ~`seconds`."""
+    R = _oracle()
+    P = R.init_params(arch, np.random.default_rng(0), dtype=np.float32)
+    n0 = 20
+    t0 = time.perf_counter()
+    R.generate(arch, P, B, n0, seed=1)
+    per = (time.perf_counter() - t0) / n0
+    n = max(n0, int(seconds / max(per, 1e-6)))
+    t0 = time.perf_counter()
+    R.generate(arch, P, B, n, seed=1)
     dt = time.perf_counter() - t0
-    return {'value': B * T * n / dt, 'unit': 'audio samples/s', 'cores': int(cores), 'kind': 'port',
-            'sample': 'oracle/wavenet_ref.py numpy fp32 train step (fwd+xent+bwd+TF1 Adam), arch3, B=1, '
-                      'T=512, %d steps in %.1f s on the GPU box host (TF-CPU reference not installable)' % (n, dt)}
+    return {'value': B * n / dt, 'unit': 'audio samples/s', 'cores': _cores(), 'kind': 'port',
+            'sample': 'oracle/wavenet_ref.py numpy fp32 cached generation, arch3, B=%d, %d steps in %.1f s '
+                      '(C3 runs 48,000 steps; rate is per step, so the sample is scaled down)' % (B, n, dt)}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=8)
-    ap.add_argument('--arch', default=os.path.join(ROOT, 'par', 'arch3.json'))
-    ap.add_argument('--batch', type=int, default=8, help='streams per GPU')
-    ap.add_argument('--slice', type=int, default=4096)
-    ap.add_argument('--probe', default='auto')
-    ap.add_argument('--cpu-seconds', type=float, default=15.0)
-    ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--gc', type=int, default=None, help='--num-global-cond for GC archs')
-    ap.add_argument('--no-gen', action='store_true')
-    ap.add_argument('--gen-seconds', type=float, default=3.0)
-    args = ap.parse_args()
+class TrainBench:
+    """One (arch, B, T) training configuration on this rank: synthetic data from the GLOBAL
+    dealer over world·B slots (each rank keeps its rows, data.py:210-224), the plan, and a
+    step = forward + loss + backward + DP gradient all-reduce + TF1 Adam."""
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    if world != args.gpus:
-        raise SystemExit('--gpus %d but WORLD_SIZE=%d (launch N>1 with torch.distributed.run)' % (args.gpus, world))
-    dp = lbdist.init()          # one process per GPU; RCCL when WORLD_SIZE > 1
-    rank = dp.rank
-
-    arch = load_arch(args.arch, num_global_cond=args.gc)
-    B, T = args.batch, args.slice
-    net = WaveNetTrain(**arch, batch_sz=B, l2_factor=1e-3, print_interval=0, seed=0)   # par1.json values
-    opt = AdamOptimizer(1e-3)
-    dev = net.device
-
-    # synthetic data: the GLOBAL dealer over world·B slots; each rank keeps its rows
-    hop = mel_hop_sz(arch)
-    src = SyntheticSource(seed=1234, hop=hop, n_mel=arch['n_lc_in'] if arch['n_lc_out'] else 0,
-                          n_voices=max(1, arch['n_gc_category']), n_quant=arch['n_quant'])
-    dealer = SliceDealer(src, world * B, T, recep_field_sz(arch), hop, arch['n_lc_in'])
-    ring = []
-    for _ in range(8):
-        _, wav, mel, ids = next(dealer)
+    def __init__(self, arch, B, T, dp, backward=True):
+        import torch
+        from lbwn.arch import mel_hop_sz, recep_field_sz
+        from lbwn.data import SliceDealer, SyntheticSource
+        from lbwn.optim import AdamOptimizer
+        from lbwn.tmodel import WaveNetTrain
+        self.arch, self.B, self.T, self.dp, self.backward = arch, B, T, dp, backward
+        self.net = WaveNetTrain(**arch, batch_sz=B, l2_factor=1e-3, print_interval=0, seed=0)   # par1.json values
+        self.opt = AdamOptimizer(1e-3)
+        dev = self.net.device
+        hop = mel_hop_sz(arch)
+        src = SyntheticSource(seed=1234, hop=hop, n_mel=arch['n_lc_in'] if arch['n_lc_out'] else 0,
+                              n_voices=max(1, arch['n_gc_category']), n_quant=arch['n_quant'])
+        dealer = SliceDealer(src, dp.world * B, T, recep_field_sz(arch), hop, arch['n_lc_in'])
+        self.ring = []
         rows = dp.rows(B)
-        ring.append((torch.as_tensor(wav[rows], dtype=torch.int32).to(dev),
-                     None if mel is None else torch.as_tensor(mel[rows], dtype=torch.float32).to(dev),
-                     torch.as_tensor(ids[rows], dtype=torch.int32).to(dev)))
-    torch.cuda.synchronize()
-    plan = net._plan(T)
+        for _ in range(8):
+            _, wav, mel, ids = next(dealer)
+            self.ring.append((torch.as_tensor(wav[rows], dtype=torch.int32).to(dev),
+                              None if mel is None else torch.as_tensor(mel[rows], dtype=torch.float32).to(dev),
+                              torch.as_tensor(ids[rows], dtype=torch.int32).to(dev)))
+        torch.cuda.synchronize()
+        self.plan = self.net._plan(T)
 
-    def step(i):
-        q, mel, ids = ring[i % len(ring)]
-        net.forward(q, mel, ids, backward=True)
-        dp.reduce_grads(net)
-        opt.apply(net)
+    def step(self, i):
+        q, mel, ids = self.ring[i % len(self.ring)]
+        self.net.forward(q, mel, ids, backward=self.backward)
+        if self.backward:
+            self.dp.reduce_grads(self.net)
+            self.opt.apply(self.net)
 
-    def probe(name):
+    def probe(self, name):
+        import torch
+        from lbwn import _lib
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         e.record()   # materialise the HIP events
-        _lib.check(net.lib.lbwn_plan_probe(plan, name.encode(), s.cuda_event, e.cuda_event))
+        _lib.check(self.net.lib.lbwn_plan_probe(self.plan, name.encode(), s.cuda_event, e.cuda_event))
         return s, e
 
-    M = B * T
-    # candidates for the dominant kernel, likeliest first (one probe per warmup step): the
-    # backward and forward layer chains, then the single-launch GEMMs
-    cands = ['layer_bwd', 'dskip', 'layer_fwd', 'post1_fwd', 'dpost1', 'ds', 'post2_fwd', 'dpost2', 'dh']
-    warm_t = {}
-    for i in range(args.warmup):
-        pr = None
-        if args.probe == 'auto' and i >= 1 and i - 1 < len(cands):
-            pr = (cands[i - 1], probe(cands[i - 1]))
-        step(i)
-        if pr:
-            torch.cuda.synchronize()
-            warm_t[pr[0]] = pr[1][0].elapsed_time(pr[1][1])
-    dom = args.probe if args.probe != 'auto' else (max(warm_t, key=warm_t.get) if warm_t else 'layer_bwd')
+    def run(self, steps, warmup, probes=None, probe_mode='auto'):
+        """Warm up (one probe per warmup step to find the dominant kernel), then time
+        exactly `steps` steps between barrier + synchronize pairs; max over ranks."""
+        import torch
+        import torch.distributed as dist
+        world = self.dp.world
+        cands = probes or []
+        warm_t = {}
+        for i in range(warmup):
+            pr = None
+            if probe_mode == 'auto' and i >= 1 and i - 1 < len(cands):
+                pr = (cands[i - 1], self.probe(cands[i - 1]))
+            self.step(i)
+            if pr:
+                torch.cuda.synchronize()
+                warm_t[pr[0]] = pr[1][0].elapsed_time(pr[1][1])
+        dom = None
+        if cands:
+            dom = probe_mode if probe_mode != 'auto' else (max(warm_t, key=warm_t.get) if warm_t else cands[0])
+        samples = {dom: [], 'layer_fwd': []} if dom else {}
+        pending = []
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            if dom:
+                name = dom if i % 2 == 0 else 'layer_fwd'
+                pending.append((name, self.probe(name)))
+            self.step(warmup + i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        # a chain hand-off that timed out leaves its code in the plan's status word: the
+        # numbers of such a run are computed on garbage and must not be reported
+        self.net.check_status(self.T)
+        for name, (s, e) in pending:
+            samples[name].append(s.elapsed_time(e))
+        ms = self.dp.max_over_ranks(dt * 1000.0 / steps, self.net.device)
+        return ms, dom, samples, warm_t
 
-    # ---- timed region ----
-    samples = {dom: [], 'layer_fwd': []}
-    pending = []
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        if i % 2 == 0:
-            pending.append((dom, probe(dom)))
-        else:
-            pending.append(('layer_fwd', probe('layer_fwd')))
-        step(args.warmup + i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    for name, (s, e) in pending:
-        samples[name].append(s.elapsed_time(e))
-    ms = dt * 1000.0 / args.steps
-    ms = dp.max_over_ranks(ms, dev)
-    value = world * B * T / (ms / 1000.0)
-
-    def roof(name, ms_list):
-        bound, work = kernel_work(name, arch, M)
+    def roof(self, name, ms_list):
+        bound, work = kernel_work(name, self.arch, self.B * self.T)
         avg = float(np.mean(ms_list)) / 1000.0
         peak = FP32_MFMA_PEAK if bound == 'mfma' else HBM_PEAK
         ach = work / avg
@@ -242,6 +272,145 @@ def main():
                 'unit': 'TFLOP/s' if bound == 'mfma' else 'GB/s', 'frac': ach / peak,
                 'avg_launch_us': avg * 1e6, 'work_per_launch': work, 'traffic': traffic_from_profiles(name)}
 
+    def close(self):
+        import torch
+        del self.net, self.ring
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
+
+CANDS = ['layer_bwd', 'dskip', 'layer_fwd', 'post1_fwd', 'dpost1', 'ds', 'post2_fwd', 'dpost2', 'dh']
+
+
+def sub_bench(arch_file, B, T, dp, steps, warmup, gc=None, backward=True, label=''):
+    """A secondary configuration (C1 / C4 / C5-per-GPU) in the same run."""
+    from lbwn.arch import load_arch
+    arch = load_arch(arch_file, num_global_cond=gc)
+    tb = TrainBench(arch, B, T, dp, backward=backward)
+    ms, dom, samples, warm_t = tb.run(steps, warmup, probes=CANDS if backward else None)
+    out = {'workload': label, 'arch': os.path.basename(arch_file), 'batch_per_gpu': B, 'slice_sz': T,
+           'value': dp.world * B * T / (ms / 1000.0), 'unit': 'audio samples/s', 'ms_per_step': ms,
+           'steps': steps, 'warmup': warmup}
+    if dom:
+        out['roofline'] = tb.roof(dom, samples[dom])
+        out['roofline_dilconv'] = tb.roof('layer_fwd', samples['layer_fwd'])
+    tb.close()
+    return out
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=8)
+    ap.add_argument('--arch', default=None, help='default: par/arch3.json at N=1 (C2), par/arch5.json at N>1 (C5)')
+    ap.add_argument('--batch', type=int, default=8, help='streams per GPU')
+    ap.add_argument('--slice', type=int, default=4096)
+    ap.add_argument('--probe', default='auto')
+    ap.add_argument('--cpu-seconds', type=float, default=12.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--gc', type=int, default=None, help='--num-global-cond for GC archs')
+    ap.add_argument('--no-gen', action='store_true')
+    ap.add_argument('--no-extras', action='store_true', help='N=1: skip the C1 / C4 / C5-per-GPU sub-benchmarks')
+    ap.add_argument('--gen-seconds', type=float, default=3.0)
+    ap.add_argument('--dry-run', action='store_true',
+                    help='launcher + DP plumbing only, on the CPU over gloo (no GPU call): tests')
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launch(args, argv):
+    """`bench.py --gpus N` outside torch.distributed.run: start N rank processes of this
+    script (children, never an exec) with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, and
+    exit with the worst child status.  This parent never touches the GPU."""
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')    # dmabuf IPC only on this pool (RCCL)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0:
+                    rc = rc or code
+                    for q in procs:          # one rank failed: the collective would hang
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc if rc >= 0 else 128 - rc
+
+
+def dry_run(args):
+    """Rank processes join a gloo group, reduce a gradient-sized buffer through
+    lbwn.dist exactly as a training step does, and rank 0 prints one JSON line."""
+    import torch
+    from lbwn import dist as lbdist
+    from lbwn.arch import ParamLayout, load_arch
+    dp = lbdist.init(device_type='cpu')
+    arch = load_arch(args.arch or os.path.join(ROOT, 'par', 'arch5.json' if dp.world > 1 else 'arch3.json'),
+                     num_global_cond=args.gc)
+    n = ParamLayout(arch).n_total
+
+    class _Net:
+        grad_flat = torch.full((n,), float(dp.rank + 1))
+        stats = torch.tensor([1.0, 10.0 * (dp.rank + 1), 2.0, 0.0])
+    net = _Net()
+    t0 = time.perf_counter()
+    dp.reduce_grads(net)
+    ms = dp.max_over_ranks((time.perf_counter() - t0) * 1e3, 'cpu')
+    want = dp.world * (dp.world + 1) / 2
+    ok = bool(torch.all(net.grad_flat == want)) and float(net.stats[1]) == 10.0 * want
+    if dp.rank == 0:
+        print(json.dumps({'dry_run': True, 'world_size': dp.world, 'backend': torch.distributed.get_backend()
+                          if dp.enabled else None, 'grad_floats': n, 'reduce_ok': ok, 'reduce_ms': ms,
+                          'arch': os.path.basename(args.arch or ('arch5.json' if dp.world > 1 else 'arch3.json')),
+                          'batch_per_gpu': args.batch}), flush=True)
+    if dp.enabled:
+        torch.distributed.destroy_process_group()
+    return 0 if ok else 1
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        return launch(args, argv)
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    if world != args.gpus:
+        raise SystemExit('--gpus %d but WORLD_SIZE=%d' % (args.gpus, world))
+    if args.dry_run:
+        return dry_run(args)
+
+    import torch
+    import torch.distributed as dist
+    from lbwn import dist as lbdist
+    from lbwn.arch import load_arch
+    dp = lbdist.init()          # one process per GPU; RCCL when WORLD_SIZE > 1
+    rank = dp.rank
+    arch_file = args.arch or os.path.join(ROOT, 'par', 'arch3.json' if world == 1 else 'arch5.json')
+    arch = load_arch(arch_file, num_global_cond=args.gc)
+    B, T = args.batch, args.slice
+    tb = TrainBench(arch, B, T, dp)
+    net = tb.net
+    ms, dom, samples, warm_t = tb.run(args.steps, args.warmup, probes=CANDS, probe_mode=args.probe)
+    value = world * B * T / (ms / 1000.0)
+    cid = 'C2' if world == 1 and os.path.basename(arch_file) == 'arch3.json' else (
+        'C5' if os.path.basename(arch_file) == 'arch5.json' else 'custom')
+    name = os.path.basename(arch_file)
     out = {
         'metric': 'audio samples/sec: train fwd+bwd & cached autoregressive gen, 1/2/4/8 GPU',
         'value': value, 'unit': 'audio samples/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
@@ -250,22 +419,44 @@ def main():
                        '(error vs fp64 <= the f32 MFMA: tests/test_gpu_parity.py::test_gemm_split_accuracy)'
                        if net.lib.lbwn_gemm_get_mode() == 1 else 'f32 MFMA (v_mfma_f32_32x32x2_f32)'),
         'data': 'synthetic 16 kHz harmonic tones, mu-law 256, dealt with the reference slicing/mask semantics',
-        'config': {'workload': 'train step fwd+xent+bwd+TF1-Adam, par/arch3.json (5x10 layers, res/dil 32, '
-                               'skip/post 512, Q 256), B=%d streams x T=%d per GPU' % (B, T),
-                   'arch': os.path.basename(args.arch), 'batch_per_gpu': B, 'global_batch': world * B,
-                   'slice_sz': T, 'parallelism': 'dp%d' % world},
-        'roofline': roof(dom, samples[dom]),
-        'roofline_dilconv': roof('layer_fwd', samples['layer_fwd']),
+        'config': {'workload': '%s: train step fwd+xent+bwd+TF1-Adam, par/%s (5x10 layers, res/dil %d, skip/post %d, '
+                               'Q %d%s), B=%d streams x T=%d per GPU' % (
+                                   cid, name, arch['n_res'], arch['n_skip'], arch['n_quant'],
+                                   (', GC %d/%d' % (arch['n_gc_embed'], arch['n_gc_category']) if arch['n_gc_embed']
+                                    else '') + (', LC %d->%d x%s' % (arch['n_lc_in'], arch['n_lc_out'],
+                                                                     arch['lc_upsample']) if arch['n_lc_out'] else ''),
+                                   B, T),
+                   'arch': name, 'batch_per_gpu': B, 'global_batch': world * B,
+                   'slice_sz': T, 'parallelism': 'dp%d' % world, 'world_size_seen': dist.get_world_size()
+                   if dist.is_initialized() else 1},
+        'roofline': tb.roof(dom, samples[dom]),
+        'roofline_dilconv': tb.roof('layer_fwd', samples['layer_fwd']),
         'warmup_probe_ms': warm_t,
     }
     if world == 1 and not args.no_gen and arch['n_lc_out'] == 0:
         out['gen'] = bench_gen(net, arch, B=10, seconds=args.gen_seconds)
+        if not args.no_cpu_baseline:
+            out['gen']['cpu_baseline'] = cpu_baseline_gen(arch, args.cpu_seconds * 0.5)
+    tb.close()
+    if world == 1 and not args.no_extras and args.arch is None:
+        par = lambda f: os.path.join(ROOT, 'par', f)   # noqa: E731
+        out['c4'] = sub_bench(par('arch5.json'), 32, 4096, dp, 10, 3, label='C4: arch5 deep stack, B=32 x T=4096, '
+                              'train fwd+bwd+Adam, 1 GPU')
+        out['c5_per_gpu'] = sub_bench(par('arch5.json'), 8, 4096, dp, 10, 3,
+                                      label='C5 per-GPU share on one GPU: arch5, B=8 x T=4096 (the N>1 runs '
+                                            'default to this per rank: scaling reference)')
+        out['c1'] = sub_bench(par('arch1.json'), 2, 512, dp, 20, 5, backward=False,
+                              label='C1: arch1 (GC 17/377), B=2 x T=512, forward + masked xent loss')
+        if not args.no_cpu_baseline:
+            out['c1']['cpu_baseline'] = cpu_baseline(load_arch(par('arch1.json')), args.cpu_seconds * 0.5, B=2,
+                                                     T=512, backward=False, label='arch1')
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(arch, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 def traffic_from_profiles(kernel):
@@ -283,4 +474,4 @@ def traffic_from_profiles(kernel):
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main())

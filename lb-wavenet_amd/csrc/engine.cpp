@@ -222,7 +222,7 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->oSPLIT2 = carve(cur, sizeof(float) * (size_t)lbwn_pre_grad_ws_floats(p->Q, p->Cr));   // dPRE partials
   // three column sums at once in the backward (dlogits, dH1, dS)
   p->oCOLS = carve(cur, sizeof(float) * 3 * (size_t)lbwn_colsum_ws_floats((int)M, std::max({p->Cs, p->Cp, p->Q, p->Cr})));
-  // [status (16 B) | hand-off flags], zeroed together before every chain launch
+  // [status (16 B) | hand-off flags]: status zeroed once per step, flags before each chain
   p->oSTATUS = carve(cur, 16 + sizeof(unsigned) * (size_t)B * ((T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS));
   p->oFLAGS = p->oSTATUS + 16;
   {
@@ -473,7 +473,9 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   int e;
   if ((e = ensure_device(p))) return e;
   LBWN_REQUIRE(p->Lo == 0 || mel, "train_forward: LC arch needs the mel input");
-  if (!p->chain) LBWN_HIP(hipMemsetAsync(at<char>(ws, p->oSTATUS), 0, 16, st));  // chains zero it themselves
+  // the sticky status word (chain spin timeouts OR their codes in) lives for one step:
+  // zeroed here, read by the host after the step (lbwn_plan_tensor "status")
+  LBWN_HIP(hipMemsetAsync(at<char>(ws, p->oSTATUS), 0, 16, st));
   const int L = p->L, B = p->B, T = p->T, H = p->H, Cr = p->Cr, Cd = p->Cd;
   const long M = p->M, ldz = (long)L * Cd;
   float* X = at<float>(ws, p->oX);

@@ -408,7 +408,9 @@ LBWN_DEV bool wait_flag_ge(unsigned* f, unsigned want, unsigned* status, unsigne
   for (;;) {
     if (__hip_atomic_load((gu32*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) return true;
     if (wall_clock64() - t0 > SPIN_TIMEOUT) {
-      __hip_atomic_store((gu32*)status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // OR, not store: the word is zeroed once per step (lbwn_train_forward), so a forward
+      // timeout (1) survives the backward chain and both read back as 3
+      __hip_atomic_fetch_or((gu32*)status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -1491,7 +1493,8 @@ int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   LBWN_REQUIRE(!c.wpack_x3 || (((uintptr_t)c.wpack_x3) & 15) == 0, "chain fwd: split images not 16-B aligned");
   const int tps = (c.T + LP - 1) / LP;
   LBWN_REQUIRE((unsigned*)c.status + 4 == c.flags, "chain: status word must head the flag block");
-  LBWN_HIP(hipMemsetAsync(c.status, 0, (16 + (size_t)c.B * tps * 4 + 15) / 16 * 16, st));
+  // hand-off flags only: the status word is sticky for the whole step
+  LBWN_HIP(hipMemsetAsync(c.flags, 0, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st));
   if (c.wpack_x3) chain_fwd_kernel<true><<<c.grid, 256, 0, st>>>(k);
   else chain_fwd_kernel<false><<<c.grid, 256, 0, st>>>(k);
   LBWN_CHECK_LAUNCH();
@@ -1512,7 +1515,8 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   k.trace = c.trace ? c.trace + 16L * c.L : nullptr; k.trace_blk = c.trace_blk;
   const int tps = (c.T + LP - 1) / LP;
   LBWN_REQUIRE((unsigned*)c.status + 4 == c.flags, "chain: status word must head the flag block");
-  LBWN_HIP(hipMemsetAsync(c.status, 0, (16 + (size_t)c.B * tps * 4 + 15) / 16 * 16, st));
+  // hand-off flags only: the status word is sticky for the whole step
+  LBWN_HIP(hipMemsetAsync(c.flags, 0, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st));
   chain_bwd_kernel<<<c.grid, 256, 0, st>>>(k);
   LBWN_CHECK_LAUNCH();
   return 0;

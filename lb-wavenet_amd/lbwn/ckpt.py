@@ -80,10 +80,14 @@ class Checkpoint:
                 pass
         return path_pfx
 
-    def restore(self):
+    def restore(self, select=None):
+        """``select(name, tensor) -> tensor`` picks the part of a stored tensor this
+        process owns (data-parallel SAVE rows); identity by default."""
         f = '{}-{}'.format(self.ckpt_path, self.resume_step)
         print('Restoring from {}'.format(f))
         loaded = load_tensors(f)
+        if select is not None:
+            loaded = {k: select(k, v) for k, v in loaded.items()}
         missing = [k for k in self.saveable_objects if k not in loaded]
         if missing:
             print('Checkpoint {} lacks {} variables (first: {})'.format(f, len(missing), missing[0]), file=sys.stderr)

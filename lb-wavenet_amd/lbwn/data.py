@@ -21,7 +21,7 @@ from .ops import mu_encode_np
 
 class SliceDealer:
     def __init__(self, files, batch_sz, slice_sz, recep_field_sz, mel_hop_sz=1, mel_spectrum_sz=0,
-                 log=None):
+                 log=None, start=0):
         if slice_sz % mel_hop_sz != 0:      # data.py:32-36
             requested = slice_sz
             slice_sz += mel_hop_sz - (slice_sz % mel_hop_sz)
@@ -33,14 +33,16 @@ class SliceDealer:
         self.mel_hop_sz = mel_hop_sz
         self.mel_spectrum_sz = mel_spectrum_sz
         self.log = log or sys.stderr
-        self.files_read = 0
+        # the shared read counter is seeded with the resume position (ckpt_position), as
+        # _wav_gen seeds datum_count (data.py:79, :96): counts stay absolute across resumes
+        self.files_read = int(start)
         self._files = iter(files)
         self._gens = [self._slot() for _ in range(batch_sz)]
 
     def _next_file(self):
         vid, wav, mel = next(self._files)
         self.files_read += 1
-        return vid, wav, mel
+        return self.files_read, vid, wav, mel
 
     def _slot(self):
         hop, F, T = self.mel_hop_sz, self.recep_field_sz, self.slice_sz
@@ -48,7 +50,7 @@ class SliceDealer:
         parts_w, parts_m, parts_i = [], [], []
         while True:
             try:
-                vid, wav, mel = self._next_file()
+                cnt, vid, wav, mel = self._next_file()
             except StopIteration:
                 return
             snip = len(wav) % hop
@@ -69,7 +71,7 @@ class SliceDealer:
                 if mel is not None:
                     parts_m.append(mel[pos // hop:(pos + need) // hop])
                 pos += need
-                yield (np.concatenate(parts_w), np.concatenate(parts_m) if parts_m else None,
+                yield (cnt, np.concatenate(parts_w), np.concatenate(parts_m) if parts_m else None,
                        np.concatenate(parts_i))
                 parts_w, parts_m, parts_i = [], [], []
                 need = T
@@ -84,13 +86,15 @@ class SliceDealer:
         return self
 
     def __next__(self):
-        """(files_read, wav[B,T], mel[B,T/hop,C] or None, ids[B,T]); StopIteration when
-        the shared file iterator runs dry (data.py:219-227)."""
+        """(latest_file_read_count, wav[B,T], mel[B,T/hop,C] or None, ids[B,T]);
+        StopIteration when the shared file iterator runs dry (data.py:217-227).  The count is
+        that of the file the LAST slot's slice ended in (``batch[-1][0]``, data.py:220), not
+        the number of reads so far: later slots may have read ahead."""
         batch = [next(g) for g in self._gens]
-        wav = np.stack([b[0] for b in batch])
-        mel = np.stack([b[1] for b in batch]) if batch[0][1] is not None else None
-        ids = np.stack([b[2] for b in batch])
-        return self.files_read, wav, mel, ids
+        wav = np.stack([b[1] for b in batch])
+        mel = np.stack([b[2] for b in batch]) if batch[0][2] is not None else None
+        ids = np.stack([b[3] for b in batch])
+        return batch[-1][0], wav, mel, ids
 
 
 def npy_catalog(sam_file, repeat=True, shuffle_seed=None, skip=0):
@@ -227,7 +231,7 @@ class MaskedSliceWav:
             import queue
             import threading
             dealer = SliceDealer(self._files(), self.batch_sz, self.slice_sz, self.recep_field_sz,
-                                 self.mel_hop_sz, self.mel_spectrum_sz)
+                                 self.mel_hop_sz, self.mel_spectrum_sz, start=int(self.ckpt_position[0]))
             q = queue.Queue(maxsize=self.prefetch_sz)
             rows = self.rows
 

@@ -56,6 +56,7 @@ class WaveNetTrain:
         self.resume_step = resume_step
         self.n_valid_total = n_valid_total
         self.print_interval = print_interval
+        self.dp = None      # lbwn.dist.DPContext when training data-parallel (set by train.py)
         self.device = torch.device(device)
         self.lib = _lib.load()
         self.layout = ParamLayout(self.arch)
@@ -193,6 +194,18 @@ class WaveNetTrain:
                                                     _lib.ptr(mel), sp))
         return self.stats
 
+    def status(self, T=None):
+        """The plan's sticky status word for the last step (synchronises): 0 = ok; bit 0 =
+        a forward-chain hand-off timed out, bit 1 = a backward-chain one (the step's
+        outputs are then garbage and must not be applied)."""
+        T = T if T is not None else self._last[0].shape[1]
+        return int(self.plan_tensor(T, 'status')[:1].view(torch.int32).item())
+
+    def check_status(self, T=None):
+        st = self.status(T)
+        if st:
+            raise RuntimeError('lbwn: chain hand-off timed out (status word %#x): the last step is invalid' % st)
+
     def l2_loss(self):
         """tmodel.py:250-261: Σ_{trainable, non-BIAS} Σv²/2 (the weight region of the flat buffer)."""
         w = self.flat[:self.layout.n_weights]
@@ -213,7 +226,8 @@ class WaveNetTrain:
         l2 = float(self.l2_loss())
         total = mean + self.l2_factor * l2
         B, T = self._last[0].shape
-        avg_diff = int(st[2]) // (B * (T - 1))
+        world = self.dp.world if self.dp is not None else 1     # stats[2] is summed over ranks
+        avg_diff = int(st[2]) // (world * B * (T - 1))
         pct = cnt[1] * 100.0 / self.n_valid_total if self.n_valid_total else 0.0
         return ('{:5d}\t{:8.4f}\t{:8.4f}\t{:7.2f}\t{:5.0f}\t{:5.0f}\t{:10d}\t{:14d}\t{:5.2f}'.format(
             cnt[0], total, mean, l2, avg_diff, nv, cnt[1], int(self.n_valid_total), pct))
@@ -227,15 +241,35 @@ class WaveNetTrain:
 
     # ---- checkpoints (ckpt.py:53-81) --------------------------------------------------------
     def save(self, step, optimizer=None):
-        """Write '<ckpt_path>-<step>.safetensors'; with ``optimizer`` its Adam slots too."""
+        """Write '<ckpt_path>-<step>.safetensors'; with ``optimizer`` its Adam slots too.
+        Data-parallel: a collective (every rank calls it).  The weights are replicated, but
+        SAVE is per stream, so the ranks' rows are gathered and rank 0 writes the SAVE of
+        the GLOBAL batch [world·B, d, Cr] -- the same file a single process over world·B
+        streams writes; the other ranks return None."""
         if self.device.type == 'cuda':
             torch.cuda.synchronize(self.device)
-        extra = optimizer.state_tensors(self) if optimizer is not None else None
+        extra = dict(optimizer.state_tensors(self)) if optimizer is not None else {}
+        if self.dp is not None and self.dp.enabled:
+            extra.update(self._gather_save())
+            if self.dp.rank != 0:
+                return None
         return self.ckpt.save(step, extra)
 
+    def _gather_save(self):
+        import torch.distributed as dist
+        parts = [torch.empty_like(self.save_flat) for _ in range(self.dp.world)]
+        dist.all_gather(parts, self.save_flat)
+        return OrderedDict((n, torch.cat([p[o:o + int(np.prod(s))].view(*s) for p in parts], 0))
+                           for n, (o, s) in self.save_index.items())
+
     def restore(self, optimizer=None):
-        """Load '<ckpt_path>-<resume_step>' into the live buffers (ckpt.py:63-81)."""
-        loaded = self.ckpt.restore()
+        """Load '<ckpt_path>-<resume_step>' into the live buffers (ckpt.py:63-81).  Under
+        data parallelism each rank takes its own rows of the global-batch SAVE."""
+        select = None
+        if self.dp is not None and self.dp.enabled:
+            rows = self.dp.rows(self.batch_sz)
+            select = lambda name, t: t[rows] if name in self.save_vars else t   # noqa: E731
+        loaded = self.ckpt.restore(select)
         if optimizer is not None:
             optimizer.load_state_tensors(self, loaded)
         self.global_step_host = int(self.counters[0])

@@ -57,6 +57,18 @@ def get_args(argv=None):
     return p.parse_args(argv)
 
 
+def prepare_arch(arch, num_global_cond):
+    """The ARCH_FILE dict brought to WaveNetTrain's 14 keys; -gc may supply the
+    n_gc_category the file lacks (train.py:77-80, :138-146: par/arch2.json, arch4.json).
+    Errors print to stderr and exit(1), like the reference."""
+    from lbwn.arch import ArchError, normalize_arch
+    try:
+        return normalize_arch(arch, num_global_cond=num_global_cond)
+    except ArchError as e:
+        print(str(e), file=sys.stderr)
+        sys.exit(1)
+
+
 def main(argv=None):
     args = get_args(argv)
     from sys import stderr
@@ -101,8 +113,8 @@ def main(argv=None):
     from lbwn.optim import AdamOptimizer
     from lbwn.tmodel import WaveNetTrain
 
+    arch = prepare_arch(arch, args.num_global_cond)
     dp = lbdist.init()
-    arch = normalize_arch(arch)
     hop = hop_of(arch)
     B = par['batch_sz']
     dset = MaskedSliceWav(None, args.sam_file, par['sample_rate'], par['slice_sz'], par['prefetch_sz'],
@@ -123,6 +135,7 @@ def main(argv=None):
                        resume_step=args.resume_step or 0, n_valid_total=par.get('n_valid_total', 0),
                        print_interval=args.progress_interval if dp.rank == 0 else 0,
                        seed=args.seed if args.seed is not None else 0)
+    net.dp = dp
     dset.set_receptive_field_size(net.get_recep_field_sz())
     dset.build()
     dset.init_vars()
@@ -145,14 +158,20 @@ def main(argv=None):
             break
         net.forward(wav_input, mel_input, id_mask, backward=True)
         dp.reduce_grads(net)
+        if args.progress_interval and net.global_step_host % args.progress_interval == 0:
+            net.check_status()                # a chain hand-off timeout invalidates the step
         net.maybe_print()                     # tmodel.py:272-281 prints before the step counters advance
         optimizer.apply(net)
-        if step % args.save_interval == 0 and step != args.resume_step and dp.rank == 0:
-            net_save_path = net.save(step, optimizer)
-            dset_save_path = dset.save(step, file_read_count)
-            print('Saved checkpoints to {} and {}'.format(net_save_path, dset_save_path), file=stderr)
+        if step % args.save_interval == 0 and step != args.resume_step:
+            net.check_status()
+            net_save_path = net.save(step, optimizer)        # collective under DP
+            if dp.rank == 0:
+                dset_save_path = dset.save(step, file_read_count)
+                print('Saved checkpoints to {} and {}'.format(net_save_path, dset_save_path), file=stderr)
         step += 1
     torch.cuda.synchronize()
+    if step > (args.resume_step or 1):
+        net.check_status()
     return net
 
 

@@ -37,15 +37,18 @@ def _import_reference():
     return ops, data
 
 
-def _dealer(data_mod, files, batch_sz, slice_sz, recep, hop, nmel):
-    """Drive the reference's slice factory + batch loop with a plain shared iterator."""
+def _dealer(data_mod, files, batch_sz, slice_sz, recep, hop, nmel, start=0):
+    """Drive the reference's slice factory + batch loop with a plain shared iterator.
+    ``start`` plays the dataset's ckpt_position: _wav_gen seeds its counter with it and
+    the file stream is skipped by it (data.py:79-88, :250), so the i-th file read after a
+    resume carries the count start + i."""
     dset = data_mod.MaskedSliceWav.__new__(data_mod.MaskedSliceWav)
     dset.slice_sz = slice_sz
     dset.batch_sz = batch_sz
     dset.mel_hop_sz = hop
     dset.mel_spectrum_sz = nmel
     dset.recep_field_sz = recep
-    shared = iter([(i + 1, vid, wav, mel) for i, (vid, wav, mel) in enumerate(files)])
+    shared = iter([(start + i + 1, vid, wav, mel) for i, (vid, wav, mel) in enumerate(files[start:])])
     gens = [dset._gen_concat_slice_factory(shared)() for _ in range(batch_sz)]
     out = []
     while True:
@@ -54,7 +57,7 @@ def _dealer(data_mod, files, batch_sz, slice_sz, recep, hop, nmel):
         except StopIteration:
             break
         out.append((np.stack([b[1] for b in batch]), np.stack([b[2] for b in batch]),
-                    np.stack([b[3] for b in batch])))
+                    np.stack([b[3] for b in batch]), batch[-1][0]))     # data.py:220
     return out
 
 
@@ -78,6 +81,7 @@ CASES = {
     'hop256_b4': (8, 30, 200, 9000, 4, 512, 1023, 256, 5, 376),
     'recep5115_b2': (9, 12, 3000, 30000, 2, 4096, 5115, 256, 2, 17),
 }
+RESUME_AT = 6
 
 
 def main():
@@ -104,24 +108,28 @@ def main():
                (5, np.arange(7, dtype=np.float64) + 100, np.zeros((7, 2))),
                (2, np.arange(3, dtype=np.float64) + 200, np.zeros((3, 2))),
                (7, np.arange(12, dtype=np.float64) + 300, np.zeros((12, 2)))]
-    cases['small'] = (f_small, 1, 8, 4, 1, 2)
+    cases['small'] = (f_small, 1, 8, 4, 1, 2, 0)
     for name, (seed, nf, lo, hi, B, T, F, hop, nmel, mv) in CASES.items():
-        cases[name] = (make_files(seed, nf, lo, hi, hop, nmel, mv), B, T, F, hop, nmel)
+        cases[name] = (make_files(seed, nf, lo, hi, hop, nmel, mv), B, T, F, hop, nmel, 0)
+    # a resumed stream: the same files with ckpt_position = RESUME_AT
+    seed, nf, lo, hi, B, T, F, hop, nmel, mv = CASES['hop4_b3']
+    cases['hop4_b3_resume'] = (make_files(seed, nf, lo, hi, hop, nmel, mv), B, T, F, hop, nmel, RESUME_AT)
     meta = []
-    for name, (files, B, T, F, hop, nmel) in cases.items():
-        batches = _dealer(data, files, B, T, F, hop, nmel)
+    for name, (files, B, T, F, hop, nmel, start) in cases.items():
+        batches = _dealer(data, files, B, T, F, hop, nmel, start)
         d = {'n_batches': np.array(len(batches)), 'B': np.array(B), 'T': np.array(T),
              'F': np.array(F), 'hop': np.array(hop), 'nmel': np.array(nmel),
-             'n_files': np.array(len(files))}
+             'n_files': np.array(len(files)), 'start': np.array(start)}
         if name == 'small':
             for i, (vid, wav, mel) in enumerate(files):
                 d['file_vid_%d' % i] = np.array(vid)
                 d['file_wav_%d' % i] = wav
                 d['file_mel_%d' % i] = mel
-        for j, (w, m, ids) in enumerate(batches):
+        for j, (w, m, ids, cnt) in enumerate(batches):
             d['wav_%d' % j] = w.astype(np.int64)          # ramps: exact integers
             d['mel_%d' % j] = m.astype(np.int64)
             d['ids_%d' % j] = ids
+            d['cnt_%d' % j] = np.array(int(cnt))           # latest_file_read_count
         np.savez_compressed(os.path.join(HERE, 'dealer_%s.npz' % name), **d)
         meta.append('%s: %d files -> %d batches of [%d,%d]' % (name, len(files), len(batches), B, T))
     print('\n'.join(meta))

@@ -1,6 +1,7 @@
 """Host-side drop-in surface (CPU): checkpoints (ckpt.py), the MaskedSliceWav dataset
 (data.py:20-293), train.py argument handling (train.py:12-80), and the data-parallel
 gradient reduction over gloo with world_size 2."""
+import json
 import os
 import sys
 
@@ -120,6 +121,39 @@ def test_masked_slice_wav_resume_and_rows(tmp_path):
     np.testing.assert_array_equal(a[3][2:4], b[3])
 
 
+def test_masked_slice_wav_double_resume_counts_are_absolute(tmp_path):
+    """save -> resume -> save -> resume: the read counter is seeded with ckpt_position
+    (data.py:79, :96), so the second resume continues after every file read so far."""
+    cat = _write_catalog(tmp_path, n_files=7)
+    mk = lambda step, **kw: MaskedSliceWav(None, cat, 16000, 64, 2, 3, 4, 2, 5, str(tmp_path / 'x.dset'), step, **kw)
+    ref = mk(0, random_seed=11)
+    ref.init_sample_catalog()
+    files = ref._files()
+    order = [next(files)[1][:6].tolist() for _ in range(40)]
+    ds = mk(0, random_seed=11)
+    ds.init_sample_catalog()
+    ds.set_receptive_field_size(13)
+    ds.build()
+    for _ in range(3):
+        cnt1 = ds.get_op()[0]
+    ds.save(3, cnt1)
+    r1 = mk(3)
+    r1.init_sample_catalog()
+    r1.set_receptive_field_size(13)
+    r1.build()
+    r1.restore()
+    assert next(r1._files())[1][:6].tolist() == order[cnt1]
+    for _ in range(4):
+        cnt2 = r1.get_op()[0]
+    assert cnt2 > cnt1                       # absolute, not counted from the resume
+    r1.save(7, cnt2)
+    r2 = mk(7)
+    r2.init_sample_catalog()
+    r2.restore()
+    assert int(r2.ckpt_position[0]) == cnt2
+    assert next(r2._files())[1][:6].tolist() == order[cnt2]
+
+
 def test_train_cli_errors(tmp_path, monkeypatch):
     sys.path.insert(0, os.path.join(ROOT, 'lb-wavenet_amd'))
     import train
@@ -133,6 +167,15 @@ def test_train_cli_errors(tmp_path, monkeypatch):
     with pytest.raises(SystemExit) as e:
         train.main(['--cpu-only', str(tmp_path / 'ck'), os.path.join(ROOT, 'par', 'arch3.json'), par, 'none.txt'])
     assert e.value.code == 1
+    # -gc supplies n_gc_category for arch files that lack it (train.py:77-80, :138-146)
+    for f in ('arch2', 'arch4'):
+        with open(os.path.join(ROOT, 'par', f + '.json')) as fp:
+            raw = json.load(fp)
+        with pytest.raises(SystemExit) as e:
+            train.prepare_arch(raw, None)
+        assert e.value.code == 1
+        a = train.prepare_arch(raw, 12)
+        assert a['n_gc_category'] == 12 and 'lc_hop_sz' not in a
     args = train.get_args(['-bs', '4', '-ss', '1024', '-lr', '0.01', '-rs', '7', 'p', 'a', 'b', 'c'])
     assert (args.batch_size, args.slice_size, args.learning_rate, args.resume_step) == (4, 1024, 0.01, 7)
 
@@ -203,3 +246,57 @@ def test_dp_gloo_two_ranks_equals_single_process(tmp_path):
     for n, e in lay.entries.items():   # Adam divides the summed raw grads by the GLOBAL n_valid
         np.testing.assert_allclose(got['grads'][e.offset:e.offset + e.numel] / got['stats'][1], G[n].reshape(-1),
                                    rtol=2e-4, atol=1e-7, err_msg=n)
+
+
+def _ckpt_worker(rank, world, port, path):
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, 'lb-wavenet_amd'))
+    from lbwn.dist import DPContext
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    dp = DPContext(world, rank, rank)
+    net = WaveNetTrain(**small_arch(), batch_sz=2, l2_factor=0.0, device='cpu', ckpt_path=path, seed=0)
+    net.dp = dp
+    net.save_flat.copy_(torch.arange(net.save_flat.numel(), dtype=torch.float32) + 1000.0 * rank)
+    ret = net.save(5)                       # collective
+    assert (ret is None) == (rank != 0)
+    dist.barrier()
+    back = WaveNetTrain(**small_arch(), batch_sz=2, l2_factor=0.0, device='cpu', ckpt_path=path, resume_step=5,
+                        seed=1)
+    back.dp = dp
+    back.restore()
+    assert torch.equal(back.save_flat, net.save_flat), rank     # each rank gets its own rows back
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_checkpoint_gathers_per_rank_save(tmp_path):
+    """SAVE is per stream: under DP the checkpoint holds the global batch's SAVE rows
+    (what one process over world·B streams writes) and each rank restores its own."""
+    import torch.multiprocessing as mp
+    path = str(tmp_path / 'dp.net')
+    port = 29500 + (os.getpid() + 7) % 1000
+    mp.spawn(_ckpt_worker, args=(2, port, path), nprocs=2, join=True)
+    t = load_tensors(path + '-5')
+    one = WaveNetTrain(**small_arch(), batch_sz=4, l2_factor=0.0, device='cpu', seed=0)
+    for n, v in one.save_vars.items():
+        assert tuple(t[n].shape) == tuple(v.shape), n
+        per_rank = t[n].shape[0] // 2
+        assert torch.all(t[n][per_rank:] - t[n][:per_rank] == 1000.0), n
+
+
+def test_bench_self_launch_dry_run():
+    """`bench.py --gpus 2` outside torch.distributed.run spawns its own ranks (children,
+    no exec) and the DP plumbing reduces through lbwn.dist over gloo; --dry-run stops
+    before any GPU call.  N>1 defaults to C5 (arch5, 8 streams per GPU)."""
+    import json as _json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK')}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '2', '--dry-run'],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, r.stdout
+    d = _json.loads(lines[0])
+    assert d['world_size'] == 2 and d['backend'] == 'gloo' and d['reduce_ok']
+    assert d['arch'] == 'arch5.json' and d['batch_per_gpu'] == 8

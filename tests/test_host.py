@@ -12,21 +12,24 @@ from tests.conftest import GOLDEN, ROOT
 from tests.golden.make_golden import CASES, make_files
 
 
-@pytest.mark.parametrize('name', ['small', 'hop4_b3', 'hop256_b4', 'recep5115_b2'])
+@pytest.mark.parametrize('name', ['small', 'hop4_b3', 'hop256_b4', 'recep5115_b2', 'hop4_b3_resume'])
 def test_product_dealer_matches_reference_golden(name):
+    """wav/mel/ids and latest_file_read_count (data.py:220) against the reference's own
+    dealer; the _resume case starts at ckpt_position = 6 (data.py:79, :250)."""
     g = np.load(os.path.join(GOLDEN, 'dealer_%s.npz' % name))
     if name == 'small':
         files = [(int(g['file_vid_%d' % i]), g['file_wav_%d' % i], g['file_mel_%d' % i])
                  for i in range(int(g['n_files']))]
     else:
-        seed, nf, lo, hi, B, T, F, hop, nmel, mv = CASES[name]
+        seed, nf, lo, hi, B, T, F, hop, nmel, mv = CASES[name.replace('_resume', '')]
         files = make_files(seed, nf, lo, hi, hop, nmel, mv)
-    B, T, F, hop, nmel = (int(g[k]) for k in ('B', 'T', 'F', 'hop', 'nmel'))
+    B, T, F, hop, nmel, start = (int(g[k]) for k in ('B', 'T', 'F', 'hop', 'nmel', 'start'))
     import io
-    d = SliceDealer(files, B, T, F, hop, nmel, log=io.StringIO())
+    d = SliceDealer(files[start:], B, T, F, hop, nmel, log=io.StringIO(), start=start)
     out = list(d)
     assert len(out) == int(g['n_batches'])
-    for j, (_, w, m, ids) in enumerate(out):
+    for j, (cnt, w, m, ids) in enumerate(out):
+        assert cnt == int(g['cnt_%d' % j]), j
         np.testing.assert_array_equal(ids, g['ids_%d' % j])
         np.testing.assert_array_equal(w.astype(np.int64), g['wav_%d' % j])
         np.testing.assert_array_equal(m.astype(np.int64), g['mel_%d' % j])
