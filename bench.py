@@ -6,11 +6,14 @@ MI355X with synthetic 16 kHz µ-law input dealt by the reference's slicing seman
   §8 C2) is the headline line; the same run adds C4 (arch5, B = 32), the per-GPU share of C5
   (arch5, B = 8, one GPU), C1 (arch1, B = 2, T = 512, forward + loss) and C3 (cached
   generation, arch3, B = 10) as sub-objects, each with its CPU baseline where one applies.
-* N > 1: C5 -- arch5 at 8 streams per GPU, data-parallel (one process per GPU, RCCL
-  all-reduce of the flat gradient bucket + loss stats): per-GPU work is fixed, so scaling is
-  weak.  ``python bench.py --gpus N`` without torch.distributed.run spawns the N ranks
-  itself (before anything touches the GPU; no exec); under torch.distributed.run it reads
-  RANK / LOCAL_RANK / WORLD_SIZE like any worker.
+* N > 1: data-parallel (one process per GPU, RCCL all-reduce of the flat gradient bucket +
+  loss stats), per-GPU work fixed, so scaling is weak.  The headline line keeps the N = 1
+  configuration per GPU (arch3, B = 8 per GPU) so that value(N) / value(1) is a true
+  weak-scaling ratio; the same run then measures C5 -- arch5 at 8 streams per GPU, B = 8N
+  in total (BASELINE configs[4] at N = 8) -- as the ``c5`` sub-object, whose one-GPU
+  reference is the N = 1 line's ``c5_per_gpu``.  ``python bench.py --gpus N`` without
+  torch.distributed.run spawns the N ranks itself (before anything touches the GPU; no
+  exec); under torch.distributed.run it reads RANK / LOCAL_RANK / WORLD_SIZE like any worker.
 
 Prints ONE JSON line (rank 0).  `value` = audio samples/s for the whole job (all ranks):
 N·B·T / step time.  `roofline` is for the dominant kernel, timed live with HIP events
@@ -262,7 +265,9 @@ class TrainBench:
         ms = self.dp.max_over_ranks(dt * 1000.0 / steps, self.net.device)
         return ms, dom, samples, warm_t
 
-    def roof(self, name, ms_list):
+    def roof(self, name, ms_list, traffic=True):
+        """`traffic`: PMC bytes from profiles/pmc_traffic.json, which holds the headline (C2)
+        configuration only -- sub-benchmarks pass False."""
         bound, work = kernel_work(name, self.arch, self.B * self.T)
         avg = float(np.mean(ms_list)) / 1000.0
         peak = FP32_MFMA_PEAK if bound == 'mfma' else HBM_PEAK
@@ -270,7 +275,8 @@ class TrainBench:
         return {'kernel': name, 'bound': bound, 'achieved': ach / 1e12 if bound == 'mfma' else ach / 1e9,
                 'peak': peak / 1e12 if bound == 'mfma' else peak / 1e9,
                 'unit': 'TFLOP/s' if bound == 'mfma' else 'GB/s', 'frac': ach / peak,
-                'avg_launch_us': avg * 1e6, 'work_per_launch': work, 'traffic': traffic_from_profiles(name)}
+                'avg_launch_us': avg * 1e6, 'work_per_launch': work,
+                'traffic': traffic_from_profiles(name) if traffic else None}
 
     def close(self):
         import torch
@@ -292,8 +298,8 @@ def sub_bench(arch_file, B, T, dp, steps, warmup, gc=None, backward=True, label=
            'value': dp.world * B * T / (ms / 1000.0), 'unit': 'audio samples/s', 'ms_per_step': ms,
            'steps': steps, 'warmup': warmup}
     if dom:
-        out['roofline'] = tb.roof(dom, samples[dom])
-        out['roofline_dilconv'] = tb.roof('layer_fwd', samples['layer_fwd'])
+        out['roofline'] = tb.roof(dom, samples[dom], traffic=False)
+        out['roofline_dilconv'] = tb.roof('layer_fwd', samples['layer_fwd'], traffic=False)
     tb.close()
     return out
 
@@ -303,7 +309,7 @@ def parse_args(argv=None):
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=8)
-    ap.add_argument('--arch', default=None, help='default: par/arch3.json at N=1 (C2), par/arch5.json at N>1 (C5)')
+    ap.add_argument('--arch', default=None, help='default: par/arch3.json (C2 per GPU); C5 (arch5) rides along')
     ap.add_argument('--batch', type=int, default=8, help='streams per GPU')
     ap.add_argument('--slice', type=int, default=4096)
     ap.add_argument('--probe', default='auto')
@@ -311,7 +317,7 @@ def parse_args(argv=None):
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--gc', type=int, default=None, help='--num-global-cond for GC archs')
     ap.add_argument('--no-gen', action='store_true')
-    ap.add_argument('--no-extras', action='store_true', help='N=1: skip the C1 / C4 / C5-per-GPU sub-benchmarks')
+    ap.add_argument('--no-extras', action='store_true', help='skip the C1 / C4 / C5 sub-benchmarks')
     ap.add_argument('--gen-seconds', type=float, default=3.0)
     ap.add_argument('--dry-run', action='store_true',
                     help='launcher + DP plumbing only, on the CPU over gloo (no GPU call): tests')
@@ -361,8 +367,7 @@ def dry_run(args):
     from lbwn import dist as lbdist
     from lbwn.arch import ParamLayout, load_arch
     dp = lbdist.init(device_type='cpu')
-    arch = load_arch(args.arch or os.path.join(ROOT, 'par', 'arch5.json' if dp.world > 1 else 'arch3.json'),
-                     num_global_cond=args.gc)
+    arch = load_arch(args.arch or os.path.join(ROOT, 'par', 'arch3.json'), num_global_cond=args.gc)
     n = ParamLayout(arch).n_total
 
     class _Net:
@@ -377,7 +382,7 @@ def dry_run(args):
     if dp.rank == 0:
         print(json.dumps({'dry_run': True, 'world_size': dp.world, 'backend': torch.distributed.get_backend()
                           if dp.enabled else None, 'grad_floats': n, 'reduce_ok': ok, 'reduce_ms': ms,
-                          'arch': os.path.basename(args.arch or ('arch5.json' if dp.world > 1 else 'arch3.json')),
+                          'arch': os.path.basename(args.arch or 'arch3.json'),
                           'batch_per_gpu': args.batch}), flush=True)
     if dp.enabled:
         torch.distributed.destroy_process_group()
@@ -401,15 +406,15 @@ def main(argv=None):
     from lbwn.arch import load_arch
     dp = lbdist.init()          # one process per GPU; RCCL when WORLD_SIZE > 1
     rank = dp.rank
-    arch_file = args.arch or os.path.join(ROOT, 'par', 'arch3.json' if world == 1 else 'arch5.json')
+    arch_file = args.arch or os.path.join(ROOT, 'par', 'arch3.json')
     arch = load_arch(arch_file, num_global_cond=args.gc)
     B, T = args.batch, args.slice
     tb = TrainBench(arch, B, T, dp)
     net = tb.net
     ms, dom, samples, warm_t = tb.run(args.steps, args.warmup, probes=CANDS, probe_mode=args.probe)
     value = world * B * T / (ms / 1000.0)
-    cid = 'C2' if world == 1 and os.path.basename(arch_file) == 'arch3.json' else (
-        'C5' if os.path.basename(arch_file) == 'arch5.json' else 'custom')
+    cid = {'arch3.json': 'C2' + (' per GPU' if world > 1 else ''),
+           'arch5.json': 'C5' if B == 8 and world > 1 else 'arch5'}.get(os.path.basename(arch_file), 'custom')
     name = os.path.basename(arch_file)
     out = {
         'metric': 'audio samples/sec: train fwd+bwd & cached autoregressive gen, 1/2/4/8 GPU',
@@ -450,6 +455,10 @@ def main(argv=None):
         if not args.no_cpu_baseline:
             out['c1']['cpu_baseline'] = cpu_baseline(load_arch(par('arch1.json')), args.cpu_seconds * 0.5, B=2,
                                                      T=512, backward=False, label='arch1')
+    if world > 1 and not args.no_extras and args.arch is None:
+        out['c5'] = sub_bench(os.path.join(ROOT, 'par', 'arch5.json'), 8, 4096, dp, 10, 3,
+                              label='C5: arch5, B=8 per GPU x %d GPUs = global B=%d, T=4096, DP over RCCL '
+                                    '(one-GPU reference: the N=1 line\'s c5_per_gpu)' % (world, 8 * world))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(arch, args.cpu_seconds)
     if rank == 0:

@@ -288,7 +288,7 @@ def test_dp_checkpoint_gathers_per_rank_save(tmp_path):
 def test_bench_self_launch_dry_run():
     """`bench.py --gpus 2` outside torch.distributed.run spawns its own ranks (children,
     no exec) and the DP plumbing reduces through lbwn.dist over gloo; --dry-run stops
-    before any GPU call.  N>1 defaults to C5 (arch5, 8 streams per GPU)."""
+    before any GPU call."""
     import json as _json
     import subprocess
     env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK')}
@@ -299,4 +299,4 @@ def test_bench_self_launch_dry_run():
     assert len(lines) == 1, r.stdout
     d = _json.loads(lines[0])
     assert d['world_size'] == 2 and d['backend'] == 'gloo' and d['reduce_ok']
-    assert d['arch'] == 'arch5.json' and d['batch_per_gpu'] == 8
+    assert d['arch'] == 'arch3.json' and d['batch_per_gpu'] == 8
