@@ -39,6 +39,10 @@ struct lbwn_plan {
   bool dskip_main = true;        // dSKIP after the chain on the main stream at full rate (else aux, lean)
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // second side stream after the backward chain: the HBM-bound slab reduction and dPRE scatter
+  // run beside the MFMA-bound dSKIP on the main stream instead of in front of it
+  hipStream_t aux2 = nullptr;
+  hipEvent_t ev_chain = nullptr, ev_join2 = nullptr;
   size_t oSPLIT_AUX = 0;
   // Weights pre-split into bf16 planes once per step for the bf16-split GEMMs (gemm.hip):
   // [W3_SKIP_F] SKIPcat as skip-fwd B, [W3_POST1_F] POST1 as post1-fwd B, [W3_POST2_F] POST2 as
@@ -47,6 +51,9 @@ struct lbwn_plan {
   size_t oW3[6] = {0, 0, 0, 0, 0, 0};
   ~lbwn_plan() {
     if (aux) (void)hipStreamDestroy(aux);
+    if (aux2) (void)hipStreamDestroy(aux2);
+    if (ev_chain) (void)hipEventDestroy(ev_chain);
+    if (ev_join2) (void)hipEventDestroy(ev_join2);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
   }
@@ -329,6 +336,9 @@ int ensure_device(lbwn_plan* p) {
     LBWN_HIP(hipStreamCreateWithPriority(&p->aux, hipStreamNonBlocking, least));
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
+    LBWN_HIP(hipStreamCreateWithPriority(&p->aux2, hipStreamNonBlocking, greatest));
+    LBWN_HIP(hipEventCreateWithFlags(&p->ev_chain, hipEventDisableTiming));
+    LBWN_HIP(hipEventCreateWithFlags(&p->ev_join2, hipEventDisableTiming));
   }
   return 0;
 }
@@ -714,13 +724,24 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     Probe(p, st, "layer_bwd");
     if ((e = lbwn_chain_bwd_launch(c, st))) return e;
     Probe::end(p, st, "layer_bwd");
+    // slab reduction + dPRE on the second side stream (HBM-bound, beside dSKIP's MFMA work)
+    hipStream_t rst = st;
+    if (p->aux2) {
+      rst = p->aux2;
+      LBWN_HIP(hipEventRecord(p->ev_chain, st));
+      LBWN_HIP(hipStreamWaitEvent(rst, p->ev_chain, 0));
+    }
     lbwn_layer_red_args r;
     r.slab = SLABS; r.nparts = ntiles; r.stride = sstr; r.Cr = Cr; r.Cd = Cd;
     r.dsig = G->sig; r.dgate = G->gate; r.dres = G->res;
     r.dbsig = G->sig_b; r.dbgate = G->gate_b; r.dbres = G->res_b;
-    Probe(p, st, "layer_reduce");
-    if ((e = lbwn_layer_reduce_all_launch(r, L, (long)ntiles * sstr, st))) return e;
-    Probe::end(p, st, "layer_reduce");
+    Probe(p, rst, "layer_reduce");
+    if ((e = lbwn_layer_reduce_all_launch(r, L, (long)ntiles * sstr, rst))) return e;
+    Probe::end(p, rst, "layer_reduce");
+    if ((e = lbwn_pre_grad_launch(wav_q, at<float>(ws, p->oGA[0]), at<float>(ws, p->oGC0[0]), 1, B, T, Cr, Q, G->pre,
+                                  G->pre_b, at<float>(ws, p->oSPLIT2), rst)))
+      return e;
+    if (p->aux2) LBWN_HIP(hipEventRecord(p->ev_join2, rst));
   } else {
       for (int l = L - 1; l >= 0; --l) {
       lbwn_layer_args a = layer_base(p, P, WPK, ids, l);
@@ -750,9 +771,11 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   if ((e = cond_backward(p, P, G, ws, mel, st))) return e;
   if (p->dskip_main && (e = dskip(st, false, SPL))) return e;
   // dx_0 = (g + dcur) + shift(dprev) formed inside the scatter; dPRE = onehot(q)ᵀ·dx_0, dPRE_BIAS = Σ dx_0
-  if ((e = lbwn_pre_grad_launch(wav_q, at<float>(ws, p->oGA[0]), at<float>(ws, p->oGC0[0]), 1, B, T, Cr, Q, G->pre,
-                                G->pre_b, at<float>(ws, p->oSPLIT2), st)))
+  // (the chain path enqueued it on the second side stream above)
+  if (!p->chain && (e = lbwn_pre_grad_launch(wav_q, at<float>(ws, p->oGA[0]), at<float>(ws, p->oGC0[0]), 1, B, T,
+                                             Cr, Q, G->pre, G->pre_b, at<float>(ws, p->oSPLIT2), st)))
     return e;
   if (p->overlap) LBWN_HIP(hipStreamWaitEvent(st, p->ev_join, 0));
+  if (p->chain && p->aux2) LBWN_HIP(hipStreamWaitEvent(st, p->ev_join2, 0));
   return 0;
 }

@@ -89,6 +89,14 @@ LBWN_DEV int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+// Work item of this block over the whole (tiles × split-K) grid (grid = dim3(tiles, 1, splits)),
+// k-split-major: one XCD runs every output tile of its k-slices together, so each slice's rows
+// of both operands come from HBM into ONE L2 (per-z remapping spread a slice over all eight:
+// ~3.4x the algorithmic bytes on dSKIP/dPOST1, profiles/pmc_traffic.json r01).
+LBWN_DEV int gemm_work() { return xcd_remap(blockIdx.x + gridDim.x * blockIdx.z, gridDim.x * gridDim.z); }
+LBWN_DEV int gemm_tile() { return gemm_work() % gridDim.x; }
+LBWN_DEV int gemm_split() { return gemm_work() / gridDim.x; }
+
 // Block tile BMT × BNT, 4 waves as 2 × 2, each wave (BMT/2) × (BNT/2) = MI × NI MFMA tiles.
 // 128×128 tiles: four blocks (16 waves) per CU, i.e. at most 128 VGPRs; every register
 // above that costs a wave per SIMD, and the k-loop needs that occupancy to hide its LDS reads
@@ -104,9 +112,9 @@ __global__ __launch_bounds__(NT, (BMT * BNT > 128 * 128) ? 2 : 4) void gemm_f32_
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
-  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int t = gemm_tile();
   const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
-  const int kz0 = blockIdx.z * g.k_per_split;
+  const int kz0 = gemm_split() * g.k_per_split;
   const int kz1 = min(g.K, kz0 + g.k_per_split);
   const int ntiles = (kz1 - kz0 + BK - 1) / BK;
 
@@ -159,7 +167,7 @@ __global__ __launch_bounds__(NT, (BMT * BNT > 128 * 128) ? 2 : 4) void gemm_f32_
   // any is used (a load under a per-row branch is waited for on its own: one memory round trip
   // per element, from HBM in the training step), then out-of-range rows / columns are skipped.
   const int h = lane >> 5, ci = lane & 31;
-  float* C = g.C + (long)blockIdx.z * g.split_stride;
+  float* C = g.C + (long)gemm_split() * g.split_stride;
   const bool raw = g.split_stride != 0;
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
@@ -371,7 +379,7 @@ template <int MI>
 LBWN_DEV void x3_epilogue_rows(const lbwn_gemm_args& g, floatx16 (&acc)[MI][2], int m0, int n0, int wm, int wn,
                                int lane) {
   const int h = lane >> 5, ci = lane & 31;
-  float* C = g.C + (long)blockIdx.z * g.split_stride;
+  float* C = g.C + (long)gemm_split() * g.split_stride;
   const bool raw = g.split_stride != 0;
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
@@ -423,9 +431,9 @@ __global__ __launch_bounds__(128 * WM, (WM == 2 && STAGES == 1) ? X3_OCC : 1) vo
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
-  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int t = gemm_tile();
   const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
-  const int kz0 = blockIdx.z * g.k_per_split;
+  const int kz0 = gemm_split() * g.k_per_split;
   const int kz1 = min(g.K, kz0 + g.k_per_split);
   const int ntiles = (kz1 - kz0 + X3_BK - 1) / X3_BK;
 
