@@ -22,6 +22,9 @@ struct lbwn_plan {
   // workspace carving (byte offsets)
   size_t oX, oZ, oS, oR2, oLOG, oDH, oDS, oDZ, oGA[2], oGC0[2], oSLAB, oSPLIT, oSPLIT2, oCOLS,
       oHEADP, oBSUM, oWPK, oWPKX, oFLAGS, oSTATUS, oOCG, oCTRACE;
+  // bf16-split backward chain: σ(v_gate) rows from the forward chain [L][M][32], backward images
+  size_t oSG = 0, oWPKB = 0;
+  bool fwd_x3 = false;            // the last forward wrote SG (X3 chain)
   int ctrace_blk = -1;            // LBWN_CHAIN_TRACE=<block>: chain cycle stamps (debug)
   size_t oGCTAB, oGCD, oGCPART, oLCACT[8], oCOND, oDVALL, oLCCAT, oDLCCAT, oDLC[2];
   int split_dlc, split_up[8];
@@ -240,6 +243,7 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   const char* nc = getenv("LBWN_NO_CHAIN");
   p->chain = p->Cr == 32 && p->Cd == 32 && !(nc && nc[0] == '1');
   p->oOCG = p->chain ? carve(cur, sizeof(float) * (size_t)L * M * 32) : 0;
+  p->oSG = p->chain ? carve(cur, sizeof(float) * (size_t)L * M * 32) : 0;
   const char* ov = getenv("LBWN_OVERLAP");
   p->overlap = p->chain && !(ov && ov[0] == '0');
   // dSKIP after the chain on the main stream at full rate (default): with the backward chain at
@@ -278,6 +282,7 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->oBSUM = carve(cur, sizeof(float) * (size_t)p->Cs);
   p->oWPK = carve(cur, sizeof(float) * (size_t)L * lbwn_layer_image_floats());
   p->oWPKX = carve(cur, 2 * (size_t)L * lbwn_layer_image_x3_elems());
+  p->oWPKB = carve(cur, sizeof(float) * (size_t)L * lbwn_layer_image_bx3_floats());
   p->total = cur;
   *out = p;
   return 0;
@@ -505,6 +510,10 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
       (e = lbwn_pack_layers_x3_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b,
                                       at<unsigned short>(ws, p->oWPKX), L, Cr, Cd, st)))
     return e;
+  // ... and the backward chain's split images (dx weights + f32 residual image)
+  if (x3 && p->chain &&
+      (e = lbwn_pack_layers_bx3_launch(P->sig, P->gate, P->res, at<float>(ws, p->oWPKB), L, Cr, Cd, st)))
+    return e;
   if (x3) {
     const float* wsrc[6] = {P->skip, P->post1, P->post2, P->post2, P->post1, P->skip};
     const float* jw[6];
@@ -532,6 +541,8 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     memset(&c, 0, sizeof(c));
     c.X = X; c.xls = p->x_layer_stride; c.Z = Z; c.ldz = ldz; c.wpack = WPK; c.ids = ids;
     c.wpack_x3 = x3 ? at<unsigned short>(ws, p->oWPKX) : nullptr;
+    if (x3 && p->oSG) { c.SG = at<float>(ws, p->oSG); c.sgls = M * 32; }
+    p->fwd_x3 = c.SG != nullptr;
     c.gc_tab = cd.gc_tab; c.gc_ld = cd.gc_ld; c.cond = cd.cond; c.ldcond = cd.ldcond;
     c.flags = at<unsigned>(ws, p->oFLAGS); c.status = at<unsigned>(ws, p->oSTATUS);
     if (p->ctrace_blk >= 0) { c.trace = at<long long>(ws, p->oCTRACE); c.trace_blk = p->ctrace_blk; }
@@ -653,46 +664,43 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     if (nj && (e = lbwn_colsum_multi_launch(nj, cx, cld, cn, cout, cacc, (int)M, COLS, st))) return e;
     if (G->skip_b && (e = lbwn_bcast_rows_launch(G->skip_b, L, Cs, st))) return e;
   }
-  // weight gradients of the head and skip GEMMs: beside the layer chain (aux stream) or here
-  hipStream_t ws_st = st;
-  float* WSPL = SPL;
-  auto wgemm = [&](const lbwn_gemm_args& a, int split) {
-    return p->overlap ? lbwn_gemm_launch_lean(a, 0, 0, split, WSPL, ws_st) : lbwn_gemm_launch(a, 0, 0, split, WSPL, ws_st);
-  };
-  if (p->overlap) {
-    ws_st = p->aux;
-    WSPL = at<float>(ws, p->oSPLIT_AUX);
-    LBWN_HIP(hipEventRecord(p->ev_fork, st));
-    LBWN_HIP(hipStreamWaitEvent(ws_st, p->ev_fork, 0));
-  }
-  // dPOST2 = R2ᵀ·dlogits, db2 = Σ dlogits.  (Kept on the aux stream: moving it to the main
-  // stream at full rate measured slower, 3.83 vs 3.68 ms: the lean GEMMs get ~25 TF beside the
-  // chain at one wave per SIMD, so the aux stream mostly runs after the chain either way.)
-  g = gemm0();
-  g.A = R2; g.lda = Cp; g.B = LOG; g.ldb = Q; g.C = G->post2; g.ldc = Q; g.M = Cp; g.N = Q; g.K = (int)M;
-  Probe(p, ws_st, "dpost2");
-  if ((e = wgemm(g, p->split_post2))) return e;
-  Probe::end(p, ws_st, "dpost2");
-  // dPOST1 = relu(S)ᵀ·dH1, db1 = Σ dH1
-  g = gemm0();
-  g.A = S; g.lda = Cs; g.relu_a = 1; g.B = DH; g.ldb = Cp; g.C = G->post1; g.ldc = Cp; g.M = Cs; g.N = Cp;
-  g.K = (int)M;
-  Probe(p, ws_st, "dpost1");
-  if ((e = wgemm(g, p->split_post1))) return e;
-  Probe::end(p, ws_st, "dpost1");
-  // dSKIPcat = Zcatᵀ·dS; every layer's SKIP_BIAS gets the same Σ dS
-  auto dskip = [&](hipStream_t s2, bool lean, float* spl) -> int {
+  // weight gradients of the head and skip GEMMs (dPOST2, dPOST1; dSKIP unless on the main
+  // stream).  With the chain they go to the aux stream AFTER the chain launch, forked on the
+  // chain's completion: a chain block takes a whole CU's LDS, so nothing runs beside it, and
+  // aux blocks dispatched before it would hold CUs its lock-step tiles wait for.  After the
+  // chain they share the chip with dSKIP (main) and the slab reduction (aux2) at full rate.
+  auto dskip = [&](hipStream_t s2, float* spl) -> int {
     int e2;
-    g = gemm0();
-    g.A = Z; g.lda = ldz; g.B = DS; g.ldb = Cs; g.C = G->skip; g.ldc = Cs; g.M = (int)ldz; g.N = Cs; g.K = (int)M;
+    lbwn_gemm_args gk = gemm0();
+    gk.A = Z; gk.lda = ldz; gk.B = DS; gk.ldb = Cs; gk.C = G->skip; gk.ldc = Cs; gk.M = (int)ldz; gk.N = Cs;
+    gk.K = (int)M;
     Probe(p, s2, "dskip");
-    if ((e2 = lean ? lbwn_gemm_launch_lean(g, 0, 0, p->split_skip, spl, s2)
-                   : lbwn_gemm_launch(g, 0, 0, p->split_skip, spl, s2))) return e2;
+    if ((e2 = lbwn_gemm_launch(gk, 0, 0, p->split_skip, spl, s2))) return e2;
     Probe::end(p, s2, "dskip");
     return 0;
   };
-  if (!p->dskip_main && (e = dskip(ws_st, p->overlap, WSPL))) return e;
-  if (p->overlap) LBWN_HIP(hipEventRecord(p->ev_join, ws_st));
+  auto aux_gemms = [&](hipStream_t ws_st, float* WSPL) -> int {
+    int e2;
+    // dPOST2 = R2ᵀ·dlogits (db2 = Σ dlogits: the column sums above)
+    lbwn_gemm_args gk = gemm0();
+    gk.A = R2; gk.lda = Cp; gk.B = LOG; gk.ldb = Q; gk.C = G->post2; gk.ldc = Q; gk.M = Cp; gk.N = Q; gk.K = (int)M;
+    Probe(p, ws_st, "dpost2");
+    if ((e2 = lbwn_gemm_launch(gk, 0, 0, p->split_post2, WSPL, ws_st))) return e2;
+    Probe::end(p, ws_st, "dpost2");
+    // dPOST1 = relu(S)ᵀ·dH1
+    gk = gemm0();
+    gk.A = S; gk.lda = Cs; gk.relu_a = 1; gk.B = DH; gk.ldb = Cp; gk.C = G->post1; gk.ldc = Cp; gk.M = Cs;
+    gk.N = Cp; gk.K = (int)M;
+    Probe(p, ws_st, "dpost1");
+    if ((e2 = lbwn_gemm_launch(gk, 0, 0, p->split_post1, WSPL, ws_st))) return e2;
+    Probe::end(p, ws_st, "dpost1");
+    if (!p->dskip_main && (e2 = dskip(ws_st, WSPL))) return e2;
+    return 0;
+  };
+  // LBWN_WG_AFTER=1: after the chain on the aux stream (above); default: here on the main stream
+  static const char* wga = getenv("LBWN_WG_AFTER");
+  const bool wg_after = p->overlap && wga && wga[0] == '1';
+  if (!wg_after && (e = aux_gemms(st, SPL))) return e;
   // residual stack in reverse (conditioning recomputed from the forward's GCTAB / COND)
   Cond cd;
   if (p->Ge > 0) {
@@ -714,6 +722,9 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     lbwn_chain_args c;
     memset(&c, 0, sizeof(c));
     c.X = X; c.xls = p->x_layer_stride; c.DZ = DZ; c.ldz = ldz; c.wpack = WPK; c.ids = ids;
+    if (p->fwd_x3 && lbwn_gemm_mode() == 1) {   // bf16-split backward: no gate recompute (SG)
+      c.Z = Z; c.SG = at<float>(ws, p->oSG); c.sgls = M * 32; c.bimg = at<float>(ws, p->oWPKB);
+    }
     c.slab = SLABS; c.ocg = at<float>(ws, p->oOCG); c.ocls = M * 32;
     c.gc_tab = cd.gc_tab; c.gc_ld = cd.gc_ld; c.cond = cd.cond; c.ldcond = cd.ldcond;
     c.gc_dtab = cd.gc_dtab; c.dv_out = cd.dv_out; c.lddv = cd.ldcond;
@@ -724,6 +735,12 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     Probe(p, st, "layer_bwd");
     if ((e = lbwn_chain_bwd_launch(c, st))) return e;
     Probe::end(p, st, "layer_bwd");
+    if (wg_after) {   // fork on the chain's completion: head/skip weight gradients on aux
+      LBWN_HIP(hipEventRecord(p->ev_fork, st));
+      LBWN_HIP(hipStreamWaitEvent(p->aux, p->ev_fork, 0));
+      if ((e = aux_gemms(p->aux, at<float>(ws, p->oSPLIT_AUX)))) return e;
+      LBWN_HIP(hipEventRecord(p->ev_join, p->aux));
+    }
     // slab reduction + dPRE on the second side stream (HBM-bound, beside dSKIP's MFMA work)
     hipStream_t rst = st;
     if (p->aux2) {
@@ -769,13 +786,13 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     if ((e = lbwn_layer_reduce_all_launch(r, L, (long)p->nblk * sstr, st))) return e;
   }
   if ((e = cond_backward(p, P, G, ws, mel, st))) return e;
-  if (p->dskip_main && (e = dskip(st, false, SPL))) return e;
+  if (p->dskip_main && (e = dskip(st, SPL))) return e;
   // dx_0 = (g + dcur) + shift(dprev) formed inside the scatter; dPRE = onehot(q)ᵀ·dx_0, dPRE_BIAS = Σ dx_0
   // (the chain path enqueued it on the second side stream above)
   if (!p->chain && (e = lbwn_pre_grad_launch(wav_q, at<float>(ws, p->oGA[0]), at<float>(ws, p->oGC0[0]), 1, B, T,
                                              Cr, Q, G->pre, G->pre_b, at<float>(ws, p->oSPLIT2), st)))
     return e;
-  if (p->overlap) LBWN_HIP(hipStreamWaitEvent(st, p->ev_join, 0));
+  if (wg_after) LBWN_HIP(hipStreamWaitEvent(st, p->ev_join, 0));
   if (p->chain && p->aux2) LBWN_HIP(hipStreamWaitEvent(st, p->ev_join2, 0));
   return 0;
 }

@@ -73,6 +73,10 @@ int lbwn_pack_layers_x3_launch(const float* sig, const float* gate, const float*
                                const float* res, const float* res_b, unsigned short* out, int L, int Cr, int Cd,
                                hipStream_t st);
 int lbwn_layer_image_floats();
+// backward split images (WD bf16 + Rs f32) for the bf16-split backward chain, floats per layer
+int lbwn_layer_image_bx3_floats();
+int lbwn_pack_layers_bx3_launch(const float* sig, const float* gate, const float* res, float* out, int L, int Cr,
+                                int Cd, hipStream_t st);
 int lbwn_layer_nblocks(int B, int T);
 int lbwn_layer_bwd_grid(int B, int T);   // = number of slab partials per layer
 int lbwn_pack_layers_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
@@ -99,6 +103,10 @@ struct lbwn_chain_args {
   float* dx0_a; float* dx0_c;  // layer 0's dx parts [B·T][32]
   long long* trace = nullptr;  // debug: cycle stamps of block trace_blk, [L][16] (LBWN_CHAIN_TRACE)
   int trace_blk = 0;
+  // bf16-split backward (chain_bwd_x3_kernel): σ(v_gate) rows [L][M][32] written by the X3
+  // forward chain (layer stride sgls floats), and the backward images (lbwn_pack_layers_bx3)
+  float* SG = nullptr; long sgls = 0;
+  const float* bimg = nullptr;
 };
 int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st);
 int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st);

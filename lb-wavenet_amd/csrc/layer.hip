@@ -376,6 +376,7 @@ struct ChainFK {
   int B, T, H, L, nbl, Cd;
   long long* trace; int trace_blk;   // debug stamps (null in production)
   const unsigned short* ximg;        // L split images (XIMG_US bf16 each): the bf16-split form
+  float* SG; long sgls;              // σ(v_gate) rows [L][M][32] for chain_bwd_x3_kernel, or null
 };
 
 // GC + LC term of layer l for this lane's position, in acc layout: cv[q] = sig channels
@@ -605,9 +606,12 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
       const float* xp = (r >= d) ? cur + (r - d) * XS : HALO + r * XS;
       if (X3) conv_half_x3(xp, (const unsigned short*)Wl, pi, h, acc_s, acc_g);
       else conv_half(xp, Wl, pi, h, acc_s, acc_g);
-      floatx16 z;
+      floatx16 z, sgv;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) z[q] = tanhf_(acc_s[q]) * sigmoidf_(acc_g[q]);
+      for (int q = 0; q < 16; ++q) {
+        sgv[q] = sigmoidf_(acc_g[q]);
+        z[q] = tanhf_(acc_s[q]) * sgv[q];
+      }
       FSTAMP(4);
       if (l + 1 < a.L) {
         // 6. residual: x_{l+1} = x_l + br + RES·z → LDS (next layer's rows) and HBM (sc1)
@@ -660,6 +664,7 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
       __syncthreads();
       if (tid == 0 && l + 1 < a.L) publish_flag(a.flags + tile, (unsigned)(l + 1));
       if (valid) store_rows16(a.Z + m * a.ldz + (long)l * a.Cd, z, a.Cd, h);  // skip GEMM input
+      if (X3 && a.SG && valid) store_rows16(a.SG + (long)l * a.sgls + m * 32, sgv, 32, h);
       FSTAMP(6);
       // 9. image of layer l+2 into IMG[l&1] (everyone is past this layer's reads of it)
       if (l + 2 < a.L) {
@@ -749,6 +754,8 @@ struct ChainBK {
   unsigned* flags; unsigned* status;
   int B, T, H, L, nbl, Cd;
   long long* trace; int trace_blk;   // debug stamps (null in production)
+  // bf16-split form (chain_bwd_x3_kernel): z rows (row stride lddz), σ rows [L][M][32], images
+  const float* Zf; const float* SG; long sgls; const float* bimg;
 };
 
 // dv rows of wave w's 32 positions (DV, position-major) scatter-added into the GC gradient
@@ -1139,6 +1146,423 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
   }
 }
 
+// ---- backward chain on the bf16 cores (the X3 arithmetic of DESIGN §4.0) -----------------------
+// Same tile walk, hand-off and slab layout as chain_bwd_kernel; what changes:
+//  * no gate recompute: the X3 forward chain stores σ(v_gate) (SG [L][M][32]) beside z (Zcat),
+//    so tanh = z·σ⁻¹ and dv come from two row loads (prefetched a layer ahead) instead of a
+//    second 64-channel conv;
+//  * dx = W·dv (K = 64) and the weight gradients dSIG/dGATE = Xᵀ·DV (K = 128 positions) and
+//    dRES = Zᵀ·G run on v_mfma_f32_32x32x16_bf16 / 16x16x32 from exact 3-term splits (six
+//    products); dz = dZ + RES·g (16 f32 MFMAs) stays on v_mfma_f32_32x32x2_f32;
+//  * this layer's x rows (both taps) and z rows are LDS-DMA'd into unpadded tiles during the
+//    G build, the next layer's weight image right after the publish; DV, G and OC live in
+//    32-float rows with an XOR swizzle of the 4-float groups (swz) so that both the own-row
+//    b128 writes and the column reads of the weight-gradient products are conflict-free.
+// Backward image per layer: WD[tap][in][plane][kk] (bf16, row XW_ROW) with kk = 16s+8h+j holding
+// out channel o = 32(s>>1) + 16(s&1) + 8(j>>2) + 4h + (j&3) (sig 0..31 | gate 32..63): the k order
+// of the dv registers used as the B operand; then Rs f32 [c][XS] for the dz product.  Padded to
+// a whole number of 1-KiB DMA pieces.
+constexpr int BD_US = 2 * 32 * XW_ROW;
+constexpr int BIMG_F = (BD_US / 2 + 32 * XS + 255) / 256 * 256;   // 7680 floats
+constexpr int CBX_LDS = BIMG_F + 7 * LP * 32 + 8 * 96;            // IMG | Xp Xc ZT | DVs DVg G OC | part
+static_assert(CBX_LDS * 4 + 16 <= 160 * 1024, "chain bwd x3 LDS");
+
+__global__ void pack_layers_bx3_kernel(const float* sig, const float* gate, const float* res, float* out, int Cr,
+                                       int Cd) {
+  const int l = blockIdx.x;
+  const float* ws = sig + (long)l * 2 * Cr * Cd;
+  const float* wg = gate + (long)l * 2 * Cr * Cd;
+  const float* wr = res + (long)l * Cd * Cr;
+  float* img = out + (long)l * BIMG_F;
+  unsigned short* wd = (unsigned short*)img;
+  for (int e = threadIdx.x; e < 2 * 32 * 32; e += blockDim.x) {
+    const int tap = e >> 10, in = (e >> 5) & 31, kk = 2 * (e & 31);
+    floatx2 x = {0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k2 = kk + u, s2 = k2 >> 4, hh = (k2 >> 3) & 1, j = k2 & 7;
+      const int o = 32 * (s2 >> 1) + 16 * (s2 & 1) + 8 * (j >> 2) + 4 * hh + (j & 3), oc = o & 31;
+      const float* wk = o < 32 ? ws : wg;
+      if (in < Cr && oc < Cd) x[u] = wk[(tap * Cr + in) * Cd + oc];
+    }
+    unsigned hi, mi, lo;
+    split2(x, hi, mi, lo);
+    unsigned short* row = wd + (tap * 32 + in) * XW_ROW + kk;
+    *(unsigned*)(row) = hi;
+    *(unsigned*)(row + 64) = mi;
+    *(unsigned*)(row + 128) = lo;
+  }
+  float* rs = img + BD_US / 2;
+  for (int e = threadIdx.x; e < 32 * XS; e += blockDim.x) {
+    const int c = e / XS, o = e % XS;
+    rs[e] = (c < Cd && o < Cr) ? wr[c * Cr + o] : 0.f;
+  }
+  for (int e = BD_US / 2 + 32 * XS + threadIdx.x; e < BIMG_F; e += blockDim.x) img[e] = 0.f;
+}
+
+// element (p, c) of a 32-float-row tile with the 4-float groups XOR-permuted by row pair
+LBWN_DEV int swz(int p, int c) { return p * 32 + (c ^ (((p >> 1) & 7) << 2)); }
+
+// acc += A·B over one 32-deep k-step of v_mfma_f32_16x16x32_bf16 from split fragments
+LBWN_DEV floatx4 mfma16_x3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+  return acc;
+}
+
+// gc_scatter over the swizzled dv planes
+LBWN_DEV void gc_scatter_x3(float* gtab, long ld, const int* ids_b, const float* DVs, const float* DVg, int t0, int T,
+                            int w, int lane, int Cd, int uni_id) {
+  const int tw0 = t0 + 32 * w;
+  const int nv = min(32, T - tw0);
+  if (nv <= 0) return;
+  const int* idw = ids_b + tw0;
+  int id0 = uni_id;
+  if (id0 < 0) {
+    id0 = idw[0];
+    bool uni = true;
+    for (int p = 1; p < nv; ++p) uni &= (idw[p] == id0);
+    if (!uni) id0 = -1;
+  }
+  const int o = lane, oc = o & 31;
+  const float* pl = o < 32 ? DVs : DVg;
+  if (oc >= Cd) return;
+  const int col = o < 32 ? oc : Cd + oc;
+  if (id0 >= 0) {
+    float s = 0.f;
+    for (int p = 0; p < nv; ++p) s += pl[swz(32 * w + p, oc)];
+    atomicAdd(gtab + (long)id0 * ld + col, s);
+  } else {
+    for (int p = 0; p < nv; ++p) atomicAdd(gtab + (long)idw[p] * ld + col, pl[swz(32 * w + p, oc)]);
+  }
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// One LDS-DMA piece (global_load_lds_dwordx4: 64 lanes × 16 B from per-lane addresses to
+// lds_dst + 16·lane) issued from inline asm, so the compiler neither knows the LDS it writes (no
+// conservative vmcnt(0) before every later LDS access) nor counts it: the kernel lands these
+// pieces itself with an explicit vmcnt(0) drain + barrier before their first reader.
+LBWN_DEV void dma16(const void* g, float* lds_dst) {
+  const unsigned base =
+      __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)lds_dst);
+  unsigned saved;   // m0 is reserved by the compiler: saved and restored around the piece
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(saved)
+               : "s"(base), "v"(g)
+               : "memory");
+}
+
+__global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
+  __shared__ __attribute__((aligned(16))) float sm[CBX_LDS];
+  __shared__ int s_fail;
+  float* IMG = sm;
+  const unsigned short* WD = (const unsigned short*)IMG;
+  const float* Rs = IMG + BD_US / 2;
+  float* Xp = IMG + BIMG_F;
+  float* Xc = Xp + LP * 32;
+  float* ZT = Xc + LP * 32;
+  float* DVs = ZT + LP * 32;
+  float* DVg = DVs + LP * 32;
+  float* G = DVg + LP * 32;
+  float* OC = G + LP * 32;
+  float* part = OC + LP * 32;   // [8][96] bias partials
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int pi = lane & 31, h = lane >> 5;
+  const int r = 32 * w + pi;
+  const int tps = (a.T + LP - 1) / LP, ntiles = a.B * tps;
+  const int oc_bytes = (int)std::min<long>(a.ocls * 4, 0x7fffffffL);
+  if (tid == 0) s_fail = 0;
+  for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
+    const int tile = ntiles - 1 - it;
+    const int b = tile / tps, tt = tile % tps, t0 = tt * LP;
+    const int t = t0 + r;
+    const bool valid = t < a.T;
+    const long mb = (long)b * a.T, m = mb + t, mc = mb + min(t, a.T - 1);
+    const long sb = (long)b * (a.H + a.T) * 32;
+    const int myid = (a.gc_tab && valid) ? a.ids[m] : 0;
+    const int wave_id = __shfl(myid, 0);
+    const bool wave_uni = __all(!valid || myid == wave_id);
+    // per-layer rows of this lane's position: dZ, z, σ (issued a layer ahead)
+    floatx4 dzr[4], zr[4], sgr[4];
+    auto load_regs = [&](int l) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        dzr[q] = *(const floatx4*)(a.DZ + mc * a.lddz + (long)l * 32 + 8 * q + 4 * h);
+        zr[q] = *(const floatx4*)(a.Zf + mc * a.lddz + (long)l * 32 + 8 * q + 4 * h);
+        sgr[q] = *(const floatx4*)(a.SG + (long)l * a.sgls + mc * 32 + 8 * q + 4 * h);
+      }
+    };
+    auto dma_image = [&](int l) {
+      const float* src = a.bimg + (long)l * BIMG_F + lane * 4;
+      for (int i = w; i < BIMG_F / 256; i += 4) dma16(src + i * 256, IMG + i * 256);
+    };
+    __syncthreads();  // previous tile's LDS use done
+    dma_image(a.L - 1);
+    load_regs(a.L - 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    floatx16 oa;  // out_a of layer l+1, own row
+#pragma unroll
+    for (int q = 0; q < 16; ++q) oa[q] = 0.f;
+    const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && it == (int)blockIdx.x;
+#define XSTAMP(i) if (trc) a.trace[16 * l + (i)] = clock64()
+    for (int l = a.L - 1; l >= 0; --l) {
+      XSTAMP(0);
+      const int d = 1 << (l % a.nbl);
+      const int dn = (l + 1 < a.L) ? 1 << ((l + 1) % a.nbl) : 0;
+      // 1. G = dx_{l+1} rows: out_c0_{l+1}[t + dn] (own OC / the producer's published rows) + out_a
+      floatx4 gl[4], go[4];
+      if (dn) {
+        const int ptt = tt + max(1, dn / LP);
+        if (ptt < tps) {
+          if (tid == 0 && !s_fail) {
+            if (!wait_flag_ge(a.flags + (long)b * tps + ptt, (unsigned)(a.L - l - 1), a.status, 2u)) s_fail = 1;
+          }
+          __syncthreads();
+        }
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)(l + 1) * a.ocls, (short)0, oc_bytes, BUF_DW3);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = tid + 256 * i, row = e >> 3, c4 = (e & 7) * 4, sr = row + dn;
+          const int ts = min(t0 + sr, a.T - 1);
+          gl[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
+          go[i] = *(const floatx4*)(OC + swz(min(sr, LP - 1), c4));
+        }
+      }
+      if (dn) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = tid + 256 * i, row = e >> 3, c4 = (e & 7) * 4, sr = row + dn, ts = t0 + sr;
+          floatx4 v = sr < LP ? go[i] : gl[i];
+          if (ts >= a.T) v = floatx4{0.f, 0.f, 0.f, 0.f};
+          *(floatx4*)(G + swz(row, c4)) = v;
+        }
+        // lands this wave's part of the weight image (LDS-DMA'd after the last layer's publish)
+        // and the prefetched rows; the barrier then covers every wave's part
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      // the prefetched rows are consumed here, in the compiler's view, so that it has no load of
+      // its own outstanding behind the DMA pieces below (its waits would count them)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(dzr[q]), "v"(zr[q]), "v"(sgr[q]));
+      // this layer's x rows (x[t-d] | x[t]) and z rows by LDS-DMA into Xp / Xc / ZT (free since the
+      // last layer's end barrier; first read after this layer's publish drain + barrier)
+      {
+        const float* xl = a.X + (long)l * a.xls + sb;
+        const int c4 = (lane & 7) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = 32 * w + 8 * j + (lane >> 3);
+          const int trow = min(t0 + row, a.T - 1);
+          dma16(xl + (long)(a.H + trow - d) * 32 + c4, Xp + (32 * w + 8 * j) * 32);
+          dma16(xl + (long)(a.H + trow) * 32 + c4, Xc + (32 * w + 8 * j) * 32);
+          dma16(a.Zf + (mb + trow) * a.lddz + (long)l * 32 + c4, ZT + (32 * w + 8 * j) * 32);
+        }
+      }
+      XSTAMP(1);
+      floatx16 gv;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {   // own row: + out_a (the top layer writes it, g = 0)
+        float* gp = G + swz(r, 8 * q + 4 * h);
+        floatx4 v = dn ? *(const floatx4*)gp : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[j] += oa[4 * q + j]; gv[4 * q + j] = v[j]; }
+        *(floatx4*)gp = v;
+      }
+      // 2. dz = dZ + RES·g  (f32 MFMA)
+      floatx16 dz;
+      {
+        floatx4 rx[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          rx[q] = *(const floatx4*)(Rs + pi * XS + 8 * q + 4 * h);
+          floatx4 v = dzr[q];
+          if (!valid) v = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dz[4 * q + j] = v[j];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dz = mfma32(rx[q][j], gv[4 * q + j], dz);
+      }
+      // 3. dv from z and σ: tanh = z/σ (σ = 0 only where dv is 0 anyway)
+      floatx16 dvs, dvg;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float zz = zr[q >> 2][q & 3], sg = sgr[q >> 2][q & 3];
+        const float th = sg > 1e-30f ? zz * __builtin_amdgcn_rcpf(sg) : 0.f;
+        dvs[q] = dz[q] * sg * (1.f - th * th);
+        dvg[q] = dz[q] * zz * (1.f - sg);
+      }
+      {
+        float* dvo = (a.dv_out && valid) ? a.dv_out + m * a.lddv + (long)l * 64 : nullptr;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const floatx4 vs = floatx4{dvs[4 * q], dvs[4 * q + 1], dvs[4 * q + 2], dvs[4 * q + 3]};
+          const floatx4 vg = floatx4{dvg[4 * q], dvg[4 * q + 1], dvg[4 * q + 2], dvg[4 * q + 3]};
+          *(floatx4*)(DVs + swz(r, 8 * q + 4 * h)) = vs;
+          *(floatx4*)(DVg + swz(r, 8 * q + 4 * h)) = vg;
+          if (dvo) {
+            *(floatx4*)(dvo + 8 * q + 4 * h) = vs;
+            *(floatx4*)(dvo + 32 + 8 * q + 4 * h) = vg;
+          }
+        }
+      }
+      XSTAMP(2);
+      // 4. dx on the bf16 cores: out_a = g + W1·dv, out_c0 = W0·dv  (k-steps 0,1: sig; 2,3: gate)
+      floatx16 acc_a = gv, acc_c;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc_c[q] = 0.f;
+      {
+        // fragments of k-step s+1 read while step s's MFMAs issue
+        bf16x8 fa[2][3], fc[2][3];
+        auto loadf = [&](int s2, int buf) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            fa[buf][p] = *(const bf16x8*)(WD + (32 + pi) * XW_ROW + 64 * p + 16 * s2 + 8 * h);
+            fc[buf][p] = *(const bf16x8*)(WD + pi * XW_ROW + 64 * p + 16 * s2 + 8 * h);
+          }
+        };
+        loadf(0, 0);
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const int o8 = 8 * (s2 & 1), cb = s2 & 1;
+          if (s2 + 1 < 4) loadf(s2 + 1, cb ^ 1);
+          bf16x8 bx[3];
+          if (s2 < 2)
+            split8(floatx4{dvs[o8], dvs[o8 + 1], dvs[o8 + 2], dvs[o8 + 3]},
+                   floatx4{dvs[o8 + 4], dvs[o8 + 5], dvs[o8 + 6], dvs[o8 + 7]}, bx);
+          else
+            split8(floatx4{dvg[o8], dvg[o8 + 1], dvg[o8 + 2], dvg[o8 + 3]},
+                   floatx4{dvg[o8 + 4], dvg[o8 + 5], dvg[o8 + 6], dvg[o8 + 7]}, bx);
+          acc_a = mfma_x3(fa[cb], bx, acc_a);
+          acc_c = mfma_x3(fc[cb], bx, acc_c);
+        }
+      }
+      {
+        const __amdgpu_buffer_rsrc_t rw =
+            __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)l * a.ocls, (short)0, oc_bytes, BUF_DW3);
+        const bool pub = l > 0 && valid && r < min(d, LP);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const floatx4 v = floatx4{acc_c[4 * q], acc_c[4 * q + 1], acc_c[4 * q + 2], acc_c[4 * q + 3]};
+          *(floatx4*)(OC + swz(r, 8 * q + 4 * h)) = v;
+          if (pub) __builtin_amdgcn_raw_buffer_store_b128(v, rw, (int)((m * 32 + 8 * q + 4 * h) * 4), 0, 16);
+        }
+      }
+      if (l == 0 && valid) {
+        store_rows16(a.dx0_a + m * 32, acc_a, 32, h);
+        store_rows16(a.dx0_c + m * 32, acc_c, 32, h);
+      }
+      oa = acc_a;
+      XSTAMP(3);
+      // 5. publish out_c0_l; the drain also lands this layer's x / z DMA
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // DV, G, Xp/Xc/ZT complete; the weight image is dead
+      if (tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
+      if (l > 0) {
+        dma_image(l - 1);
+        load_regs(l - 1);
+      }
+      if (a.gc_dtab)
+        gc_scatter_x3(a.gc_dtab + (long)l * 64, a.gc_ld, a.ids + mb, DVs, DVg, t0, a.T, w, lane, 32,
+                      wave_uni ? wave_id : -1);
+      XSTAMP(4);
+      // 6. dSIG / dGATE tile w: A[i=in][k=pos] = X[pos][in], B[k][j=o] = DV[pos][o]; positions of
+      //    k-step s: p = 16s + 2j + h (the lane halves read rows of opposite parity: no conflicts)
+      floatx16 accW;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) accW[q] = 0.f;
+      {
+        const float* X = (w & 1) ? Xc : Xp;
+        const float* DP = (w >> 1) ? DVg : DVs;
+        float xa[2][8], da[2][8];
+        auto loadk = [&](int s2, int buf) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int p = 16 * s2 + 2 * j + h;
+            xa[buf][j] = X[p * 32 + pi];
+            da[buf][j] = DP[swz(p, pi)];
+          }
+        };
+        loadk(0, 0);
+#pragma unroll
+        for (int s2 = 0; s2 < LP / 16; ++s2) {
+          const int cb = s2 & 1;
+          if (s2 + 1 < LP / 16) loadk(s2 + 1, cb ^ 1);
+          bf16x8 fx[3], fd[3];
+          split8(floatx4{xa[cb][0], xa[cb][1], xa[cb][2], xa[cb][3]},
+                 floatx4{xa[cb][4], xa[cb][5], xa[cb][6], xa[cb][7]}, fx);
+          split8(floatx4{da[cb][0], da[cb][1], da[cb][2], da[cb][3]},
+                 floatx4{da[cb][4], da[cb][5], da[cb][6], da[cb][7]}, fd);
+          accW = mfma_x3(fx, fd, accW);
+        }
+      }
+      XSTAMP(5);
+      // 7. dRES quarter of wave w (16x16: z channels 16(w>>1).., res out 16(w&1)..) over all LP
+      //    positions: A[i=c][k=pos] = z[pos][c], B[k][j=o] = g[pos][o]; k = 8·(lane>>4) + j
+      floatx4 accR = {0.f, 0.f, 0.f, 0.f};
+      {
+        const int i16 = lane & 15, kg = lane >> 4, cz = 16 * (w >> 1) + i16, og = 16 * (w & 1) + i16;
+        float za[8], ga[8];
+#pragma unroll
+        for (int s2 = 0; s2 < LP / 32; ++s2) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int p = 32 * s2 + 4 * j + kg;
+            za[j] = ZT[p * 32 + cz];
+            ga[j] = G[swz(p, og)];
+          }
+          bf16x8 fz[3], fg[3];
+          split8(floatx4{za[0], za[1], za[2], za[3]}, floatx4{za[4], za[5], za[6], za[7]}, fz);
+          split8(floatx4{ga[0], ga[1], ga[2], ga[3]}, floatx4{ga[4], ga[5], ga[6], ga[7]}, fg);
+          accR = mfma16_x3(fz, fg, accR);
+        }
+      }
+      // 8. bias partials (column sums of DV and G) and the slab
+      float* slab = a.slab + ((long)l * ntiles + tile) * SLAB;
+      if (tid < 128) {
+        const int c4 = (tid & 15) * 4, pc = tid >> 4;
+        const float* pl = c4 < 32 ? DVs : DVg;
+        floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < 16; ++p) s4 += *(const floatx4*)(pl + swz(pc * 16 + p, c4 & 31));
+        *(floatx4*)(part + pc * 96 + c4) = s4;
+      } else if (tid < 192) {
+        const int c4 = ((tid - 128) & 7) * 4, pc = (tid - 128) >> 3;
+        floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < 16; ++p) s4 += *(const floatx4*)(G + swz(pc * 16 + p, c4));
+        *(floatx4*)(part + pc * 96 + 64 + c4) = s4;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) slab[w * 1024 + acc_row(q, h) * 32 + pi] = accW[q];
+      {
+        const int i16 = lane & 15, kg = lane >> 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) slab[4096 + (16 * (w >> 1) + 4 * kg + q) * 32 + 16 * (w & 1) + i16] = accR[q];
+      }
+      __syncthreads();   // every read of Xp/Xc/ZT/DV/G of this layer is done; part complete
+      if (tid < 96) {
+        float s1 = 0.f;
+#pragma unroll
+        for (int pc = 0; pc < 8; ++pc) s1 += part[pc * 96 + tid];
+        slab[5120 + tid] = s1;
+      }
+      XSTAMP(6);
+    }
+#undef XSTAMP
+  }
+}
+
 // Sum every layer's slab partials: grid (column groups, L).
 __global__ __launch_bounds__(256) void layer_reduce_all_kernel(RedK a, long slab_layer, long dsig_l, long dres_l,
                                                                long db_l) {
@@ -1423,6 +1847,14 @@ BwdK to_bwd(const lbwn_layer_args& a) {
 int lbwn_layer_slab_stride() { return SLAB; }
 int lbwn_layer_image_floats() { return WIMG; }
 int lbwn_layer_image_x3_elems() { return XIMG_US; }
+int lbwn_layer_image_bx3_floats() { return BIMG_F; }
+int lbwn_pack_layers_bx3_launch(const float* sig, const float* gate, const float* res, float* out, int L, int Cr,
+                                int Cd, hipStream_t st) {
+  LBWN_REQUIRE(Cr <= 32 && Cd <= 32 && (((uintptr_t)out) & 15) == 0, "pack_layers_bx3: bad arguments");
+  pack_layers_bx3_kernel<<<L, 256, 0, st>>>(sig, gate, res, out, Cr, Cd);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
 
 int lbwn_pack_layers_x3_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                                const float* res, const float* res_b, unsigned short* out, int L, int Cr, int Cd,
@@ -1490,6 +1922,7 @@ int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   k.B = c.B; k.T = c.T; k.H = c.H; k.L = c.L; k.nbl = c.nbl; k.Cd = c.Cd;
   k.trace = c.trace; k.trace_blk = c.trace_blk;
   k.ximg = c.wpack_x3;
+  k.SG = c.SG; k.sgls = c.sgls;
   LBWN_REQUIRE(!c.wpack_x3 || (((uintptr_t)c.wpack_x3) & 15) == 0, "chain fwd: split images not 16-B aligned");
   const int tps = (c.T + LP - 1) / LP;
   LBWN_REQUIRE((unsigned*)c.status + 4 == c.flags, "chain: status word must head the flag block");
@@ -1513,11 +1946,16 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   k.flags = c.flags; k.status = c.status;
   k.B = c.B; k.T = c.T; k.H = c.H; k.L = c.L; k.nbl = c.nbl; k.Cd = c.Cd;
   k.trace = c.trace ? c.trace + 16L * c.L : nullptr; k.trace_blk = c.trace_blk;
+  k.Zf = c.Z; k.SG = c.SG; k.sgls = c.sgls; k.bimg = c.bimg;
+  const bool x3 = c.bimg && c.SG && c.Z;
+  if (x3) LBWN_REQUIRE((((uintptr_t)c.bimg) & 15) == 0 && (((uintptr_t)c.SG) & 15) == 0 && (c.ldz & 3) == 0,
+                       "chain bwd x3: misaligned images / rows");
   const int tps = (c.T + LP - 1) / LP;
   LBWN_REQUIRE((unsigned*)c.status + 4 == c.flags, "chain: status word must head the flag block");
   // hand-off flags only: the status word is sticky for the whole step
   LBWN_HIP(hipMemsetAsync(c.flags, 0, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st));
-  chain_bwd_kernel<<<c.grid, 256, 0, st>>>(k);
+  if (x3) chain_bwd_x3_kernel<<<c.grid, 256, 0, st>>>(k);
+  else chain_bwd_kernel<<<c.grid, 256, 0, st>>>(k);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
