@@ -1353,19 +1353,16 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(dzr[q]), "v"(zr[q]), "v"(sgr[q]));
       // this layer's x rows (x[t-d] | x[t]) and z rows by LDS-DMA into Xp / Xc / ZT (free since the
-      // last layer's end barrier; first read after this layer's publish drain + barrier)
-      {
-        const float* xl = a.X + (long)l * a.xls + sb;
-        const int c4 = (lane & 7) * 4;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int row = 32 * w + 8 * j + (lane >> 3);
-          const int trow = min(t0 + row, a.T - 1);
-          dma16(xl + (long)(a.H + trow - d) * 32 + c4, Xp + (32 * w + 8 * j) * 32);
-          dma16(xl + (long)(a.H + trow) * 32 + c4, Xc + (32 * w + 8 * j) * 32);
-          dma16(a.Zf + (mb + trow) * a.lddz + (long)l * 32 + c4, ZT + (32 * w + 8 * j) * 32);
-        }
-      }
+      // last layer's end barrier; first read after this layer's publish drain + barrier); the
+      // pieces are issued between the dz MFMAs (row group j: 3 pieces)
+      const float* xl = a.X + (long)l * a.xls + sb;
+      auto dma_rows3 = [&](int j) {
+        const int row = 32 * w + 8 * j + (lane >> 3), c4 = (lane & 7) * 4;
+        const int trow = min(t0 + row, a.T - 1);
+        dma16(xl + (long)(a.H + trow - d) * 32 + c4, Xp + (32 * w + 8 * j) * 32);
+        dma16(xl + (long)(a.H + trow) * 32 + c4, Xc + (32 * w + 8 * j) * 32);
+        dma16(a.Zf + (mb + trow) * a.lddz + (long)l * 32 + c4, ZT + (32 * w + 8 * j) * 32);
+      };
       XSTAMP(1);
       floatx16 gv;
 #pragma unroll
@@ -1389,9 +1386,11 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
           for (int j = 0; j < 4; ++j) dz[4 * q + j] = v[j];
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < 4; ++q) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) dz = mfma32(rx[q][j], gv[4 * q + j], dz);
+          dma_rows3(q);
+        }
       }
       // 3. dv from z and σ: tanh = z/σ (σ = 0 only where dv is 0 anyway)
       floatx16 dvs, dvg;
@@ -1464,14 +1463,12 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
       }
       oa = acc_a;
       XSTAMP(3);
-      // 5. publish out_c0_l; the drain also lands this layer's x / z DMA
+      // 5. publish out_c0_l (the drain also lands this layer's x / z DMA pieces)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // DV, G, Xp/Xc/ZT complete; the weight image is dead
       if (tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
-      if (l > 0) {
-        dma_image(l - 1);
-        load_regs(l - 1);
-      }
+      // the next layer's weight image and rows are issued between the dSIG MFMAs below (landed
+      // by the next layer's G build: vmcnt(0) + barrier)
       if (a.gc_dtab)
         gc_scatter_x3(a.gc_dtab + (long)l * 64, a.gc_ld, a.ids + mb, DVs, DVg, t0, a.T, w, lane, 32,
                       wave_uni ? wave_id : -1);
@@ -1494,10 +1491,16 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
           }
         };
         loadk(0, 0);
+        const float* isrc = a.bimg + (long)(l > 0 ? l - 1 : 0) * BIMG_F + lane * 4;
 #pragma unroll
         for (int s2 = 0; s2 < LP / 16; ++s2) {
           const int cb = s2 & 1;
           if (s2 + 1 < LP / 16) loadk(s2 + 1, cb ^ 1);
+          if (l > 0) {
+            const int pc = w + 4 * s2;   // image pieces w, w+4, ... (30 of 1 KiB)
+            if (pc < BIMG_F / 256) dma16(isrc + pc * 256, IMG + pc * 256);
+            if (s2 == 2) load_regs(l - 1);
+          }
           bf16x8 fx[3], fd[3];
           split8(floatx4{xa[cb][0], xa[cb][1], xa[cb][2], xa[cb][3]},
                  floatx4{xa[cb][4], xa[cb][5], xa[cb][6], xa[cb][7]}, fx);
@@ -1508,23 +1511,23 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
       }
       XSTAMP(5);
       // 7. dRES quarter of wave w (16x16: z channels 16(w>>1).., res out 16(w&1)..) over all LP
-      //    positions: A[i=c][k=pos] = z[pos][c], B[k][j=o] = g[pos][o]; k = 8·(lane>>4) + j
+      //    positions on v_mfma_f32_16x16x4_f32 (K = 2048 flop/pos is too little to pay for
+      //    splitting): A[i=c][k=pos] = z[pos][c], B[k][j=o] = g[pos][o]; k = lane>>4
       floatx4 accR = {0.f, 0.f, 0.f, 0.f};
       {
         const int i16 = lane & 15, kg = lane >> 4, cz = 16 * (w >> 1) + i16, og = 16 * (w & 1) + i16;
-        float za[8], ga[8];
 #pragma unroll
-        for (int s2 = 0; s2 < LP / 32; ++s2) {
+        for (int c8 = 0; c8 < LP / 32; ++c8) {
+          float za[8], ga[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const int p = 32 * s2 + 4 * j + kg;
+            const int p = 32 * c8 + 4 * j + kg;
             za[j] = ZT[p * 32 + cz];
             ga[j] = G[swz(p, og)];
           }
-          bf16x8 fz[3], fg[3];
-          split8(floatx4{za[0], za[1], za[2], za[3]}, floatx4{za[4], za[5], za[6], za[7]}, fz);
-          split8(floatx4{ga[0], ga[1], ga[2], ga[3]}, floatx4{ga[4], ga[5], ga[6], ga[7]}, fg);
-          accR = mfma16_x3(fz, fg, accR);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) accR = __builtin_amdgcn_mfma_f32_16x16x4f32(za[j], ga[j], accR, 0, 0, 0);
         }
       }
       // 8. bias partials (column sums of DV and G) and the slab

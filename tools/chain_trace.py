@@ -39,6 +39,19 @@ for n, m in zip(fnames, fmed):
 print('  layer total                %6d  = %.2f us at 2.4 GHz' % (ftot, ftot / 2400.0))
 print('    of which residual + stores %6d, next own tap %6d' % (np.median(fw[1:-2, 8] - fw[1:-2, 4]), np.median(fw[1:-2, 5] - fw[1:-2, 8])))
 tr = allr[1]   # backward
+if net.lib.lbwn_gemm_get_mode() == 1:      # chain_bwd_x3_kernel: XSTAMP(0..6)
+    names = ['G wait+build, DMA issue', 'dz,dv,DV', 'dx MFMA + OC', 'publish+img DMA+prefetch', 'dSIG MFMA',
+             'dRES+bias+slab+bar']
+    order = list(range(L - 1, -1, -1))
+    seg = np.diff(tr[:, :7], axis=1)[order]
+    med = np.median(seg[1:-1], axis=0)
+    per = np.median(np.diff(tr[order, 0]))          # layer start to next layer start
+    print('chain_bwd_x3 block %s, per layer (median cycles over layers):' % BLK)
+    for n, m in zip(names, med):
+        print('  %-26s %6d  (%4.1f %%)' % (n, m, 100.0 * m / per))
+    print('  layer period               %6d  = %.2f us at 2.4 GHz;  whole tile %d cycles' %
+          (per, per / 2400.0, tr[0, 6] - tr[L - 1, 0]))
+    sys.exit(0)
 names = ['stage x/dz + bar', 'gate recompute', 'G wait+build', 'dz,dv,DV', 'dx MFMA+OC', 'publish bar',
          'dSIG MFMA', 'bar+dRES', 'bias+slab+bar', 'image+bar']
 seg = np.diff(tr[:, :11], axis=1)          # [L][10]
