@@ -72,3 +72,38 @@ def test_train_resume_generate(tmp_path, capsys):
     assert np.all(np.abs(wav) <= 1.03)
     for i in range(3):
         assert os.path.exists(tmp_path / 'out' / ('gen.i%d.wav' % i))
+
+
+def test_generate_teacher_wav_end_to_end(tmp_path):
+    """generate.py --teacher-wav (generate.py:52-59, imodel.py:44-46, :260): a 16-bit 8 kHz
+    wav is read, cut (--teacher-start/--teacher-duration), resampled to 16 kHz, µ-law encoded
+    on the GPU (TF-fp32 form, ops.py:4-9) and forces the inputs; the draws must equal the
+    oracle's generation forced by the oracle's own encoding of the same samples."""
+    import generate
+    from scipy.io import wavfile
+    from lbwn.arch import normalize_arch
+    from lbwn.tmodel import WaveNetTrain
+    from oracle import wavenet_ref as R
+    arch = normalize_arch(dict(n_blocks=2, n_block_layers=4, n_quant=256, n_res=32, n_dil=32, n_skip=64, n_post=32,
+                               n_gc_embed=0, n_gc_category=0, use_bias=True))
+    af = tmp_path / 'arch.json'
+    af.write_text(json.dumps(arch))
+    tr = WaveNetTrain(**arch, batch_sz=1, l2_factor=0.0, print_interval=0, ckpt_path=str(tmp_path / 'g.net'))
+    tr.init_vars(5, bias_scale=0.2)
+    with torch.no_grad():
+        tr.vars['POST2'].mul_(4.0)
+    tr.save(1)
+    t = np.arange(800) / 8000.0
+    x = 0.6 * np.sin(2 * np.pi * 220 * t) + 0.2 * np.sin(2 * np.pi * 530 * t)
+    wavfile.write(str(tmp_path / 'teach.wav'), 8000, (x * 32767).astype(np.int16))
+    wav = generate.main(['--teacher-wav', str(tmp_path / 'teach.wav'), '--teacher-start', '0.01',
+                         '--teacher-duration', '0.05', '--gen-seconds', '0.02', '--batch-size', '2',
+                         '--chunk-size', '100', str(af), str(tmp_path / 'g.net-1'), str(tmp_path / 'out')])
+    teacher = generate.load_teacher(str(tmp_path / 'teach.wav'), 16000, 0.01, 0.05)
+    assert teacher.shape == (800,)                     # 0.05 s at 8 kHz, resampled to 16 kHz
+    n = int((0.02 + teacher.shape[0] / 16000) * 16000)
+    assert wav.shape == (2, (n // 100) * 100)
+    P = {k: v.cpu().double().numpy() for k, v in tr.vars.items()}
+    tq = R.mu_encode_tf32(teacher, 256)
+    _, w_ref = R.generate(arch, P, 2, n, seed=0, teacher_q=tq)
+    np.testing.assert_allclose(wav, w_ref[:, :wav.shape[1]], rtol=1e-6, atol=1e-6)
