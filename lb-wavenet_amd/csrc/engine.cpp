@@ -25,6 +25,12 @@ struct lbwn_plan {
   // bf16-split backward chain: σ(v_gate) rows from the forward chain [L][M][32], backward images
   size_t oSG = 0, oWPKB = 0;
   bool fwd_x3 = false;            // the last forward wrote SG (X3 chain)
+  // n_skip / n_post that are not multiples of 4 (par/arch2.json: 8 / 6) run padded to the
+  // next multiple of 4 inside the plan (Cs, Cp): the head weights are copied into zero-padded
+  // images each step (zero rows/columns keep the padded channels at exactly 0 through relu and
+  // every product) and the head gradients are copied back out of padded buffers.
+  int Cs_ref = 0, Cp_ref = 0;
+  size_t oPADP = 0, oPADG = 0;
   int ctrace_blk = -1;            // LBWN_CHAIN_TRACE=<block>: chain cycle stamps (debug)
   size_t oGCTAB, oGCD, oGCPART, oLCACT[8], oCOND, oDVALL, oLCCAT, oDLCCAT, oDLC[2];
   int split_dlc, split_up[8];
@@ -35,11 +41,12 @@ struct lbwn_plan {
   int nblk;                      // layer-bwd blocks = slab partials per layer
   bool chain = false;            // persistent layer-chain kernels (n_res = n_dil = 32)
   int chain_grid = 0;            // resident blocks for the chain (set on first use)
-  // Backward overlap: the weight-gradient GEMMs (dPOST2, dPOST1, dSKIP) do not feed the
-  // layer chain, which keeps the MFMA pipes ~1/3 busy at one wave per SIMD, so they run on
-  // a low-priority stream in lean-LDS form (21 KB beside the chain's 131 KB block).
+  // Backward side streams (chain plans): the head weight gradients (dPOST2, dPOST1) run on the
+  // main stream before the chain (LBWN_WG_AFTER=1: on `aux` after it); dSKIP follows the chain
+  // on the main stream while `aux2` runs the HBM-bound slab reduction and dPRE beside it.  A
+  // chain block takes a whole CU's LDS, so nothing co-resides with the chains.
   bool overlap = false;
-  bool dskip_main = true;        // dSKIP after the chain on the main stream at full rate (else aux, lean)
+  bool dskip_main = true;        // dSKIP after the chain on the main stream (LBWN_DSKIP_MAIN=0: with the aux GEMMs)
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // second side stream after the backward chain: the HBM-bound slab reduction and dPRE scatter
@@ -129,7 +136,9 @@ size_t carve(size_t& cur, size_t bytes) {
 int pick_split(int M, int N, long K) {
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
   const long slab_cap = std::max<long>(1, (64L << 20) / (4L * M * N));
-  const long s = std::max<long>(1, std::min<long>({1024 / tiles, K / 512, slab_cap}));
+  // one wave of 2-blocks-per-CU slots (512): more splits only add slab traffic (dPOST1 at 64
+  // splits wrote 67 MB of slabs for 134 MB of operands, profiles/pmc_traffic.json)
+  const long s = std::max<long>(1, std::min<long>({512 / tiles, K / 512, slab_cap}));
   return (int)s;
 }
 
@@ -138,6 +147,75 @@ T* at(void* ws, size_t off) {
   return reinterpret_cast<T*>(static_cast<char*>(ws) + off);
 }
 
+}  // namespace
+
+namespace {
+// padded head images: SKIP [L·Cd][Cs] | SKIP_BIAS [L][Cs] | POST1 [Cs][Cp] | POST1_BIAS [Cp] | POST2 [Cp][Q]
+size_t head_pad_floats(const lbwn_plan* p) {
+  const size_t L = p->L, Cd = p->Cd, Cs = p->Cs, Cp = p->Cp, Q = p->Q;
+  return L * Cd * Cs + L * Cs + Cs * Cp + Cp + Cp * Q + 5 * 64;
+}
+struct HeadPad { float *skip, *skip_b, *post1, *post1_b, *post2; };
+HeadPad head_pad_layout(const lbwn_plan* p, float* base) {
+  auto up = [](size_t n) { return (n + 63) / 64 * 64; };   // 256-B aligned pieces
+  const size_t L = p->L, Cd = p->Cd, Cs = p->Cs, Cp = p->Cp, Q = p->Q;
+  HeadPad h;
+  h.skip = base;
+  h.skip_b = h.skip + up(L * Cd * Cs);
+  h.post1 = h.skip_b + up(L * Cs);
+  h.post1_b = h.post1 + up(Cs * Cp);
+  h.post2 = h.post1_b + up(Cp);
+  return h;
+}
+// rows x cols (reference widths) <-> the same block at padded row widths
+int copy2d(float* dst, size_t dld, const float* src, size_t sld, size_t cols, size_t rows, hipStream_t st) {
+  if (!src || !dst) return 0;
+  LBWN_HIP(hipMemcpy2DAsync(dst, dld * 4, src, sld * 4, cols * 4, rows, hipMemcpyDeviceToDevice, st));
+  return 0;
+}
+// P (reference layouts) -> zero-padded images; returns the params struct pointing at them
+int head_pad_params(const lbwn_plan* p, const lbwn_params* P, void* ws, lbwn_params& out, bool copy,
+                    hipStream_t st) {
+  out = *P;
+  if (!p->oPADP) return 0;
+  HeadPad h = head_pad_layout(p, reinterpret_cast<float*>(static_cast<char*>(ws) + p->oPADP));
+  const size_t L = p->L, Cd = p->Cd, Cs = p->Cs, Cp = p->Cp, Q = p->Q, cs = p->Cs_ref, cp = p->Cp_ref;
+  if (copy) {
+    LBWN_HIP(hipMemsetAsync(h.skip, 0, sizeof(float) * head_pad_floats(p), st));
+    int e;
+    if ((e = copy2d(h.skip, Cs, P->skip, cs, cs, L * Cd, st))) return e;
+    if ((e = copy2d(h.skip_b, Cs, P->skip_b, cs, cs, L, st))) return e;
+    if ((e = copy2d(h.post1, Cp, P->post1, cp, cp, cs, st))) return e;
+    if ((e = copy2d(h.post1_b, Cp, P->post1_b, cp, cp, 1, st))) return e;
+    if ((e = copy2d(h.post2, Q, P->post2, Q, Q, cp, st))) return e;
+  }
+  out.skip = h.skip; out.post1 = h.post1; out.post2 = h.post2;
+  if (P->skip_b) out.skip_b = h.skip_b;
+  if (P->post1_b) out.post1_b = h.post1_b;
+  return 0;
+}
+// gradient struct writing into the padded buffers, and the copy back into the caller's
+int head_pad_grads(const lbwn_plan* p, const lbwn_params* G, void* ws, lbwn_params& out) {
+  out = *G;
+  if (!p->oPADG) return 0;
+  HeadPad h = head_pad_layout(p, reinterpret_cast<float*>(static_cast<char*>(ws) + p->oPADG));
+  out.skip = h.skip; out.post1 = h.post1; out.post2 = h.post2;
+  if (G->skip_b) out.skip_b = h.skip_b;
+  if (G->post1_b) out.post1_b = h.post1_b;
+  return 0;
+}
+int head_unpad_grads(const lbwn_plan* p, const lbwn_params* G, void* ws, hipStream_t st) {
+  if (!p->oPADG) return 0;
+  HeadPad h = head_pad_layout(p, reinterpret_cast<float*>(static_cast<char*>(ws) + p->oPADG));
+  const size_t L = p->L, Cd = p->Cd, Cs = p->Cs, Cp = p->Cp, Q = p->Q, cs = p->Cs_ref, cp = p->Cp_ref;
+  int e;
+  if ((e = copy2d(G->skip, cs, h.skip, Cs, cs, L * Cd, st))) return e;
+  if (G->skip_b && (e = copy2d(G->skip_b, cs, h.skip_b, Cs, cs, L, st))) return e;
+  if ((e = copy2d(G->post1, cp, h.post1, Cp, cp, cs, st))) return e;
+  if (G->post1_b && (e = copy2d(G->post1_b, cp, h.post1_b, Cp, cp, 1, st))) return e;
+  if ((e = copy2d(G->post2, Q, h.post2, Q, Q, cp, st))) return e;
+  return 0;
+}
 }  // namespace
 
 int lbwn_recep_field_sz(const lbwn_arch* a) {
@@ -151,10 +229,9 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   LBWN_REQUIRE(a->n_blocks >= 1 && a->n_block_layers >= 1 && a->n_block_layers <= 16, "plan: bad depth");
   LBWN_REQUIRE(a->n_res >= 1 && a->n_res <= 32 && a->n_dil >= 1 && a->n_dil <= 32,
                "plan: n_res/n_dil must be in [1, 32] (got %d/%d)", a->n_res, a->n_dil);
-  LBWN_REQUIRE(a->n_skip % 4 == 0 && a->n_post % 4 == 0 && a->n_quant % 4 == 0,
-               "plan: n_skip/n_post/n_quant must be multiples of 4");
+  LBWN_REQUIRE(a->n_skip >= 1 && a->n_post >= 1 && a->n_quant % 4 == 0,
+               "plan: n_skip/n_post >= 1 and n_quant a multiple of 4 required");
   LBWN_REQUIRE(B >= 1 && T >= 2, "plan: batch_sz >= 1 and slice_sz >= 2 required");
-  LBWN_REQUIRE(a->n_res % 4 == 0 && a->n_dil % 4 == 0, "plan: n_res/n_dil must be multiples of 4");
   LBWN_REQUIRE(a->n_gc_embed >= 0 && (a->n_gc_embed == 0 || a->n_gc_category >= 1),
                "plan: GC needs n_gc_category >= 1");
   LBWN_REQUIRE(a->n_gc_embed <= 32, "plan: n_gc_embed > 32 not supported");
@@ -178,8 +255,10 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->H = 1 << (a->n_block_layers - 1);
   p->Cr = a->n_res;
   p->Cd = a->n_dil;
-  p->Cs = a->n_skip;
-  p->Cp = a->n_post;
+  p->Cs_ref = a->n_skip;
+  p->Cp_ref = a->n_post;
+  p->Cs = (a->n_skip + 3) / 4 * 4;
+  p->Cp = (a->n_post + 3) / 4 * 4;
   p->Q = a->n_quant;
   p->M = (long)B * T;
   p->Ge = a->n_gc_embed;
@@ -283,6 +362,11 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->oWPK = carve(cur, sizeof(float) * (size_t)L * lbwn_layer_image_floats());
   p->oWPKX = carve(cur, 2 * (size_t)L * lbwn_layer_image_x3_elems());
   p->oWPKB = carve(cur, sizeof(float) * (size_t)L * lbwn_layer_image_bx3_floats());
+  if (p->Cs != p->Cs_ref || p->Cp != p->Cp_ref) {
+    const size_t hp = head_pad_floats(p);
+    p->oPADP = carve(cur, sizeof(float) * hp);
+    p->oPADG = carve(cur, sizeof(float) * hp);
+  }
   p->total = cur;
   *out = p;
   return 0;
@@ -488,6 +572,9 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   int e;
   if ((e = ensure_device(p))) return e;
   LBWN_REQUIRE(p->Lo == 0 || mel, "train_forward: LC arch needs the mel input");
+  lbwn_params Ppad;
+  if ((e = head_pad_params(p, P, ws, Ppad, true, st))) return e;
+  P = &Ppad;
   // the sticky status word (chain spin timeouts OR their codes in) lives for one step:
   // zeroed here, read by the host after the step (lbwn_plan_tensor "status")
   LBWN_HIP(hipMemsetAsync(at<char>(ws, p->oSTATUS), 0, 16, st));
@@ -613,6 +700,13 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   hipStream_t st = (hipStream_t)stream;
   int e;
   if ((e = ensure_device(p))) return e;
+  // padded head widths: the forward's padded images, gradients into padded buffers
+  const lbwn_params* Gref = G;
+  lbwn_params Ppad, Gpad;
+  if ((e = head_pad_params(p, P, ws, Ppad, false, st))) return e;
+  if ((e = head_pad_grads(p, G, ws, Gpad))) return e;
+  P = &Ppad;
+  G = &Gpad;
   const int L = p->L, B = p->B, T = p->T, Cr = p->Cr, Cd = p->Cd, Cs = p->Cs, Cp = p->Cp, Q = p->Q;
   const long M = p->M, ldz = (long)L * Cd;
   float* X = at<float>(ws, p->oX);
@@ -794,5 +888,6 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     return e;
   if (wg_after) LBWN_HIP(hipStreamWaitEvent(st, p->ev_join, 0));
   if (p->chain && p->aux2) LBWN_HIP(hipStreamWaitEvent(st, p->ev_join2, 0));
+  if ((e = head_unpad_grads(p, Gref, ws, st))) return e;
   return 0;
 }

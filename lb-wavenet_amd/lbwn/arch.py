@@ -140,7 +140,10 @@ class Entry:
 
 class ParamLayout:
     """Flat fp32 layout.  Region [0, n_weights): non-BIAS trainables (get the L2 term,
-    tmodel.py:250-261); [n_weights, n_total): biases.  Offsets are multiples of 4 floats."""
+    tmodel.py:250-261); [n_weights, n_total): biases.  Every kind (the per-layer arrays the
+    engine addresses as base + l·numel, and the single tensors) starts at a multiple of 4
+    floats; the layers of a kind are dense (no padding between them, e.g. RESIDUAL_BIAS
+    [n_res = 3] of par/arch2.json at stride 3)."""
 
     def __init__(self, arch):
         self.arch = arch
@@ -151,13 +154,17 @@ class ParamLayout:
         self.entries = OrderedDict()
         self._cur = 0
         self.kind_base = {}
+        self._kind_of = {}
 
         def add(name, shape, is_bias, cat, kind=None):
-            if kind is not None and kind not in self.kind_base:
-                self.kind_base[kind] = self._cur
+            if kind is None or kind not in self.kind_base:
+                self._cur = (self._cur + 3) // 4 * 4
+                if kind is not None:
+                    self.kind_base[kind] = self._cur
             e = Entry(name, shape, self._cur, is_bias, cat)
             self.entries[name] = e
-            self._cur += (e.numel + 3) // 4 * 4
+            self._kind_of[name] = kind
+            self._cur += e.numel
 
         def sfx(b, bl):
             return '_%d_%d' % (b, bl)
@@ -184,7 +191,7 @@ class ParamLayout:
                     add(cat.name + sfx(b, bl), [Lo, Cd], False, cat, kind)
         add('POST1', [Cs, Cp], False, ArchCat.POST1, 'post1')
         add('POST2', [Cp, Q], False, ArchCat.POST2, 'post2')
-        self.n_weights = self._cur
+        self.n_weights = self._cur = (self._cur + 3) // 4 * 4
         if ub:
             add('PRE_BIAS', [Cr], True, ArchCat.PRE, 'pre_b')
             for kind, cat in (('sig_b', ArchCat.SIGNAL), ('gate_b', ArchCat.GATE)):
@@ -196,14 +203,13 @@ class ParamLayout:
                 add('SKIP_BIAS' + sfx(b, bl), [Cs], True, ArchCat.SKIP, 'skip_b')
             add('POST1_BIAS', [Cp], True, ArchCat.POST1, 'post1_b')
             add('POST2_BIAS', [Q], True, ArchCat.POST2, 'post2_b')
-        self.n_total = self._cur
+        self.n_total = (self._cur + 3) // 4 * 4
         self._check_contiguity()
 
     def _check_contiguity(self):
         # per-layer kinds must be dense arrays over layers for (base, stride) addressing
-        for kind, cat_names in (('sig', 'SIGNAL_'), ('gate', 'GATE_'), ('res', 'RESIDUAL_'),
-                                ('skip', 'SKIP_')):
-            es = [e for e in self.entries.values() if e.name.startswith(cat_names) and not e.is_bias]
+        for kind in set(self.kind_base):
+            es = [e for e in self.entries.values() if self._kind_of.get(e.name) == kind]
             for i in range(1, len(es)):
                 assert es[i].offset == es[i - 1].offset + es[i - 1].numel, (kind, es[i].name)
 

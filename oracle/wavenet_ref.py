@@ -375,7 +375,8 @@ def loss_fcn(arch, P, logits, wav_q, ids, l2_factor):
     sum_xent = float((xent * mask).sum())
     mean = sum_xent / n_valid if n_valid else 0.0
     diffs = tgt.astype(np.int64) - np.argmax(lg, axis=2).astype(np.int64)
-    avg_diff = int(np.abs(diffs * mask).sum()) // (B * (T - 1))   # int32 reduce_mean
+    sum_absdiff = int(np.abs(diffs * mask).sum())
+    avg_diff = sum_absdiff // (B * (T - 1))   # int32 reduce_mean
     l2 = l2_loss(P)
     total = mean + l2_factor * l2
     dlog = np.zeros_like(logits)
@@ -385,7 +386,7 @@ def loss_fcn(arch, P, logits, wav_q, ids, l2_factor):
         np.put_along_axis(onehot, tgt[..., None], 1.0, axis=2)
         dlog[:, :-1, :] = (sm - onehot) * mask[..., None] / n_valid
     stats = dict(total=total, mean_xent=mean, l2=l2, avg_diff=avg_diff, n_valid=n_valid,
-                 sum_xent=sum_xent)
+                 sum_xent=sum_xent, sum_absdiff=sum_absdiff)
     return stats, dlog
 
 

@@ -46,3 +46,7 @@ def test_plan_rejects_bad_arch_without_gpu():
     assert lib.lbwn_plan_create(ctypes.byref(a), 8, 4096, ctypes.byref(h)) == 0
     assert lib.lbwn_plan_workspace_bytes(h) > 500 * 2 ** 20
     lib.lbwn_plan_destroy(h)
+    # par/arch2.json widths (n_res 3, n_dil 4, n_skip 8, n_post 6): accepted, head padded inside
+    a.n_res, a.n_dil, a.n_skip, a.n_post = 3, 4, 8, 6
+    assert lib.lbwn_plan_create(ctypes.byref(a), 2, 512, ctypes.byref(h)) == 0
+    lib.lbwn_plan_destroy(h)

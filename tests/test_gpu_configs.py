@@ -52,7 +52,14 @@ def _check_config(arch, B, T, seed=0, grads=True, z_identical=True):
     assert int(net.plan_tensor(T, 'status').view(torch.int32)[0]) == 0, 'chain hand-off timed out'
     stats = net.stats.cpu().numpy()
     assert int(stats[1]) == st['n_valid']
-    assert int(stats[2]) // (B * (T - 1)) == st['avg_diff']
+    # Σ|argmax diff|: exact except where the top two logits are within fp32 noise (narrow heads
+    # such as arch2's n_post 6 give near-flat logits): each such position may move by <= Q-1
+    lgv = lg[:, :-1]
+    srt = np.sort(lgv, axis=2)
+    amb = ((srt[..., -1] - srt[..., -2]) <= 1e-5 * max(1.0, np.abs(lgv).max())) & (ids[:, 1:] != 0)
+    assert abs(int(stats[2]) - st['sum_absdiff']) <= (arch['n_quant'] - 1) * int(amb.sum()), int(amb.sum())
+    if not amb.any():
+        assert int(stats[2]) // (B * (T - 1)) == st['avg_diff']
     np.testing.assert_allclose(stats[0] / st['n_valid'], st['mean_xent'], rtol=1e-5)
     for k, v in new_save.items():
         close(net.save_vars[k].cpu().numpy(), v, 1e-5, k)
@@ -120,3 +127,11 @@ def test_arch4_with_gc_override():
     """par/arch4.json lacks n_gc_category: -gc supplies it (train.py:77-80, :138-146)."""
     arch = _arch('arch4', gc=10)
     _check_config(arch, 2, 512, z_identical=False)
+
+
+def test_arch2_tiny_stack():
+    """par/arch2.json (n_res 3, n_dil 4, n_skip 8, n_post 6, GC 16 with -gc; par/arch2.json:5-8):
+    odd channel counts on the per-layer kernels, n_post 6 through the zero-padded head."""
+    arch = _arch('arch2', gc=10)
+    assert (arch['n_res'], arch['n_dil'], arch['n_skip'], arch['n_post']) == (3, 4, 8, 6)
+    _check_config(arch, 2, 512)

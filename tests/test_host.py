@@ -46,8 +46,14 @@ def test_normalize_shipped_arch_files(f):
     assert set(lay.entries) == set(shapes)
     for n, e in lay.entries.items():
         assert e.shape == shapes[n][0] and e.is_bias == shapes[n][2], n
-        assert e.offset % 4 == 0
         assert (e.offset < lay.n_weights) == (not e.is_bias)
+    assert all(o % 4 == 0 for o in lay.kind_base.values())
+    # per-layer kinds are dense (the engine addresses layer l at base + l·numel)
+    for kind, base in lay.kind_base.items():
+        es = sorted((e for n, e in lay.entries.items() if lay._kind_of[n] == kind), key=lambda e: e.offset)
+        assert es[0].offset == base
+        for a, b in zip(es, es[1:]):
+            assert b.offset == a.offset + a.numel, (kind, b.name)
 
 
 def test_arch_param_counts():

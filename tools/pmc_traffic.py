@@ -3,15 +3,16 @@ dispatch).  gfx950: FETCH_SIZE counts ½ of the bytes of wide coalesced reads, s
 hbm_bytes = (2·FETCH_SIZE + WRITE_SIZE)·1024 (MI355X_MICROARCH.md § HBM).  Dispatches are
 split into training steps at pack_layers_kernel and named in launch order: the chain
 kernels by name, the GEMMs by their position in engine.cpp's fixed enqueue sequence (arch
-without LC or GC: skip_fwd, post1_fwd, post2_fwd, then dh, ds, dz on the main stream and
-dpost2, dpost1, dskip on the aux stream; dispatch ids follow enqueue order)."""
+without LC or GC: skip_fwd, post1_fwd, post2_fwd, then dh, ds, dz, dpost2, dpost1 before the
+backward chain and dskip after it, all on the main stream; dispatch ids follow enqueue order)."""
 import csv
 import glob
 import json
 import sys
 
 GEMM_ORDER = ['skip_fwd', 'post1_fwd', 'post2_fwd', 'dh', 'ds', 'dz', 'dpost2', 'dpost1', 'dskip']
-NAMED = {'chain_fwd_kernel': 'layer_fwd', 'chain_bwd_kernel': 'layer_bwd', 'head_kernel': 'head',
+NAMED = {'chain_fwd_kernel': 'layer_fwd', 'chain_bwd_kernel': 'layer_bwd', 'chain_bwd_x3_kernel': 'layer_bwd',
+         'head_kernel': 'head',
          'layer_reduce_all_kernel': 'layer_reduce', 'pre_grad_part_kernel': 'dpre'}
 
 
@@ -41,7 +42,7 @@ def per_name(rows, skip_steps=8):
             for k, n in NAMED.items():
                 if k in name:
                     key = n
-            if 'gemm_f32_kernel' in name:
+            if 'gemm_f32_kernel' in name or 'gemm_x3_kernel' in name:
                 key = GEMM_ORDER[gi] if gi < len(GEMM_ORDER) else 'gemm%d' % gi
                 gi += 1
             if key:
