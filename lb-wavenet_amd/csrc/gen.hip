@@ -68,7 +68,7 @@ LBWN_DEV float sum_parts(const float* p, long stride, int n) {
 // l's pieces, and the compute waves' reads of slot l-1 retired, so the loaders refill it after
 // B1) and B2 (z of layer l written).  No global loads on the compute chain.
 constexpr int GI_W = 16 * 256;              // conv: [w 4][m 4][lane 64][4]  W[16kq+4m+j][32sg+8w+c]
-constexpr int GI_R = 4 * 256;               // residual: [w 4][lane 64][4] RES[4kp+j][8w+c]
+constexpr int GI_R = 4 * 256;               // residual: [h 2][q 4][c 32][4] RES[16h+4q+j][c]
 constexpr int GI_WR = GI_W + GI_R;          // 20 pieces of 1 KiB
 constexpr int GIMG = GI_WR + 192;           // global image: + conv bias [64] + residual bias [64] + zeros [64]
 constexpr int G_SLOT = GI_WR + 256;         // LDS slot: weights | bc [64] | br [64] | gc [64] | pad [64]
@@ -76,7 +76,7 @@ constexpr int G_NS = 6;                     // LDS ring depth (layers)
 constexpr int G_PIECES = 5;                 // 1-KiB pieces per loader wave per layer (4 loaders)
 constexpr int G_DMA = G_PIECES + 1;         // + one 256-B row
 constexpr int G_MAXL = 256;                 // tap table rows
-constexpr int G_LDS = G_NS * G_SLOT + (G_MAXL + 2) * 32 + 64;   // ring | taps | x | z  (162,304 B)
+constexpr int G_LDS = G_NS * G_SLOT + (G_MAXL + 2) * 32 + 4 * 32 + 2 * 32;   // ring | taps | x[4 waves] | z[2]
 static_assert(4 * G_PIECES * 256 == GI_WR, "image pieces");
 static_assert(G_LDS * 4 <= 160 * 1024, "LDS");
 
@@ -116,8 +116,6 @@ __global__ __launch_bounds__(512) void gen_wave_kernel(WaveK a) {
   __shared__ __attribute__((aligned(16))) float sm[G_LDS];
   float* RING = sm;                  // [G_NS][G_SLOT]
   float* XP = sm + G_NS * G_SLOT;    // [L (+2)][32] dilated taps of this step
-  float* X = XP + (G_MAXL + 2) * 32; // [32] current layer input
-  float* Z = X + 32;                 // [32] gate output
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, b = blockIdx.x, L = a.L;
   const long t = *a.step;
 
@@ -161,54 +159,65 @@ __global__ __launch_bounds__(512) void gen_wave_kernel(WaveK a) {
       dma4(row + lane, dst + GI_WR + lw * 64);
     };
     for (int l = 0; l < G_NS - 1 && l < L; ++l) issue(l);
-    for (int k = 0; k < L; ++k) {
-      // issued so far: taps, layers 0 .. min(k+NS-2, L-1); retire everything up to layer k
-      if (k + G_NS - 2 < L) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G_DMA * (G_NS - 2)) : "memory");
+    for (int k = -1; k < L; ++k) {
+      // barrier k (after z_k is written; k = -1: the step input) releases the residual of layer
+      // k and the conv of layer k+1, so slot k+1 must have landed.  Issued so far: taps, layers
+      // 0 .. min(k+NS-2, L-1): retire all but the min(k+NS-2, L-1) - (k+1) youngest layers.
+      const int younger = min(k + G_NS - 2, L - 1) - (k + 1);
+      if (younger >= G_NS - 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G_DMA * (G_NS - 3)) : "memory");
+      else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G_DMA * 2) : "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G_DMA) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_barrier();                                   // B1 of layer k
-      if (k + G_NS - 1 < L) issue(k + G_NS - 1);      // into slot (k-1) % NS, read-retired before B1
-      lds_barrier();                                   // B2 of layer k
+      lds_barrier();
+      // slot of layer k-1 is dead (its residual ran before barrier k): layer k+NS-1 goes there
+      // (k = 0: the slot of layer NS-1, never used yet)
+      if (k >= 0 && k + G_NS - 1 < L) issue(k + G_NS - 1);
     }
     return;
   }
 
-  // ---- compute waves
+  // ---- compute waves: ONE workgroup barrier per layer.  Every wave keeps the whole layer input
+  // x (lane c and c+32 hold channel c) and computes the residual of all 32 channels itself
+  // (16 FMAs per lane over one z half, the halves summed by v_permlane32_swap), so the next
+  // layer's conv needs no second barrier: its inputs go through the wave's own LDS row (XW).
   const int w = wid, Cr = a.Cr, Cd = a.Cd;
   const int c = lane >> 3, sg = (lane >> 2) & 1, kq = lane & 3, kp = lane & 7;
-  const int ch = 8 * w + c;                 // the channel this lane group owns (z and x)
+  const int ch = 8 * w + c;                 // the conv channel of this lane group
   const int o = 32 * sg + ch;               // conv output of this lane
-  const bool lead = kp == 0;                // one lane per group stores
+  const bool lead = kp == 0;                // one lane per group stores z
+  const int rc = lane & 31, rh = lane >> 5; // residual: out channel rc over z half rh
+  float* XW = XP + (G_MAXL + 2) * 32 + 32 * w;   // this wave's copy of the layer input
+  float* Z = XP + (G_MAXL + 2) * 32 + 128;       // z double buffer [2][32]
   const bool tr = a.trace && b == 0 && w == 0 && lane == 0;
   if (tr) a.trace[0] = clock64();
   // step input: PRE row of the previous draw (+ PRE_BIAS); the zero vector at step 0
-  float xr = 0.f;   // x[ch] of the current layer input (all 8 lanes of the group)
-  if (ch < Cr) {
+  float x = 0.f;    // x[rc] of the current layer input
+  if (rc < Cr) {
     const int code = a.code[b];
-    if (code >= 0) xr = a.pre[(long)code * Cr + ch];
-    if (a.pre_bias && a.pre_b) xr += a.pre_b[ch];
+    if (code >= 0) x = a.pre[(long)code * Cr + rc];
+    if (a.pre_bias && a.pre_b) x += a.pre_b[rc];
   }
-  if (lead) X[ch] = xr;
+  if (lane < 32) XW[rc] = x;
   if (tr) a.trace[1] = clock64();
-  // conv inputs of this lane: k-quarter kq of [x[t-d] (tap row) | x[t] (X)]
   const int xin_off = kq < 2 ? 16 * kq : 16 * (kq - 2);
   long roff = 0;   // ring offset of layer l
   int bl = 0;      // l % nbl
+  lds_barrier();   // barrier -1: taps and slot 0 landed, every wave's XW written
+  if (tr) a.trace[2] = clock64();
   for (int l = 0; l < L; ++l) {
-    lds_barrier();   // B1: x of layer l, taps and layer l's slot are in LDS
-    if (tr && l == 0) a.trace[2] = clock64();
     const float* S = RING + (l % G_NS) * G_SLOT;
-    const float* xin = (kq < 2 ? XP + l * 32 : X) + xin_off;
+    const float* xin = (kq < 2 ? XP + l * 32 : XW) + xin_off;
     floatx4 wv[4], xv[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       wv[m] = *(const floatx4*)(S + (w * 4 + m) * 256 + lane * 4);
       xv[m] = *(const floatx4*)(xin + 4 * m);
     }
-    const floatx4 rw = *(const floatx4*)(S + GI_W + w * 256 + lane * 4);
-    const float bco = S[GI_WR + o] + S[GI_WR + 128 + o], bro = S[GI_WR + 64 + ch];
+    const float bco = S[GI_WR + o] + S[GI_WR + 128 + o];
     __builtin_amdgcn_sched_barrier(0);
     const int d = 1 << bl;
-    if (lead && ch < Cr) a.rings[roff + ((long)b * d + (t & (d - 1))) * Cr + ch] = xr;
+    // x_l[t] into the ring (wave w stores channels 8w..8w+7)
+    if (rh == 0 && (rc >> 3) == w && rc < Cr) a.rings[roff + ((long)b * d + (t & (d - 1))) * Cr + rc] = x;
     roff += (long)d * a.B * Cr;
     bl = (bl + 1 == a.nbl) ? 0 : bl + 1;
     float acc0 = dot4(wv[0], xv[0], 0.f), acc1 = dot4(wv[1], xv[1], 0.f);
@@ -220,19 +229,29 @@ __global__ __launch_bounds__(512) void gen_wave_kernel(WaveK a) {
     v += bco;                                      // conv output o (+ bias + GC term)
     const float vp = dpp<DPP_HALF_MIRROR>(v);      // the partner output (sig <-> gate, same channel)
     const float z = tanhf_(sg ? vp : v) * sigmoidf_(sg ? v : vp);
-    if (tr) a.trace[4 + 2 * l] = clock64();
+    float* Zl = Z + (l & 1) * 32;
     if (lead) {
-      Z[ch] = z;
+      Zl[ch] = z;
       if (ch < Cd) a.zcat[(long)b * L * Cd + (long)l * Cd + ch] = z;
     }
-    lds_barrier();   // B2: z of layer l
-    const floatx4 zv = *(const floatx4*)(Z + 4 * kp);
-    float r = dot4(rw, zv, 0.f);
-    r += dpp<DPP_XOR1>(r);
-    r += dpp<DPP_XOR2>(r);
-    r += dpp<DPP_HALF_MIRROR>(r);
-    xr += r + bro;
-    if (lead) X[ch] = xr;
+    if (tr) a.trace[4 + 2 * l] = clock64();
+    lds_barrier();   // barrier l: z_l complete; slot l+1 landed
+    // residual of all 32 channels: x_{l+1}[rc] = x[rc] + b[rc] + Σ_k RES[k][rc]·z[k]
+    floatx4 zv[4], rw[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      zv[q] = *(const floatx4*)(Zl + 16 * rh + 4 * q);
+      rw[q] = *(const floatx4*)(S + GI_W + ((rh * 4 + q) * 32 + rc) * 4);
+    }
+    const float bro = S[GI_WR + 64 + rc];
+    float r0 = dot4(rw[0], zv[0], 0.f), r1 = dot4(rw[1], zv[1], 0.f);
+    r0 = dot4(rw[2], zv[2], r0);
+    r1 = dot4(rw[3], zv[3], r1);
+    const float r = r0 + r1;
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(r), __float_as_uint(r), false, false);
+    x += (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) + bro;
+    if (lane < 32) XW[rc] = x;   // read back by this wave's conv of layer l+1: a wave-local sync only
+    wave_sync();
     if (tr) a.trace[5 + 2 * l] = clock64();
   }
 }
@@ -251,8 +270,8 @@ __global__ void gen_pack_kernel(const float* sig, const float* gate, const float
       const int k = 16 * kq + 4 * m + j, tap = k >> 5, in = k & 31, oc = 8 * w + c;
       if (in < Cr && oc < Cd) v = (sg ? gate : sig)[(long)l * 2 * Cr * Cd + (tap * Cr + in) * Cd + oc];
     } else if (e < GI_WR) {
-      const int f = e - GI_W, w = f / 256, ln = (f % 256) / 4, j = f % 4;
-      const int zc = 4 * (ln & 7) + j, oc = 8 * w + (ln >> 3);
+      const int f = e - GI_W, j = f & 3, oc = (f >> 2) & 31, q = (f >> 7) & 3, h = f >> 9;
+      const int zc = 16 * h + 4 * q + j;
       if (zc < Cd && oc < Cr) v = res[(long)l * Cd * Cr + zc * Cr + oc];
     } else {
       const int f = e - GI_WR;
