@@ -110,6 +110,7 @@ def bench_gen(net, arch, B=10, seconds=3.0, sr=16000, chunk=1000):
     g.step(n)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    g.check_status()
     bps = gen_bytes_per_step(arch, B)
     return {'metric': 'cached autoregressive gen audio samples/s (B streams x steps / wall)',
             'value': B * n / dt, 'unit': 'audio samples/s', 'steps': n, 'batch': B, 'wall_s': dt,

@@ -4,15 +4,17 @@
 // hipGraph and replayed: the step counter, the per-layer lookback rings (the generation
 // form of the D-separation cache: layer l keeps its last d inputs, slot t mod d, replacing
 // imodel's shift-by-chunk buffers imodel.py:88-98, :190-207), the next input code, the
-// teacher vector and a counter-based RNG.  One step =
-//   gen_wave     one workgroup per stream: a compute wave runs PRE row (+bias), 50 × [dilated conv
-//                (lane = output channel, 64-term dot over LDS broadcasts), gate (lane pairs),
-//                residual] while three loader waves stream the per-layer weight images into an
-//                LDS ring by LDS-DMA, several layers ahead
-//   gen_gemv × 3 K-split row-vector products with deterministic partial sums:
-//                skip = z_cat·SKIPcat, h = relu(relu(skip + Σb)·POST1 + b1), logits = h·POST2
-//   gen_sample   logits = Σ partials + b2; inverse-CDF draw with u = hash(seed, stream, step),
-//                µ-law decode, next input = teacher[t] or the draw (imodel.py:167-187, :260-269)
+// teacher vector and a counter-based RNG.  One step = three launches:
+//   gen_wave     one workgroup per stream: four compute waves draw the PREVIOUS step (Σ post2
+//                partials + b2, inverse-CDF with u = hash(seed, stream, step), µ-law decode, next
+//                input = teacher[t] or the draw: imodel.py:167-187, :260-269), then run PRE row
+//                (+bias), 50 × [dilated conv, gate, residual] while four loader waves stream the
+//                per-layer weight images into an LDS ring by LDS-DMA, several layers ahead.  Each
+//                z_l leaves as tagged 8-byte granules; skip helper blocks of the same launch
+//                (layer pairs of SKIPcat) poll them and accumulate the skip sum as the chain runs
+//   gen_gemv × 2 K-split row-vector products with deterministic partial sums:
+//                h = relu(relu(Σ skip partials + Σb)·POST1 + b1), logits partials = h·POST2
+// (the last step of a run is drawn by gen_sample, one wave per stream, same draw code)
 #include <math.h>
 #include <string.h>
 
@@ -31,21 +33,6 @@ LBWN_DEV void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Σ_q p[q·stride], q < n, in a fixed order: all loads of a 32-chunk are issued before the
-// first add (the index is clamped instead of predicated, so no load sits behind a branch and
-// hipcc counts them as one group: one memory round trip per 32 partials, not one per 8)
-LBWN_DEV float sum_parts(const float* p, long stride, int n) {
-  float s = 0.f;
-  for (int q0 = 0; q0 < n; q0 += 32) {
-    float v[32];
-#pragma unroll
-    for (int i = 0; i < 32; ++i) v[i] = p[(long)min(q0 + i, n - 1) * stride];
-#pragma unroll
-    for (int i = 0; i < 32; ++i) s += (q0 + i < n) ? v[i] : 0.f;
-  }
-  return s;
 }
 
 // ---- per-stream layer chain --------------------------------------------------------------
@@ -80,12 +67,191 @@ constexpr int G_LDS = G_NS * G_SLOT + (G_MAXL + 2) * 32 + 4 * 32 + 2 * 32;   // 
 static_assert(4 * G_PIECES * 256 == GI_WR, "image pieces");
 static_assert(G_LDS * 4 <= 160 * 1024, "LDS");
 
+// ---- the draw (imodel.py:167-187, :260-269) ----------------------------------------------
+// logits[c] = Σ_p part[p][b][c] + bias[c] (fixed order), then the first k with
+// cumsum(e)[k] > u·Σe, e = exp(logits - max), u = hash(seed, stream, step).  Wave-level only
+// (lane = a contiguous run of ceil(Q/64) codes, shuffles, no workgroup barrier), so the four
+// compute waves of a gen_wave block all draw the same code without exchanging it, and the
+// standalone gen_sample_kernel (one wave per stream) runs the identical instruction sequence
+// (oracle/wavenet_ref.py sample_from_logits restates the transform).
+struct DrawK {
+  const float* part; int parts; const float* bias;   // partials [parts][B][Q]
+  int Q, B;
+  float* logits; int* samples; float* wav; long long max_steps;
+  const int* teacher; long long n_teacher; unsigned long long seed; int* code;
+};
+
+LBWN_DEV uint64_t splitmix(uint64_t seed, uint64_t stream, uint64_t step) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ULL + (stream << 32) + step + 0x632BE59BD9B4E019ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+// returns the next input code of stream b after step t (the teacher's or the draw); the
+// writing wave stores logits, the sample, its µ-law decode and code[b]
+template <int MP>
+LBWN_DEV int draw_wave(const DrawK& a, int b, long long t, bool write) {
+  const int lane = threadIdx.x & 63, Q = a.Q;
+  const int per = (Q + 63) >> 6, c0 = lane * per;
+  float v[MP], bv[MP];
+#pragma unroll
+  for (int j = 0; j < MP; ++j) {
+    v[j] = 0.f;
+    bv[j] = a.bias ? a.bias[min(c0 + j, Q - 1)] : 0.f;
+  }
+  constexpr int CH = MP > 4 ? 8 : 16;
+  for (int q0 = 0; q0 < a.parts; q0 += CH) {   // every load of a chunk (and the bias) issued before the first add
+    float x[MP][CH];
+#pragma unroll
+    for (int j = 0; j < MP; ++j)
+#pragma unroll
+      for (int i = 0; i < CH; ++i)
+        x[j][i] = a.part[((long)min(q0 + i, a.parts - 1) * a.B + b) * Q + min(c0 + j, Q - 1)];
+#pragma unroll
+    for (int j = 0; j < MP; ++j)
+#pragma unroll
+      for (int i = 0; i < CH; ++i) v[j] += (q0 + i < a.parts) ? x[j][i] : 0.f;
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < MP; ++j) {
+    const bool ok = j < per && c0 + j < Q;
+    if (a.bias) v[j] += bv[j];
+    if (ok) mx = fmaxf(mx, v[j]);
+    if (ok && write) a.logits[(long)b * Q + c0 + j] = v[j];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  float e[MP], loc = 0.f;
+#pragma unroll
+  for (int j = 0; j < MP; ++j) {
+    e[j] = (j < per && c0 + j < Q) ? expf(v[j] - mx) : 0.f;
+    loc += e[j];
+  }
+  float incl = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float s = __shfl_up(incl, o);
+    if (lane >= o) incl += s;
+  }
+  const float total = __shfl(incl, 63);
+  const float excl = incl - loc;
+  const uint64_t h = splitmix(a.seed, (uint64_t)b, (uint64_t)t);
+  const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+  const float target = u * total;
+  int found = Q;   // the lane whose run contains the crossing point
+  if (excl <= target && target < incl) {
+    float run = excl;
+#pragma unroll
+    for (int j = 0; j < MP; ++j) {
+      if (j < per && c0 + j < Q && found == Q) {
+        run += e[j];
+        if (run > target) found = c0 + j;
+      }
+    }
+    if (found == Q) found = min(c0 + per, Q) - 1;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) found = min(found, __shfl_xor(found, o));
+  if (found >= Q) found = Q - 1;
+  const int next = (t < a.n_teacher) ? a.teacher[t] : found;   // imodel.py:260-269
+  if (write && lane == 0) {
+    if (t < a.max_steps) {
+      a.samples[(long)b * a.max_steps + t] = found;
+      const float mu = (float)(Q - 1), inv = 1.f / mu;               // ops.py:12-20
+      const float aa = (2.f * (float)found - 1.f) * inv - 1.f;
+      const float sg = aa > 0.f ? 1.f : (aa < 0.f ? -1.f : 0.f);
+      a.wav[(long)b * a.max_steps + t] = sg * (powf(1.f + mu, fabsf(aa)) - 1.f) * inv;
+    }
+    a.code[b] = next;
+  }
+  return next;
+}
+
 struct WaveK {
   const float* pre; const float* pre_b; const float* img; const float* gc_proj;
-  float* rings; float* zcat; const long long* step; const int* code;
+  float* rings; const long long* step; const int* code;
   int B, L, nbl, Cr, Cd, pre_bias;
+  // z_l of every stream as {z, tag = step+1} granules [B][L][32] (one 8-B sc1 store each), read
+  // by the skip helper blocks of the same launch (blockIdx >= B): helper j owns layers
+  // [LG·j, LG·j+LG) of SKIPcat [L·Cd][Cs] and writes its partial skip sum [j][B][Cs]
+  unsigned long long* zg; const float* skipw; float* skip_part; int Cs, LG;
+  int* status;
+  // fused draw: this launch first draws step t-1 of its stream (the previous step's post2
+  // partials), so the sampler launch and its boundary leave the per-step chain
+  int fuse_draw; DrawK draw;
   long long* trace;   // non-null (LBWN_GEN_TRACE set at plan creation): stream 0's cycle stamps
 };
+
+constexpr long long G_SPIN_TIMEOUT = 400000000LL;   // wall_clock64 ticks (100 MHz) = 4 s
+
+// skip helper j: per group of 16 streams and per owned layer, poll the 16×Cd z granules (one
+// per thread), stage them in LDS, and accumulate Σ_k z[b][k]·SKIP[l·Cd+k][n] for column n =
+// threadIdx.x; the layer's weight column is loaded before the poll so its latency hides there
+LBWN_DEV void skip_helper(const WaveK& a, int j, long long t, float* sm) {
+  const int tid = threadIdx.x, L = a.L, Cd = a.Cd, Cs = a.Cs, B = a.B;
+  const int l0 = j * a.LG, l1 = min(L, l0 + a.LG);
+  const unsigned tag = (unsigned)(t + 1);
+  const int n = min(tid, Cs - 1), gb = tid >> 5, gk = tid & 31;
+  for (int g0 = 0; g0 < B; g0 += 16) {
+    const int nb = min(16, B - g0);
+    float acc[16];
+#pragma unroll
+    for (int bb = 0; bb < 16; ++bb) acc[bb] = 0.f;
+    int buf = 0;
+    for (int l = l0; l < l1; ++l, buf ^= 1) {
+      float w[32];
+      const float* S = a.skipw + (long)l * Cd * Cs + n;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) w[k] = S[(long)min(k, Cd - 1) * Cs];
+#pragma unroll
+      for (int k = 0; k < 32; ++k)
+        if (k >= Cd) w[k] = 0.f;
+      float zv = 0.f;
+      if (gb < nb && gk < Cd) {
+        const unsigned long long* gp = a.zg + ((long)(g0 + gb) * L + l) * 32 + gk;
+        long long ts = 0;
+        for (;;) {
+          const unsigned long long g = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((unsigned)(g >> 32) == tag) { zv = __uint_as_float((unsigned)g); break; }
+          const long long now = wall_clock64();
+          if (ts == 0) ts = now;
+          else if (now - ts > G_SPIN_TIMEOUT) {
+            __hip_atomic_store(a.status, 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      const bool trh = a.trace && tid == 0 && blockIdx.x == gridDim.x - 1 && l - l0 < 2 && g0 == 0;
+      if (trh) a.trace[2 * L + 12 + 2 * (l - l0)] = wall_clock64();
+      float* ZS = sm + buf * 512;   // [16 streams][32]; double-buffered: one barrier per layer
+      ZS[tid] = zv;
+      __syncthreads();
+#pragma unroll
+      for (int bb = 0; bb < 16; ++bb) {
+        if (bb < nb) {
+          const floatx4* zr = (const floatx4*)(ZS + bb * 32);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const floatx4 z4 = zr[q];
+            acc[bb] = fmaf(z4[0], w[4 * q], acc[bb]);
+            acc[bb] = fmaf(z4[1], w[4 * q + 1], acc[bb]);
+            acc[bb] = fmaf(z4[2], w[4 * q + 2], acc[bb]);
+            acc[bb] = fmaf(z4[3], w[4 * q + 3], acc[bb]);
+          }
+        }
+      }
+    }
+    if (a.trace && tid == 0 && blockIdx.x == gridDim.x - 1 && g0 == 0) a.trace[2 * L + 13] = wall_clock64();
+    if (tid < Cs) {
+#pragma unroll
+      for (int bb = 0; bb < 16; ++bb)
+        if (bb < nb) a.skip_part[((long)j * B + g0 + bb) * Cs + tid] = acc[bb];
+    }
+  }
+}
 
 LBWN_DEV float dot4(const floatx4& w, const floatx4& x, float acc) {
   acc = fmaf(w[0], x[0], acc);
@@ -118,6 +284,14 @@ __global__ __launch_bounds__(512) void gen_wave_kernel(WaveK a) {
   float* XP = sm + G_NS * G_SLOT;    // [L (+2)][32] dilated taps of this step
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, b = blockIdx.x, L = a.L;
   const long t = *a.step;
+
+  if (b >= a.B) {   // ---- skip helper blocks
+    const bool trh = a.trace && threadIdx.x == 0 && b == gridDim.x - 1;
+    if (trh) a.trace[2 * L + 10] = wall_clock64();
+    skip_helper(a, b - a.B, t, sm);
+    if (trh) a.trace[2 * L + 11] = wall_clock64();
+    return;
+  }
 
   if (wid >= 4) {   // ---- loader waves
     const int lw = wid - 4;
@@ -189,16 +363,25 @@ __global__ __launch_bounds__(512) void gen_wave_kernel(WaveK a) {
   float* XW = XP + (G_MAXL + 2) * 32 + 32 * w;   // this wave's copy of the layer input
   float* Z = XP + (G_MAXL + 2) * 32 + 128;       // z double buffer [2][32]
   const bool tr = a.trace && b == 0 && w == 0 && lane == 0;
-  if (tr) a.trace[0] = clock64();
-  // step input: PRE row of the previous draw (+ PRE_BIAS); the zero vector at step 0
+  if (tr) { a.trace[0] = clock64(); a.trace[2 * L + 8] = wall_clock64(); }
+  long long* trs = (a.trace && w == 0 && lane == 0) ? a.trace + 2 * L + 40 + 3 * b : nullptr;
+  if (trs) trs[0] = wall_clock64();
+  // step input: PRE row of the previous draw (+ PRE_BIAS); the zero vector at step 0.  With
+  // fuse_draw every compute wave draws step t-1 itself (wave 0 writes), while the loader waves'
+  // first taps and weight slots are in flight
+  int code;
+  if (a.fuse_draw)
+    code = a.draw.Q > 256 ? draw_wave<8>(a.draw, b, t - 1, w == 0) : draw_wave<4>(a.draw, b, t - 1, w == 0);
+  else
+    code = a.code[b];
   float x = 0.f;    // x[rc] of the current layer input
   if (rc < Cr) {
-    const int code = a.code[b];
     if (code >= 0) x = a.pre[(long)code * Cr + rc];
     if (a.pre_bias && a.pre_b) x += a.pre_b[rc];
   }
   if (lane < 32) XW[rc] = x;
   if (tr) a.trace[1] = clock64();
+  if (trs) trs[1] = wall_clock64();
   const int xin_off = kq < 2 ? 16 * kq : 16 * (kq - 2);
   long roff = 0;   // ring offset of layer l
   int bl = 0;      // l % nbl
@@ -232,7 +415,10 @@ __global__ __launch_bounds__(512) void gen_wave_kernel(WaveK a) {
     float* Zl = Z + (l & 1) * 32;
     if (lead) {
       Zl[ch] = z;
-      if (ch < Cd) a.zcat[(long)b * L * Cd + (long)l * Cd + ch] = z;
+      if (ch < Cd)   // granule for the skip helpers: fire-and-forget, no wait on the chain
+        __hip_atomic_store(a.zg + ((long)b * L + l) * 32 + ch,
+                           ((unsigned long long)(unsigned)(t + 1) << 32) | __float_as_uint(z), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
     if (tr) a.trace[4 + 2 * l] = clock64();
     lds_barrier();   // barrier l: z_l complete; slot l+1 landed
@@ -254,6 +440,8 @@ __global__ __launch_bounds__(512) void gen_wave_kernel(WaveK a) {
     wave_sync();
     if (tr) a.trace[5 + 2 * l] = clock64();
   }
+  if (tr) a.trace[2 * L + 9] = wall_clock64();
+  if (trs) trs[2] = wall_clock64();
 }
 
 // per-layer weight image in the compute waves' lane order (reference layouts in, GIMG floats
@@ -417,80 +605,12 @@ __global__ __launch_bounds__(256) void gen_gemv_kernel(GemvK a) {
   if (a.trace && tid == 0 && last) a.trace[7] = wall_clock64();
 }
 
-LBWN_DEV uint64_t splitmix(uint64_t seed, uint64_t stream, uint64_t step) {
-  uint64_t z = seed * 0x9E3779B97F4A7C15ULL + (stream << 32) + step + 0x632BE59BD9B4E019ULL;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
-  return z ^ (z >> 31);
-}
-
-struct SampleK {
-  float* logits; int Q, B;
-  const float* log_part; int parts; const float* bias;   // logits = Σ parts + bias (written to logits)
-  long long* step; int* code; const int* teacher; long long n_teacher;
-  int* samples; float* wav; long long max_steps; unsigned long long seed;
-};
-
-// one block per stream: thread c sums code c's logit partials (+b2), then wave 0 draws from
-// the softmax CDF in a fixed order: the first k with cumsum(e)[k] > u·Σe
-// (oracle/wavenet_ref.py sample_from_logits restates the same transform).  The step counter
-// was advanced by this step's skip GEMV, so this step is *step - 1.
-__global__ __launch_bounds__(256) void gen_sample_kernel(SampleK a) {
-  extern __shared__ float lg[];   // [Q]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, b = blockIdx.x;
-  const long long t = *a.step - 1;
-  for (int c = threadIdx.x; c < a.Q; c += blockDim.x) {
-    float v = sum_parts(a.log_part + (long)b * a.Q + c, (long)a.B * a.Q, a.parts);
-    if (a.bias) v += a.bias[c];
-    lg[c] = v;
-    a.logits[(long)b * a.Q + c] = v;
-  }
-  __syncthreads();
-  if (w != 0) return;
-  float mx = -INFINITY;
-  for (int c = lane; c < a.Q; c += 64) mx = fmaxf(mx, lg[c]);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-  // each lane owns a contiguous run of Q/64 codes: local sums, then an exclusive scan
-  const int per = (a.Q + 63) / 64, c0 = lane * per;
-  float loc = 0.f;
-  for (int j = 0; j < per; ++j)
-    if (c0 + j < a.Q) loc += expf(lg[c0 + j] - mx);
-  float incl = loc;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float v = __shfl_up(incl, o);
-    if (lane >= o) incl += v;
-  }
-  const float total = __shfl(incl, 63);
-  const float excl = incl - loc;
-  const uint64_t h = splitmix(a.seed, (uint64_t)b, (uint64_t)t);
-  const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
-  const float target = u * total;
-  // lane whose run contains the crossing point
-  int found = a.Q;
-  if (excl <= target && target < incl) {
-    float run = excl;
-    for (int j = 0; j < per; ++j) {
-      if (c0 + j >= a.Q) break;
-      run += expf(lg[c0 + j] - mx);
-      if (run > target) { found = c0 + j; break; }
-    }
-    if (found == a.Q) found = min(c0 + per, a.Q) - 1;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) found = min(found, __shfl_xor(found, o));
-  if (found >= a.Q) found = a.Q - 1;
-  if (lane == 0) {
-    if (t < a.max_steps) {
-      a.samples[(long)b * a.max_steps + t] = found;
-      const float mu = (float)(a.Q - 1), inv = 1.f / mu;               // ops.py:12-20
-      const float aa = (2.f * (float)found - 1.f) * inv - 1.f;
-      const float sg = aa > 0.f ? 1.f : (aa < 0.f ? -1.f : 0.f);
-      a.wav[(long)b * a.max_steps + t] = sg * (powf(1.f + mu, fabsf(aa)) - 1.f) * inv;
-    }
-    a.code[b] = (t < a.n_teacher) ? a.teacher[t] : found;              // imodel.py:260-269
-  }
+// the step's draw when it is not fused into the next gen_wave launch (the last step of a run):
+// one wave per stream, t = *step - 1 (post1 advanced the counter)
+__global__ __launch_bounds__(64) void gen_sample_kernel(DrawK a, const long long* step) {
+  const long long t = *step - 1;
+  if (a.Q > 256) draw_wave<8>(a, blockIdx.x, t, true);
+  else draw_wave<4>(a, blockIdx.x, t, true);
 }
 
 // gc_proj[l][b][o] = GC_EMBED[gc_id[b]] · [GC_SIGNAL_l | GC_GATE_l]  (imodel.py:53-56, :113-118)
@@ -531,9 +651,9 @@ struct lbwn_gen_plan {
   lbwn_arch a;
   int B, L, nbl, Cr, Cd, Cs, Cp, Q;
   long long max_steps;
-  size_t oRING, oZCAT, oSKP, oHP, oLGP, oLOG, oSTEP, oCODE, oTEACH, oSAMP, oWAV, oGCP, oBSUM, oGIMG, oTRACE, total;
+  size_t oRING, oZG, oSKP, oHP, oLGP, oLOG, oSTEP, oCODE, oTEACH, oSAMP, oWAV, oGCP, oBSUM, oGIMG, oTRACE, total;
   bool trace;
-  int ksl_skip, ks_skip, ks_h, ks_lg;
+  int lg_skip, ks_skip, ks_h, ks_lg;
   long n_ring;
   long long n_teacher, max_teacher;
   unsigned long long seed;
@@ -550,6 +670,8 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
                                     lbwn_gen_plan** out) {
   LBWN_REQUIRE(a && out && B >= 1 && max_steps >= 1 && max_teacher >= 0, "gen_plan_create: bad arguments");
   LBWN_REQUIRE(a->n_res <= 32 && a->n_dil <= 32, "gen: n_res/n_dil must be <= 32");
+  LBWN_REQUIRE(a->n_skip <= 512, "gen: n_skip must be <= 512 (one skip column per helper thread)");
+  LBWN_REQUIRE(a->n_quant <= 512, "gen: n_quant must be <= 512");
   LBWN_REQUIRE(a->n_blocks * a->n_block_layers <= G_MAXL, "gen: more than %d layers (tap cache)", G_MAXL);
   LBWN_REQUIRE(a->n_lc_out == 0, "gen: local conditioning is not supported by the cached generator "
                                  "(imodel.py has no LC path)");
@@ -565,10 +687,10 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
   p->n_ring = dsum * B * p->Cr;
   size_t cur = 0;
   p->oRING = gcarve(cur, 4 * (size_t)p->n_ring);
-  p->oZCAT = gcarve(cur, 4 * (size_t)B * p->L * p->Cd);
+  p->oZG = gcarve(cur, 8 * (size_t)B * p->L * 32);   // z granules {z, step+1}
   // K-split GEMV partials: skip (K = L·Cd, 64-row slices), post1 and post2 (32-row slices)
-  p->ksl_skip = 64;
-  p->ks_skip = (p->L * p->Cd + p->ksl_skip - 1) / p->ksl_skip;
+  p->lg_skip = 2;                                    // layers per skip helper block
+  p->ks_skip = (p->L + p->lg_skip - 1) / p->lg_skip;
   p->ks_h = (p->Cs + 31) / 32;
   p->ks_lg = (p->Cp + 31) / 32;
   p->oSKP = gcarve(cur, 4 * (size_t)p->ks_skip * B * p->Cs);
@@ -583,7 +705,7 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
   p->oGCP = gcarve(cur, 4 * (size_t)p->L * B * 64);
   p->oBSUM = gcarve(cur, 4 * (size_t)p->Cs);
   p->oGIMG = gcarve(cur, 4 * (size_t)p->L * GIMG);
-  p->oTRACE = gcarve(cur, 8 * (size_t)(2 * p->L + 8 + 32));
+  p->oTRACE = gcarve(cur, 8 * (size_t)(2 * p->L + 40 + 3 * p->B));
   p->trace = getenv("LBWN_GEN_TRACE") != nullptr;
   p->total = cur;
   *out = p;
@@ -600,8 +722,8 @@ extern "C" int lbwn_gen_tensor(const lbwn_gen_plan* p, const char* name, size_t*
   else if (!strcmp(name, "wav")) { *off = p->oWAV; *bytes = 4 * B * p->max_steps; }
   else if (!strcmp(name, "logits")) { *off = p->oLOG; *bytes = 4 * B * p->Q; }
   else if (!strcmp(name, "step")) { *off = p->oSTEP; *bytes = 8; }
-  else if (!strcmp(name, "status")) { *off = p->oSTEP + 8; *bytes = 4; }   // reserved: 0 (the barrier-synchronised chain has no failure path)
-  else if (!strcmp(name, "trace")) { *off = p->oTRACE; *bytes = 8 * (size_t)(2 * p->L + 8 + 32); }
+  else if (!strcmp(name, "status")) { *off = p->oSTEP + 8; *bytes = 4; }   // 0, or 5: a skip helper's granule poll timed out
+  else if (!strcmp(name, "trace")) { *off = p->oTRACE; *bytes = 8 * (size_t)(2 * p->L + 40 + 3 * p->B); }
   else if (!strcmp(name, "rings")) { *off = p->oRING; *bytes = 4 * (size_t)p->n_ring; }
   else if (!strcmp(name, "teacher")) { *off = p->oTEACH; *bytes = 4 * (size_t)std::max<long long>(1, p->n_teacher); }
   else LBWN_REQUIRE(false, "gen_tensor: unknown tensor '%s'", name);
@@ -649,44 +771,48 @@ extern "C" int lbwn_gen_run(lbwn_gen_plan* p, const lbwn_params* P, void* ws, in
   LBWN_REQUIRE(p && P && ws && n_steps >= 0, "gen_run: bad arguments");
   hipStream_t st = (hipStream_t)stream;
   WaveK c;
+  memset(&c, 0, sizeof(c));
   c.pre = P->pre; c.pre_b = P->pre_b; c.img = gat<float>(ws, p->oGIMG);
   c.gc_proj = p->a.n_gc_embed > 0 ? gat<float>(ws, p->oGCP) : nullptr;
-  c.rings = gat<float>(ws, p->oRING); c.zcat = gat<float>(ws, p->oZCAT);
+  c.rings = gat<float>(ws, p->oRING);
   c.step = gat<long long>(ws, p->oSTEP); c.code = gat<int>(ws, p->oCODE);
   c.trace = p->trace ? gat<long long>(ws, p->oTRACE) : nullptr;
   c.B = p->B; c.L = p->L; c.nbl = p->nbl; c.Cr = p->Cr; c.Cd = p->Cd; c.pre_bias = p->pre_bias;
-  // skip = z_cat·SKIPcat (+Σb and relu applied by the consumer), h = relu(relu(skip)·POST1 + b1),
-  // logits = h·POST2 + b2 (summed in the sampler)
-  GemvK sk = {}, p1 = {}, p2 = {};
-  memset(&sk, 0, sizeof(sk));
-  sk.in = c.zcat; sk.ldin = (long)p->L * p->Cd; sk.W = P->skip; sk.ldw = p->Cs; sk.out_part = gat<float>(ws, p->oSKP);
-  sk.B = p->B; sk.K = p->L * p->Cd; sk.N = p->Cs; sk.KSL = p->ksl_skip;
-  sk.step_advance = gat<long long>(ws, p->oSTEP);   // the sampler reads step - 1
-  p1 = sk;
-  p1.step_advance = nullptr;
-  p1.in = nullptr; p1.in_part = sk.out_part; p1.in_parts = p->ks_skip; p1.in_bias = P->skip_b ? gat<float>(ws, p->oBSUM) : nullptr;
-  p1.relu_in = 1; p1.W = P->post1; p1.ldw = p->Cp; p1.out_part = gat<float>(ws, p->oHP); p1.K = p->Cs; p1.N = p->Cp; p1.KSL = 32;
+  c.zg = gat<unsigned long long>(ws, p->oZG); c.skipw = P->skip; c.skip_part = gat<float>(ws, p->oSKP);
+  c.Cs = p->Cs; c.LG = p->lg_skip; c.status = gat<int>(ws, p->oSTEP + 8);
+  // skip = Σ helper partials (+Σb, relu: post1's input), h = relu(relu(skip)·POST1 + b1),
+  // logits = h·POST2 + b2 (summed by the draw); post1 advances the step counter
+  GemvK p1, p2;
+  memset(&p1, 0, sizeof(p1));
+  p1.in_part = c.skip_part; p1.in_parts = p->ks_skip; p1.in_bias = P->skip_b ? gat<float>(ws, p->oBSUM) : nullptr;
+  p1.relu_in = 1; p1.W = P->post1; p1.ldw = p->Cp; p1.out_part = gat<float>(ws, p->oHP);
+  p1.B = p->B; p1.K = p->Cs; p1.N = p->Cp; p1.KSL = 32;
+  p1.step_advance = gat<long long>(ws, p->oSTEP);
   p2 = p1;
+  p2.step_advance = nullptr;
   p2.in_part = p1.out_part; p2.in_parts = p->ks_h; p2.in_bias = P->post1_b; p2.relu_in = 1;
   p2.W = P->post2; p2.ldw = p->Q; p2.out_part = gat<float>(ws, p->oLGP); p2.K = p->Cp; p2.N = p->Q; p2.KSL = 32;
-  SampleK sm;
-  sm.logits = gat<float>(ws, p->oLOG); sm.Q = p->Q; sm.B = p->B;
-  sm.log_part = p2.out_part; sm.parts = p->ks_lg; sm.bias = P->post2_b;
-  sm.step = gat<long long>(ws, p->oSTEP); sm.code = gat<int>(ws, p->oCODE);
-  sm.teacher = gat<int>(ws, p->oTEACH); sm.n_teacher = p->n_teacher; sm.samples = gat<int>(ws, p->oSAMP);
-  sm.wav = gat<float>(ws, p->oWAV); sm.max_steps = p->max_steps; sm.seed = p->seed;
-  const dim3 gsk((sk.N + 63) / 64, p->ks_skip), gp1((p1.N + 63) / 64, (p1.K + 31) / 32), gp2((p2.N + 63) / 64, (p2.K + 31) / 32);
-  const size_t sample_lds = 4 * (size_t)p->Q;
-  if (p->trace) {   // GEMV stamps after the wave kernel's: [skip | post1 | post2] × 8
+  DrawK& d = c.draw;
+  d.part = p2.out_part; d.parts = p->ks_lg; d.bias = P->post2_b; d.Q = p->Q; d.B = p->B;
+  d.logits = gat<float>(ws, p->oLOG); d.samples = gat<int>(ws, p->oSAMP); d.wav = gat<float>(ws, p->oWAV);
+  d.max_steps = p->max_steps; d.teacher = gat<int>(ws, p->oTEACH); d.n_teacher = p->n_teacher; d.seed = p->seed;
+  d.code = gat<int>(ws, p->oCODE);
+  const dim3 gp1((p1.N + 63) / 64, (p1.K + 31) / 32), gp2((p2.N + 63) / 64, (p2.K + 31) / 32);
+  if (p->trace) {   // GEMV stamps after the wave kernel's: [unused | post1 | post2] × 8
     long long* tb = gat<long long>(ws, p->oTRACE) + 2 * p->L + 8;
-    sk.trace = tb; p1.trace = tb + 8; p2.trace = tb + 16;
+    p1.trace = tb + 8; p2.trace = tb + 16;
   }
+  // per step: gen_wave (chains + skip helpers; from the second step of the run on, it first
+  // draws the previous step), post1, post2; the run's last step is drawn by gen_sample
   for (int i = 0; i < n_steps; ++i) {
-    gen_wave_kernel<<<p->B, 512, 0, st>>>(c);
-    gen_gemv_kernel<<<gsk, 256, 0, st>>>(sk);
+    c.fuse_draw = i > 0;
+    gen_wave_kernel<<<p->B + p->ks_skip, 512, 0, st>>>(c);
     gen_gemv_kernel<<<gp1, 256, 0, st>>>(p1);
     gen_gemv_kernel<<<gp2, 256, 0, st>>>(p2);
-    gen_sample_kernel<<<p->B, 256, sample_lds, st>>>(sm);
+    LBWN_CHECK_LAUNCH();
+  }
+  if (n_steps > 0) {
+    gen_sample_kernel<<<p->B, 64, 0, st>>>(c.draw, c.step);
     LBWN_CHECK_LAUNCH();
   }
   return 0;

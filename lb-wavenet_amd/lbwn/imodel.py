@@ -144,9 +144,17 @@ class WaveNetGen:
             self.build_graph(gen_sz)
         self.init_buffers(gc_ids)
         self.step(int(gen_sz))
+        self.check_status()
         n_out = (int(gen_sz) // self.chunk_sz) * self.chunk_sz
         wav = self.tensor('wav').view(self.batch_sz, self.max_steps)[:, :n_out]
         return int(gen_sz), wav, int(gen_sz) % self.chunk_sz
+
+    def check_status(self):
+        """Raise if a skip helper's granule poll timed out (status 5): the step's skip sum, and
+        every draw after it, would be wrong."""
+        s = int(self.tensor('status', torch.int32).item())
+        if s != 0:
+            raise RuntimeError('generation status %d: a skip-helper hand-off timed out' % s)
 
     def samples(self):
         return self.tensor('samples', torch.int32).view(self.batch_sz, self.max_steps)
