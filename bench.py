@@ -90,17 +90,29 @@ def gen_bytes_per_step(arch, B):
     return w + B * per_stream
 
 
-def bench_gen(net, arch, B=10, seconds=3.0, sr=16000, chunk=1000):
-    """imodel.py cached generation, arch3, B=10, 3 s @ 16 kHz (BASELINE configs[2]), graph
-    replay of chunk-sized step sequences; weights = the benchmark net's."""
+def _gen(net, arch, B, chunk, env=None):
     import torch
     from lbwn.imodel import WaveNetGen
-    g = WaveNetGen(arch['n_blocks'], arch['n_block_layers'], arch['n_quant'], arch['n_res'], arch['n_dil'],
-                   arch['n_skip'], arch['n_post'], arch['n_gc_embed'], arch['n_gc_category'], arch['use_bias'],
-                   B, chunk, None, seed=1, graph=True)
-    g.load_params(net)
-    n = int(seconds * sr)
-    g.build_graph(n)
+    old = {k: os.environ.get(k) for k in (env or {})}
+    os.environ.update(env or {})
+    try:
+        g = WaveNetGen(arch['n_blocks'], arch['n_block_layers'], arch['n_quant'], arch['n_res'], arch['n_dil'],
+                       arch['n_skip'], arch['n_post'], arch['n_gc_embed'], arch['n_gc_category'], arch['use_bias'],
+                       B, chunk, None, seed=1, graph=True)
+        g.load_params(net)
+        return g
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _gen_rate(g, arch, B, n, chunk):
+    """us per step over n steps (graph replay of chunk-step runs), after a warm chunk."""
+    import torch
+    g.build_graph(n + chunk)
     gc = [1 + b % max(1, arch['n_gc_category']) for b in range(B)] if arch['n_gc_embed'] else None
     g.init_buffers(gc)
     g.step(chunk)   # capture + warm
@@ -111,15 +123,65 @@ def bench_gen(net, arch, B=10, seconds=3.0, sr=16000, chunk=1000):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     g.check_status()
+    return dt
+
+
+def gen_layer_latency(net, arch, B):
+    """Median wall time of one layer of the dependent per-stream chain (conv -> gate ->
+    residual), from the persistent kernel's in-kernel stamps (LBWN_GEN_TRACE plan)."""
+    import torch
+    from lbwn.arch import n_layers
+    g = _gen(net, arch, B, 50, env={'LBWN_GEN_TRACE': '1'})
+    if not (g.build_graph(400) and g.persistent):
+        return None
+    g.init_buffers([1 + b % max(1, arch['n_gc_category']) for b in range(B)] if arch['n_gc_embed'] else None)
+    g.step(300)
+    torch.cuda.synchronize()
+    tr = g.tensor('trace', torch.int64).cpu().numpy().astype(np.int64)
+    L = n_layers(arch)
+    lay = np.diff(np.concatenate([[tr[0]], tr[8:8 + L]])) / 100.0   # wall_clock64: 100 MHz
+    return float(np.median(lay))
+
+
+def bench_gen(net, arch, B=10, seconds=3.0, sr=16000, chunk=1000, sweep=(16, 64, 256)):
+    """imodel.py cached generation, arch3, B=10, 3 s @ 16 kHz (BASELINE configs[2]), graph
+    replay of chunk-sized step sequences; weights = the benchmark net's.  Also a B sweep and
+    the step time against the latency floor of its dependent chain."""
+    from lbwn.arch import n_layers
+    n = int(seconds * sr)
+    g = _gen(net, arch, B, chunk)
+    dt = _gen_rate(g, arch, B, n, chunk)
+    us = dt / n * 1e6
     bps = gen_bytes_per_step(arch, B)
-    return {'metric': 'cached autoregressive gen audio samples/s (B streams x steps / wall)',
-            'value': B * n / dt, 'unit': 'audio samples/s', 'steps': n, 'batch': B, 'wall_s': dt,
-            'us_per_step': dt / n * 1e6, 'config': 'imodel.py cached gen, par/arch3.json, B=%d, %.0f s @ %d Hz, '
-                                                   'chunk %d, hipGraph replay' % (B, seconds, sr, chunk),
-            'roofline': {'bound': 'hbm', 'bytes_per_step': bps, 'achieved': bps * n / dt / 1e9, 'peak': HBM_PEAK / 1e9,
-                         'unit': 'GB/s', 'frac': bps * n / dt / HBM_PEAK,
-                         'note': 'weights are L2/MALL-resident across steps; the step is a 55-stage dependent '
-                                 'chain, latency- not bandwidth-bound'}}
+    out = {'metric': 'cached autoregressive gen audio samples/s (B streams x steps / wall)',
+           'value': B * n / dt, 'unit': 'audio samples/s', 'steps': n, 'batch': B, 'wall_s': dt,
+           'us_per_step': us, 'form': 'persistent (one launch per chunk)' if g.persistent else 'per-step launches',
+           'config': 'imodel.py cached gen, par/arch3.json, B=%d, %.0f s @ %d Hz, chunk %d, hipGraph replay'
+                     % (B, seconds, sr, chunk)}
+    # latency roofline: a step is L dependent layers (conv -> gate -> residual on one CU per
+    # stream) plus the head's hand-offs; the floor counts the chain alone at its measured
+    # per-layer latency (stamps), so frac = the share of the step the unavoidable chain takes
+    t_layer = gen_layer_latency(net, arch, B)
+    L = n_layers(arch)
+    if t_layer is not None:
+        out['roofline'] = {'bound': 'latency', 'unit': 'us/step', 'achieved': us, 'peak': L * t_layer,
+                           'frac': L * t_layer / us, 'per_layer_us': t_layer,
+                           'note': 'peak = %d layers x the measured per-layer chain latency; the rest of the step is '
+                                   'the head (skip tail, skip all-gather, post-net, partial-logit gather, draw)' % L}
+    out['roofline_hbm'] = {'bound': 'hbm', 'bytes_per_step': bps, 'achieved': bps * n / dt / 1e9, 'peak': HBM_PEAK / 1e9,
+                           'unit': 'GB/s', 'frac': bps * n / dt / HBM_PEAK,
+                           'note': 'weights are L2/MALL- and LDS/register-resident across steps: not bandwidth-bound'}
+    rows = []
+    for Bs in sweep:
+        ns = 2000
+        gs = _gen(net, arch, Bs, 500)
+        dts = _gen_rate(gs, arch, Bs, ns, 500)
+        bs = gen_bytes_per_step(arch, Bs)
+        rows.append({'batch': Bs, 'us_per_step': dts / ns * 1e6, 'samples_per_s': Bs * ns / dts,
+                     'weight_and_state_GB_per_s': bs * ns / dts / 1e9,
+                     'form': 'persistent' if gs.persistent else 'per-step'})
+    out['sweep'] = rows
+    return out
 
 
 def _cores():

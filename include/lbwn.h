@@ -117,7 +117,8 @@ void lbwn_gen_plan_destroy(lbwn_gen_plan* plan);
 size_t lbwn_gen_workspace_bytes(const lbwn_gen_plan* plan);
 /* "samples" int32 [B][max_steps] (drawn µ-law codes), "wav" fp32 [B][max_steps]
  * (mu_decode of the draws, imodel.py:181-182), "logits" [B][Q] (last step), "step" int64,
- * "rings" (lookback state, SAVE layout), "teacher" int32. */
+ * "rings" (lookback state, SAVE layout), "teacher" int32, "status" int32 (0; 5 when a persistent
+ * hand-off timed out). */
 int lbwn_gen_tensor(const lbwn_gen_plan* plan, const char* name, size_t* offset, size_t* bytes);
 /* Reset the state (zero lookback rings = imodel's zero-initialised buffers, step 0 input =
  * zero vector), load the teacher codes (device int32, may be NULL) and GC ids (device
@@ -128,8 +129,13 @@ int lbwn_gen_tensor(const lbwn_gen_plan* plan, const char* name, size_t* offset,
 int lbwn_gen_start(lbwn_gen_plan* plan, const lbwn_params* params, void* workspace, const int* gc_ids,
                    const int* teacher, int64_t n_teacher, uint64_t seed, int pre_bias, void* stream);
 /* Generate n_steps more samples for every stream (the tf.while_loop body, imodel.py:214-272).
- * Device-resident step counter: the launches are graph-capturable and replayable. */
+ * Device-resident step counter: the launches are graph-capturable and replayable.  Persistent
+ * plans (lbwn_gen_is_persistent) run the whole call as ONE launch whose blocks must all be
+ * resident: nothing else may occupy the device's CUs meanwhile. */
 int lbwn_gen_run(lbwn_gen_plan* plan, const lbwn_params* params, void* workspace, int n_steps, void* stream);
+/* 1 when the plan runs the persistent one-launch form (B <= 32 and the layer/head sizes fit;
+ * LBWN_GEN_PERSIST=0 at plan creation selects the per-step launches), else 0. */
+int lbwn_gen_is_persistent(const lbwn_gen_plan* plan);
 
 /* ---- fine-grained kernels (parity tests, custom drivers) ------------------------------ */
 /* ops.mu_encode_np (ops.py:23-28, tf32=0, float64 math) / ops.mu_encode (ops.py:4-9, tf32=1) */

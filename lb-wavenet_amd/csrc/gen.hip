@@ -1,20 +1,20 @@
 // Cached single-step autoregressive generation (imodel.py:61-272).
 //
-// Per generated sample, all state stays on device so a chunk of steps can be captured in a
-// hipGraph and replayed: the step counter, the per-layer lookback rings (the generation
-// form of the D-separation cache: layer l keeps its last d inputs, slot t mod d, replacing
-// imodel's shift-by-chunk buffers imodel.py:88-98, :190-207), the next input code, the
-// teacher vector and a counter-based RNG.  One step = three launches:
-//   gen_wave     one workgroup per stream: four compute waves draw the PREVIOUS step (Σ post2
-//                partials + b2, inverse-CDF with u = hash(seed, stream, step), µ-law decode, next
-//                input = teacher[t] or the draw: imodel.py:167-187, :260-269), then run PRE row
-//                (+bias), 50 × [dilated conv, gate, residual] while four loader waves stream the
-//                per-layer weight images into an LDS ring by LDS-DMA, several layers ahead.  Each
-//                z_l leaves as tagged 8-byte granules; skip helper blocks of the same launch
-//                (layer pairs of SKIPcat) poll them and accumulate the skip sum as the chain runs
-//   gen_gemv × 2 K-split row-vector products with deterministic partial sums:
-//                h = relu(relu(Σ skip partials + Σb)·POST1 + b1), logits partials = h·POST2
-// (the last step of a run is drawn by gen_sample, one wave per stream, same draw code)
+// All state stays on device, so a chunk of steps can be captured in a hipGraph and replayed:
+// the step counter, the per-layer lookback rings (the generation form of the D-separation
+// cache: layer l keeps its last d inputs, slot t mod d, replacing imodel's shift-by-chunk
+// buffers imodel.py:88-98, :190-207), the next input code, the teacher vector and a
+// counter-based RNG.  Two execution forms, chosen at plan creation:
+//   persistent (B <= 32, the default there): ONE launch per run, gen_persist_kernel — chain
+//     blocks (one per stream) and 32 head blocks hand z, the skip vector and the partial logits
+//     to each other as tagged granules; weights of the head stay in registers for the run
+//   per step (any B): gen_wave (one workgroup per stream: PRE row (+bias), 50 × [dilated conv,
+//     gate, residual] while four loader waves stream the per-layer weight images into an LDS
+//     ring by LDS-DMA), gen_gemv × 3 (K-split row-vector products with deterministic partial
+//     sums: skip = z_cat·SKIPcat, h = relu(relu(skip + Σb)·POST1 + b1), logits = h·POST2) and
+//     gen_sample (Σ partials + b2, the draw)
+// Both draw with the same wave-level inverse-CDF code: u = hash(seed, stream, step), µ-law
+// decode, next input = teacher[t] or the draw (imodel.py:167-187, :260-269).
 #include <math.h>
 #include <string.h>
 
@@ -67,191 +67,12 @@ constexpr int G_LDS = G_NS * G_SLOT + (G_MAXL + 2) * 32 + 4 * 32 + 2 * 32;   // 
 static_assert(4 * G_PIECES * 256 == GI_WR, "image pieces");
 static_assert(G_LDS * 4 <= 160 * 1024, "LDS");
 
-// ---- the draw (imodel.py:167-187, :260-269) ----------------------------------------------
-// logits[c] = Σ_p part[p][b][c] + bias[c] (fixed order), then the first k with
-// cumsum(e)[k] > u·Σe, e = exp(logits - max), u = hash(seed, stream, step).  Wave-level only
-// (lane = a contiguous run of ceil(Q/64) codes, shuffles, no workgroup barrier), so the four
-// compute waves of a gen_wave block all draw the same code without exchanging it, and the
-// standalone gen_sample_kernel (one wave per stream) runs the identical instruction sequence
-// (oracle/wavenet_ref.py sample_from_logits restates the transform).
-struct DrawK {
-  const float* part; int parts; const float* bias;   // partials [parts][B][Q]
-  int Q, B;
-  float* logits; int* samples; float* wav; long long max_steps;
-  const int* teacher; long long n_teacher; unsigned long long seed; int* code;
-};
-
-LBWN_DEV uint64_t splitmix(uint64_t seed, uint64_t stream, uint64_t step) {
-  uint64_t z = seed * 0x9E3779B97F4A7C15ULL + (stream << 32) + step + 0x632BE59BD9B4E019ULL;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
-  return z ^ (z >> 31);
-}
-
-// returns the next input code of stream b after step t (the teacher's or the draw); the
-// writing wave stores logits, the sample, its µ-law decode and code[b]
-template <int MP>
-LBWN_DEV int draw_wave(const DrawK& a, int b, long long t, bool write) {
-  const int lane = threadIdx.x & 63, Q = a.Q;
-  const int per = (Q + 63) >> 6, c0 = lane * per;
-  float v[MP], bv[MP];
-#pragma unroll
-  for (int j = 0; j < MP; ++j) {
-    v[j] = 0.f;
-    bv[j] = a.bias ? a.bias[min(c0 + j, Q - 1)] : 0.f;
-  }
-  constexpr int CH = MP > 4 ? 8 : 16;
-  for (int q0 = 0; q0 < a.parts; q0 += CH) {   // every load of a chunk (and the bias) issued before the first add
-    float x[MP][CH];
-#pragma unroll
-    for (int j = 0; j < MP; ++j)
-#pragma unroll
-      for (int i = 0; i < CH; ++i)
-        x[j][i] = a.part[((long)min(q0 + i, a.parts - 1) * a.B + b) * Q + min(c0 + j, Q - 1)];
-#pragma unroll
-    for (int j = 0; j < MP; ++j)
-#pragma unroll
-      for (int i = 0; i < CH; ++i) v[j] += (q0 + i < a.parts) ? x[j][i] : 0.f;
-  }
-  float mx = -INFINITY;
-#pragma unroll
-  for (int j = 0; j < MP; ++j) {
-    const bool ok = j < per && c0 + j < Q;
-    if (a.bias) v[j] += bv[j];
-    if (ok) mx = fmaxf(mx, v[j]);
-    if (ok && write) a.logits[(long)b * Q + c0 + j] = v[j];
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-  float e[MP], loc = 0.f;
-#pragma unroll
-  for (int j = 0; j < MP; ++j) {
-    e[j] = (j < per && c0 + j < Q) ? expf(v[j] - mx) : 0.f;
-    loc += e[j];
-  }
-  float incl = loc;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float s = __shfl_up(incl, o);
-    if (lane >= o) incl += s;
-  }
-  const float total = __shfl(incl, 63);
-  const float excl = incl - loc;
-  const uint64_t h = splitmix(a.seed, (uint64_t)b, (uint64_t)t);
-  const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
-  const float target = u * total;
-  int found = Q;   // the lane whose run contains the crossing point
-  if (excl <= target && target < incl) {
-    float run = excl;
-#pragma unroll
-    for (int j = 0; j < MP; ++j) {
-      if (j < per && c0 + j < Q && found == Q) {
-        run += e[j];
-        if (run > target) found = c0 + j;
-      }
-    }
-    if (found == Q) found = min(c0 + per, Q) - 1;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) found = min(found, __shfl_xor(found, o));
-  if (found >= Q) found = Q - 1;
-  const int next = (t < a.n_teacher) ? a.teacher[t] : found;   // imodel.py:260-269
-  if (write && lane == 0) {
-    if (t < a.max_steps) {
-      a.samples[(long)b * a.max_steps + t] = found;
-      const float mu = (float)(Q - 1), inv = 1.f / mu;               // ops.py:12-20
-      const float aa = (2.f * (float)found - 1.f) * inv - 1.f;
-      const float sg = aa > 0.f ? 1.f : (aa < 0.f ? -1.f : 0.f);
-      a.wav[(long)b * a.max_steps + t] = sg * (powf(1.f + mu, fabsf(aa)) - 1.f) * inv;
-    }
-    a.code[b] = next;
-  }
-  return next;
-}
-
 struct WaveK {
   const float* pre; const float* pre_b; const float* img; const float* gc_proj;
-  float* rings; const long long* step; const int* code;
+  float* rings; float* zcat; const long long* step; const int* code;
   int B, L, nbl, Cr, Cd, pre_bias;
-  // z_l of every stream as {z, tag = step+1} granules [B][L][32] (one 8-B sc1 store each), read
-  // by the skip helper blocks of the same launch (blockIdx >= B): helper j owns layers
-  // [LG·j, LG·j+LG) of SKIPcat [L·Cd][Cs] and writes its partial skip sum [j][B][Cs]
-  unsigned long long* zg; const float* skipw; float* skip_part; int Cs, LG;
-  int* status;
-  // fused draw: this launch first draws step t-1 of its stream (the previous step's post2
-  // partials), so the sampler launch and its boundary leave the per-step chain
-  int fuse_draw; DrawK draw;
   long long* trace;   // non-null (LBWN_GEN_TRACE set at plan creation): stream 0's cycle stamps
 };
-
-constexpr long long G_SPIN_TIMEOUT = 400000000LL;   // wall_clock64 ticks (100 MHz) = 4 s
-
-// skip helper j: per group of 16 streams and per owned layer, poll the 16×Cd z granules (one
-// per thread), stage them in LDS, and accumulate Σ_k z[b][k]·SKIP[l·Cd+k][n] for column n =
-// threadIdx.x; the layer's weight column is loaded before the poll so its latency hides there
-LBWN_DEV void skip_helper(const WaveK& a, int j, long long t, float* sm) {
-  const int tid = threadIdx.x, L = a.L, Cd = a.Cd, Cs = a.Cs, B = a.B;
-  const int l0 = j * a.LG, l1 = min(L, l0 + a.LG);
-  const unsigned tag = (unsigned)(t + 1);
-  const int n = min(tid, Cs - 1), gb = tid >> 5, gk = tid & 31;
-  for (int g0 = 0; g0 < B; g0 += 16) {
-    const int nb = min(16, B - g0);
-    float acc[16];
-#pragma unroll
-    for (int bb = 0; bb < 16; ++bb) acc[bb] = 0.f;
-    int buf = 0;
-    for (int l = l0; l < l1; ++l, buf ^= 1) {
-      float w[32];
-      const float* S = a.skipw + (long)l * Cd * Cs + n;
-#pragma unroll
-      for (int k = 0; k < 32; ++k) w[k] = S[(long)min(k, Cd - 1) * Cs];
-#pragma unroll
-      for (int k = 0; k < 32; ++k)
-        if (k >= Cd) w[k] = 0.f;
-      float zv = 0.f;
-      if (gb < nb && gk < Cd) {
-        const unsigned long long* gp = a.zg + ((long)(g0 + gb) * L + l) * 32 + gk;
-        long long ts = 0;
-        for (;;) {
-          const unsigned long long g = __hip_atomic_load(gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((unsigned)(g >> 32) == tag) { zv = __uint_as_float((unsigned)g); break; }
-          const long long now = wall_clock64();
-          if (ts == 0) ts = now;
-          else if (now - ts > G_SPIN_TIMEOUT) {
-            __hip_atomic_store(a.status, 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-        }
-      }
-      const bool trh = a.trace && tid == 0 && blockIdx.x == gridDim.x - 1 && l - l0 < 2 && g0 == 0;
-      if (trh) a.trace[2 * L + 12 + 2 * (l - l0)] = wall_clock64();
-      float* ZS = sm + buf * 512;   // [16 streams][32]; double-buffered: one barrier per layer
-      ZS[tid] = zv;
-      __syncthreads();
-#pragma unroll
-      for (int bb = 0; bb < 16; ++bb) {
-        if (bb < nb) {
-          const floatx4* zr = (const floatx4*)(ZS + bb * 32);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const floatx4 z4 = zr[q];
-            acc[bb] = fmaf(z4[0], w[4 * q], acc[bb]);
-            acc[bb] = fmaf(z4[1], w[4 * q + 1], acc[bb]);
-            acc[bb] = fmaf(z4[2], w[4 * q + 2], acc[bb]);
-            acc[bb] = fmaf(z4[3], w[4 * q + 3], acc[bb]);
-          }
-        }
-      }
-    }
-    if (a.trace && tid == 0 && blockIdx.x == gridDim.x - 1 && g0 == 0) a.trace[2 * L + 13] = wall_clock64();
-    if (tid < Cs) {
-#pragma unroll
-      for (int bb = 0; bb < 16; ++bb)
-        if (bb < nb) a.skip_part[((long)j * B + g0 + bb) * Cs + tid] = acc[bb];
-    }
-  }
-}
 
 LBWN_DEV float dot4(const floatx4& w, const floatx4& x, float acc) {
   acc = fmaf(w[0], x[0], acc);
@@ -284,14 +105,6 @@ __global__ __launch_bounds__(512) void gen_wave_kernel(WaveK a) {
   float* XP = sm + G_NS * G_SLOT;    // [L (+2)][32] dilated taps of this step
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, b = blockIdx.x, L = a.L;
   const long t = *a.step;
-
-  if (b >= a.B) {   // ---- skip helper blocks
-    const bool trh = a.trace && threadIdx.x == 0 && b == gridDim.x - 1;
-    if (trh) a.trace[2 * L + 10] = wall_clock64();
-    skip_helper(a, b - a.B, t, sm);
-    if (trh) a.trace[2 * L + 11] = wall_clock64();
-    return;
-  }
 
   if (wid >= 4) {   // ---- loader waves
     const int lw = wid - 4;
@@ -363,25 +176,16 @@ __global__ __launch_bounds__(512) void gen_wave_kernel(WaveK a) {
   float* XW = XP + (G_MAXL + 2) * 32 + 32 * w;   // this wave's copy of the layer input
   float* Z = XP + (G_MAXL + 2) * 32 + 128;       // z double buffer [2][32]
   const bool tr = a.trace && b == 0 && w == 0 && lane == 0;
-  if (tr) { a.trace[0] = clock64(); a.trace[2 * L + 8] = wall_clock64(); }
-  long long* trs = (a.trace && w == 0 && lane == 0) ? a.trace + 2 * L + 40 + 3 * b : nullptr;
-  if (trs) trs[0] = wall_clock64();
-  // step input: PRE row of the previous draw (+ PRE_BIAS); the zero vector at step 0.  With
-  // fuse_draw every compute wave draws step t-1 itself (wave 0 writes), while the loader waves'
-  // first taps and weight slots are in flight
-  int code;
-  if (a.fuse_draw)
-    code = a.draw.Q > 256 ? draw_wave<8>(a.draw, b, t - 1, w == 0) : draw_wave<4>(a.draw, b, t - 1, w == 0);
-  else
-    code = a.code[b];
+  if (tr) a.trace[0] = clock64();
+  // step input: PRE row of the previous draw (+ PRE_BIAS); the zero vector at step 0
   float x = 0.f;    // x[rc] of the current layer input
   if (rc < Cr) {
+    const int code = a.code[b];
     if (code >= 0) x = a.pre[(long)code * Cr + rc];
     if (a.pre_bias && a.pre_b) x += a.pre_b[rc];
   }
   if (lane < 32) XW[rc] = x;
   if (tr) a.trace[1] = clock64();
-  if (trs) trs[1] = wall_clock64();
   const int xin_off = kq < 2 ? 16 * kq : 16 * (kq - 2);
   long roff = 0;   // ring offset of layer l
   int bl = 0;      // l % nbl
@@ -415,10 +219,7 @@ __global__ __launch_bounds__(512) void gen_wave_kernel(WaveK a) {
     float* Zl = Z + (l & 1) * 32;
     if (lead) {
       Zl[ch] = z;
-      if (ch < Cd)   // granule for the skip helpers: fire-and-forget, no wait on the chain
-        __hip_atomic_store(a.zg + ((long)b * L + l) * 32 + ch,
-                           ((unsigned long long)(unsigned)(t + 1) << 32) | __float_as_uint(z), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+      if (ch < Cd) a.zcat[(long)b * L * Cd + (long)l * Cd + ch] = z;
     }
     if (tr) a.trace[4 + 2 * l] = clock64();
     lds_barrier();   // barrier l: z_l complete; slot l+1 landed
@@ -440,8 +241,6 @@ __global__ __launch_bounds__(512) void gen_wave_kernel(WaveK a) {
     wave_sync();
     if (tr) a.trace[5 + 2 * l] = clock64();
   }
-  if (tr) a.trace[2 * L + 9] = wall_clock64();
-  if (trs) trs[2] = wall_clock64();
 }
 
 // per-layer weight image in the compute waves' lane order (reference layouts in, GIMG floats
@@ -605,12 +404,572 @@ __global__ __launch_bounds__(256) void gen_gemv_kernel(GemvK a) {
   if (a.trace && tid == 0 && last) a.trace[7] = wall_clock64();
 }
 
-// the step's draw when it is not fused into the next gen_wave launch (the last step of a run):
-// one wave per stream, t = *step - 1 (post1 advanced the counter)
+// ---- the draw (imodel.py:167-187, :260-269) ----------------------------------------------
+// Inverse-CDF draw of softmax(logits): the first k with cumsum(e)[k] > u·Σe, e = exp(logits -
+// max), u = hash(seed, stream, step) (oracle/wavenet_ref.py sample_from_logits restates the
+// transform).  Wave-level only — lane = a contiguous run of ceil(Q/64) codes, shuffles, no
+// workgroup barrier — so every wave that calls it with the same logits draws the same code.
+struct DrawK {
+  const float* part; int parts; const float* bias;   // logits = Σ part[p][b][:] + bias (per-step path)
+  int Q, B;
+  float* logits; int* samples; float* wav; long long max_steps;
+  const int* teacher; long long n_teacher; unsigned long long seed; int* code;
+};
+
+LBWN_DEV uint64_t splitmix(uint64_t seed, uint64_t stream, uint64_t step) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ULL + (stream << 32) + step + 0x632BE59BD9B4E019ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+// v[j] = logit of code lane·per + j.  Returns the next input code of stream b after step t (the
+// teacher's or the draw); the writing wave stores logits, the sample, its µ-law decode, code[b].
+template <int MP>
+LBWN_DEV int draw_core(float (&v)[MP], const DrawK& a, int b, long long t, bool write) {
+  const int lane = threadIdx.x & 63, Q = a.Q;
+  const int per = (Q + 63) >> 6, c0 = lane * per;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < MP; ++j) {
+    const bool ok = j < per && c0 + j < Q;
+    if (ok) mx = fmaxf(mx, v[j]);
+    if (ok && write) a.logits[(long)b * Q + c0 + j] = v[j];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  float e[MP], loc = 0.f;
+#pragma unroll
+  for (int j = 0; j < MP; ++j) {
+    e[j] = (j < per && c0 + j < Q) ? expf(v[j] - mx) : 0.f;
+    loc += e[j];
+  }
+  float incl = loc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float s = __shfl_up(incl, o);
+    if (lane >= o) incl += s;
+  }
+  const float total = __shfl(incl, 63);
+  const float excl = incl - loc;
+  const uint64_t h = splitmix(a.seed, (uint64_t)b, (uint64_t)t);
+  const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+  const float target = u * total;
+  int found = Q;   // the lane whose run contains the crossing point
+  if (excl <= target && target < incl) {
+    float run = excl;
+#pragma unroll
+    for (int j = 0; j < MP; ++j) {
+      if (j < per && c0 + j < Q && found == Q) {
+        run += e[j];
+        if (run > target) found = c0 + j;
+      }
+    }
+    if (found == Q) found = min(c0 + per, Q) - 1;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) found = min(found, __shfl_xor(found, o));
+  if (found >= Q) found = Q - 1;
+  const int next = (t < a.n_teacher) ? a.teacher[t] : found;   // imodel.py:260-269
+  if (write && lane == 0) {
+    if (t < a.max_steps) {
+      a.samples[(long)b * a.max_steps + t] = found;
+      const float mu = (float)(Q - 1), inv = 1.f / mu;               // ops.py:12-20
+      const float aa = (2.f * (float)found - 1.f) * inv - 1.f;
+      const float sg = aa > 0.f ? 1.f : (aa < 0.f ? -1.f : 0.f);
+      a.wav[(long)b * a.max_steps + t] = sg * (powf(1.f + mu, fabsf(aa)) - 1.f) * inv;
+    }
+    a.code[b] = next;
+  }
+  return next;
+}
+
+// per-step path: logits from the post2 GEMV's K-slice partials, Σ in slice order + bias
+template <int MP>
+LBWN_DEV int draw_wave(const DrawK& a, int b, long long t, bool write) {
+  const int lane = threadIdx.x & 63, Q = a.Q;
+  const int per = (Q + 63) >> 6, c0 = lane * per;
+  float v[MP], bv[MP];
+#pragma unroll
+  for (int j = 0; j < MP; ++j) {
+    v[j] = 0.f;
+    bv[j] = a.bias ? a.bias[min(c0 + j, Q - 1)] : 0.f;
+  }
+  constexpr int CH = MP > 4 ? 8 : 16;
+  for (int q0 = 0; q0 < a.parts; q0 += CH) {   // every load of a chunk (and the bias) issued before the first add
+    float x[MP][CH];
+#pragma unroll
+    for (int j = 0; j < MP; ++j)
+#pragma unroll
+      for (int i = 0; i < CH; ++i)
+        x[j][i] = a.part[((long)min(q0 + i, a.parts - 1) * a.B + b) * Q + min(c0 + j, Q - 1)];
+#pragma unroll
+    for (int j = 0; j < MP; ++j)
+#pragma unroll
+      for (int i = 0; i < CH; ++i) v[j] += (q0 + i < a.parts) ? x[j][i] : 0.f;
+  }
+  if (a.bias) {
+#pragma unroll
+    for (int j = 0; j < MP; ++j) v[j] += bv[j];
+  }
+  return draw_core<MP>(v, a, b, t, write);
+}
+
+// the per-step path's sampler: one wave per stream; the step counter was advanced by this
+// step's skip GEMV, so this step is *step - 1
 __global__ __launch_bounds__(64) void gen_sample_kernel(DrawK a, const long long* step) {
   const long long t = *step - 1;
   if (a.Q > 256) draw_wave<8>(a, blockIdx.x, t, true);
   else draw_wave<4>(a, blockIdx.x, t, true);
+}
+
+constexpr long long G_SPIN_TIMEOUT = 400000000LL;   // wall_clock64 ticks (100 MHz) = 4 s
+
+// ---- persistent generation: one launch per run (B <= 32) --------------------------------
+// Roles (one 512-thread workgroup per CU, all resident: B + P_NH <= CUs):
+//   chain block b < B   per step: draw the previous step (gather the P_NH partial-logit
+//                       granules of stream b, Σ + b2, wave-level draw), PRE row, 50 layers as in
+//                       gen_wave (LDS-DMA ring continuous across steps; the next step's taps are
+//                       DMA'd right after the last layer), z_l published as tagged granules
+//   head block m < P_NH owns skip columns [16m, 16m+16), post1 columns [16m, 16m+16) and the
+//                       same post2 rows (POST1 / POST2 slices held in registers for the run):
+//                       A. accumulates its skip columns layer by layer as the z granules arrive
+//                          (SKIP slice streamed from L2 one layer ahead);
+//                       B. publishes them, gathers the whole skip vector, relu(· + Σb);
+//                       C. h = relu(skip·POST1[:, cols] + b1), partial logits h·POST2[rows, :]
+//                          published as granules for the chain blocks' draw.
+// Every hand-off is an 8-byte {value, tag = step + 1} granule written by one sc1 store and polled
+// with relaxed agent-scope loads (no flag, no fence: MI355X_MICROARCH.md § visibility, R2);
+// single-buffered, because no producer can run a step ahead of its slowest consumer (each
+// stage waits on the previous one through the whole ring of roles).  Every spin is bounded
+// (status 5).  Three hops per step (z tail, skip all-gather, logit partials) replace the
+// per-step path's four launch boundaries and its weight re-fetches.
+constexpr int P_NH = 32;     // head blocks
+constexpr int P_MAXB = 16;   // streams (beyond 16 the per-step form is faster: measured 90 vs 87 us at B 32 / 64)
+constexpr int P_MAXL = 236;  // layers (the draw's two half-sums use tap-table rows 240..255)
+constexpr int P_DLROW = 240;
+constexpr int P_LA = 8;      // layers per head round (phase A)
+
+struct PersistK {
+  const float* pre; const float* pre_b; const float* img; const float* gc_proj;
+  float* rings; long long* step; const int* code_in;
+  int B, L, nbl, Cr, Cd, pre_bias, n_steps;
+  unsigned long long* zg;   // [B][L][32] z granules
+  int Cs, Cp, Q;
+  const float* skipw; const float* bsum; const float* post1; const float* post1_b; const float* post2;
+  unsigned long long* sg;   // [B][Cs] skip granules
+  unsigned long long* lg;   // [P_NH][B][Q] partial-logit granules
+  DrawK draw;               // outputs; draw.bias = b2
+  int* status;
+  long long* trace;         // wall stamps of the run's last step (tools/gen_trace.py), or null
+};
+
+// poll granules base[off + i·stride], i < nv (N at most; the rest re-read granule nv-1), until
+// every tag matches; v[i] = payload.  base is wave-uniform and the index 32-bit, so each load
+// is one VGPR offset on an SGPR base.  After any timeout (status != 0) every sweep gives up at
+// once, so a failed hand-off drains the launch instead of waiting out each later spin.
+template <int N>
+LBWN_DEV void sweep(const unsigned long long* base, unsigned off, unsigned stride, int nv, unsigned tag, float (&v)[N],
+                    int* status) {
+  long long ts = 0;
+  const unsigned last = (unsigned)max(nv - 1, 0);
+  for (unsigned spins = 1;; ++spins) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const unsigned idx = off + min((unsigned)i, last) * stride;
+      const unsigned long long x = __hip_atomic_load(base + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v[i] = __uint_as_float((unsigned)x);
+      ok &= (unsigned)(x >> 32) == tag;
+    }
+    if (ok) return;
+    if ((spins & 31) == 0) {   // the clock and the status word cost a round trip each: not every retry
+      if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+      const long long now = wall_clock64();
+      if (ts == 0) ts = now;
+      else if (now - ts > G_SPIN_TIMEOUT) {
+        __hip_atomic_store(status, 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+LBWN_DEV void put_granule(unsigned long long* g, unsigned tag, float v) {
+  __hip_atomic_store(g, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ring slot DMA with sc1 (L2-served): a tap line this CU read d steps ago may still sit in its L1
+LBWN_DEV void dma4_sc1(const float* src, float* lds_dst) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 4, 0, 16);
+}
+
+LBWN_DEV void persist_chain(const PersistK& a, float* sm) {
+  float* RING = sm;                  // [G_NS][G_SLOT]
+  float* XP = sm + G_NS * G_SLOT;    // [L][32] dilated taps of this step
+  float* DL = XP + P_DLROW * 32;     // [2][256] half-sums of the partial logits of the step being drawn
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, b = blockIdx.x, L = a.L, n = a.n_steps;
+  const long long t0 = *a.step;
+  const long GT = (long)n * L;       // layers of the run, in order: global index g = s·L + l
+
+  if (wid >= 4) {   // ---- loader waves
+    const int lw = wid - 4;
+    const float* zeros = a.img + GI_WR + 128;
+    auto taps = [&](long long t) {   // as gen_wave (a), for step t
+      const int h = lane >> 5, c = lane & 31;
+      long roff = 0;
+      int bl = 0;
+      for (int q = 0; 2 * q < L; ++q) {
+        const int dE = 1 << bl;
+        const long roffO = roff + (long)dE * a.B * a.Cr;
+        const int blO = (bl + 1 == a.nbl) ? 0 : bl + 1;
+        const int dO = 1 << blO;
+        if ((q & 3) == lw) {
+          const int d = h ? dO : dE, l = 2 * q + h;
+          const float* src = (l < L && c < a.Cr)
+                                 ? a.rings + (h ? roffO : roff) + ((long)b * d + (t & (d - 1))) * a.Cr + c
+                                 : zeros + c;
+          dma4_sc1(src, XP + 2 * q * 32);
+        }
+        roff = roffO + (long)dO * a.B * a.Cr;
+        bl = (blO + 1 == a.nbl) ? 0 : blO + 1;
+      }
+    };
+    auto issue = [&](long g) {   // weights of global layer g into slot g mod G_NS
+      const int l = (int)(g % L);
+      const float* src = a.img + (long)l * GIMG;
+      float* dst = RING + (g % G_NS) * G_SLOT;
+#pragma unroll
+      for (int p = 0; p < G_PIECES; ++p) {
+        const int pc = lw * G_PIECES + p;
+        dma16(src + pc * 256 + lane * 4, dst + pc * 256);
+      }
+      const float* row = lw < 2 ? src + GI_WR + lw * 64
+                       : lw == 2 ? (a.gc_proj ? a.gc_proj + ((long)l * a.B + b) * 64 : zeros)
+                                 : zeros;
+      dma4(row + lane, dst + GI_WR + lw * 64);
+    };
+    taps(t0);
+    long issued = 0;
+    for (; issued < G_NS - 1 && issued < GT; ++issued) issue(issued);
+    auto gather_half = [&](long long t) {   // partial logits of heads 16..31 for code q
+      const int q = min((int)threadIdx.x - 256, a.Q - 1);
+      float v[P_NH / 2], sum = 0.f;
+      sweep<P_NH / 2>(a.lg, (unsigned)(((P_NH / 2) * a.B + b) * a.Q + q), (unsigned)(a.B * a.Q), P_NH / 2, (unsigned)t,
+                      v, a.status);
+#pragma unroll
+      for (int i = 0; i < P_NH / 2; ++i) sum += v[i];
+      DL[256 + q] = sum;
+    };
+    for (int s = 0; s < n; ++s) {
+      if (s > 0) {
+        gather_half(t0 + s);
+        lds_barrier();   // D: the previous step's logits are in DL
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();              // -1: taps and the first slot landed, every wave's XW written
+      for (int k = 0; k < L; ++k) {
+        const long G = (long)s * L + k;
+        // barrier G releases the residual of layer G and the conv of G+1: retire all but the
+        // slots younger than G+1
+        const long younger = (issued - 1) - (G + 1);
+        if (younger >= G_NS - 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G_DMA * (G_NS - 3)) : "memory");
+        else if (younger == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G_DMA * 2) : "memory");
+        else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G_DMA) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        if (issued < GT) issue(issued++);   // into the slot of layer G-1 (dead after barrier G)
+        if (k == L - 1 && s + 1 < n) taps(t0 + s + 1);   // the ring stores of step s landed (compute waves drained)
+      }
+    }
+    gather_half(t0 + n);
+    lds_barrier();   // D of the run's last draw
+    return;
+  }
+
+  // ---- compute waves
+  const int w = wid, Cr = a.Cr, Cd = a.Cd;
+  const int c = lane >> 3, sg = (lane >> 2) & 1, kq = lane & 3, kp = lane & 7;
+  const int ch = 8 * w + c, o = 32 * sg + ch;
+  const bool lead = kp == 0;
+  const int rc = lane & 31, rh = lane >> 5;
+  float* XW = XP + (G_MAXL + 2) * 32 + 32 * w;
+  float* Z = XP + (G_MAXL + 2) * 32 + 128;
+  const int xin_off = kq < 2 ? 16 * kq : 16 * (kq - 2);
+  const int Q = a.Q, per = (Q + 63) >> 6, c0 = lane * per;
+  long long* tr = (a.trace && b == 0 && threadIdx.x == 0) ? a.trace : nullptr;
+  int code = a.code_in[b];   // step 0 of the run: the previous run's last draw (-1 at t = 0)
+  for (int s = 0; s <= n; ++s) {
+    const long long t = t0 + s;
+    if (s > 0) {
+      // draw step t-1: code q's partial logits of heads 0..15 here, 16..31 by the loader waves;
+      // logit = (Σ first half + Σ second half) + b2
+      const int q = min((int)threadIdx.x, Q - 1);
+      float v[P_NH / 2], lsum = 0.f;
+      sweep<P_NH / 2>(a.lg, (unsigned)(b * Q + q), (unsigned)(a.B * Q), P_NH / 2, (unsigned)t, v, a.status);
+#pragma unroll
+      for (int i = 0; i < P_NH / 2; ++i) lsum += v[i];
+      DL[q] = lsum;
+      if (tr && s == n) tr[5] = wall_clock64();
+      lds_barrier();   // D
+      float lv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int cc = min(c0 + j, Q - 1);
+        lv[j] = DL[cc] + DL[256 + cc];
+        if (a.draw.bias) lv[j] += a.draw.bias[cc];
+      }
+      code = draw_core<4>(lv, a.draw, b, t - 1, w == 0);
+      if (s == n) {
+        if (tr) tr[6] = wall_clock64();
+        break;
+      }
+    }
+    if (tr && s == n - 1) tr[0] = wall_clock64();
+    float x = 0.f;   // x[rc] of the current layer input: PRE row of the draw (+ PRE_BIAS); zero at t = 0
+    if (rc < Cr) {
+      if (code >= 0) x = a.pre[(long)code * Cr + rc];
+      if (a.pre_bias && a.pre_b) x += a.pre_b[rc];
+    }
+    if (lane < 32) XW[rc] = x;
+    long roff = 0;
+    int bl = 0;
+    lds_barrier();   // -1
+    for (int l = 0; l < L; ++l) {
+      const long G = (long)s * L + l;
+      const float* S = RING + (G % G_NS) * G_SLOT;
+      const float* xin = (kq < 2 ? XP + l * 32 : XW) + xin_off;
+      floatx4 wv[4], xv[4];
+#pragma unroll
+      for (int mm = 0; mm < 4; ++mm) {
+        wv[mm] = *(const floatx4*)(S + (w * 4 + mm) * 256 + lane * 4);
+        xv[mm] = *(const floatx4*)(xin + 4 * mm);
+      }
+      const float bco = S[GI_WR + o] + S[GI_WR + 128 + o];
+      __builtin_amdgcn_sched_barrier(0);
+      const int d = 1 << bl;
+      if (rh == 0 && (rc >> 3) == w && rc < Cr) a.rings[roff + ((long)b * d + (t & (d - 1))) * Cr + rc] = x;
+      roff += (long)d * a.B * Cr;
+      bl = (bl + 1 == a.nbl) ? 0 : bl + 1;
+      float acc0 = dot4(wv[0], xv[0], 0.f), acc1 = dot4(wv[1], xv[1], 0.f);
+      acc0 = dot4(wv[2], xv[2], acc0);
+      acc1 = dot4(wv[3], xv[3], acc1);
+      float v = acc0 + acc1;
+      v += dpp<DPP_XOR1>(v);
+      v += dpp<DPP_XOR2>(v);
+      v += bco;
+      const float vp = dpp<DPP_HALF_MIRROR>(v);
+      const float z = tanhf_(sg ? vp : v) * sigmoidf_(sg ? v : vp);
+      float* Zl = Z + (l & 1) * 32;
+      if (lead) {
+        Zl[ch] = z;
+        if (ch < Cd) put_granule(a.zg + ((long)b * L + l) * 32 + ch, (unsigned)(t + 1), z);
+      }
+      // the last layer's ring stores must land before the loaders DMA the next step's taps
+      if (l == L - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
+      floatx4 zv[4], rw[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        zv[q] = *(const floatx4*)(Zl + 16 * rh + 4 * q);
+        rw[q] = *(const floatx4*)(S + GI_W + ((rh * 4 + q) * 32 + rc) * 4);
+      }
+      const float bro = S[GI_WR + 64 + rc];
+      float r0 = dot4(rw[0], zv[0], 0.f), r1 = dot4(rw[1], zv[1], 0.f);
+      r0 = dot4(rw[2], zv[2], r0);
+      r1 = dot4(rw[3], zv[3], r1);
+      const float r = r0 + r1;
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(r), __float_as_uint(r), false, false);
+      x += (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) + bro;
+      if (lane < 32) XW[rc] = x;
+      wave_sync();
+      if (tr && s == n - 1) tr[8 + l] = wall_clock64();
+    }
+    if (tr && s == n - 1) tr[1] = wall_clock64();
+  }
+  if (b == 0 && threadIdx.x == 0) *a.step = t0 + n;   // every block read it at its start (see header)
+}
+
+LBWN_DEV void persist_head(const PersistK& a, int m, float* sm) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int B = a.B, L = a.L, Cd = a.Cd, Cs = a.Cs, Cp = a.Cp, Q = a.Q, n = a.n_steps;
+  const long long t0 = *a.step;
+  float* ZS = sm;                  // [P_LA layers][16 b][32 k] z of a round
+  float* RS = ZS + P_LA * 512;     // [16 b][512 k] relu(skip + Σb), zero-padded
+  float* HP = RS + P_MAXB * 512;   // [32 kg][16 b][16 c] per-thread partials (skip, then post1)
+  float* HS = HP + 32 * 256;       // [16 b][16 c] h
+  float* P1T = HS + 256;           // [16 c][516] POST1[:, 16m + c] (rows padded: conflict-free b128 reads)
+  float* P2S = P1T + 16 * 516;     // [16 r][Q] POST2[16m + r, :]
+  for (int e = tid; e < P_MAXB * 512; e += 512) RS[e] = 0.f;
+  for (int e = tid; e < 16 * 512; e += 512) {   // the head's weight slices stay in LDS for the run
+    const int cc = e >> 9, k = e & 511;
+    P1T[cc * 516 + k] = (k < Cs && m * 16 + cc < Cp) ? a.post1[(long)k * Cp + m * 16 + cc] : 0.f;
+  }
+  for (int e = tid; e < 16 * Q; e += 512) {
+    const int r = e / Q, q = e - r * Q;
+    P2S[e] = (m * 16 + r < Cp) ? a.post2[(long)(m * 16 + r) * Q + q] : 0.f;
+  }
+  // lane roles: c = column within this block's 16, kg = tid >> 4 = 4·wave + (lane >> 4)
+  const int c = tid & 15, kg = tid >> 4, kql = lane >> 4;
+  const int scol = m * 16 + c, hcol = m * 16 + c;
+  // A: wave wv takes layer l0 + wv of each round, lane quarter kql the channels 8kql..8kql+7
+  const float* wsrc = a.skipw + (long)(8 * kql) * Cs + min(scol, Cs - 1);
+  // C: post1 rows 16kg .. 16kg+15 of column hcol (P1T); post2 rows 16m .. 16m+15 of column tid (P2S)
+  const float b1 = (hcol < Cp && a.post1_b) ? a.post1_b[hcol] : 0.f;
+  // z granules polled by this thread: (stream zb0, channel zk) of every layer of a round
+  const int zb0 = tid >> 5, zk = tid & 31;
+  const bool zn0 = zb0 < B && zk < Cd;
+  long long* tr = (a.trace && m == P_NH - 1 && tid == 0) ? a.trace : nullptr;
+  for (int s = 0; s < n; ++s) {
+    const unsigned tag = (unsigned)(t0 + s + 1);
+    // A. skip columns, P_LA layers per round: the round's z granules and this lane's 8 weights
+    //    arrive in one round trip; per-thread partials pa[b] (layer wv of each round, channels
+    //    8kql..) are reduced once after the last round
+    float pa[P_MAXB];
+#pragma unroll
+    for (int bb = 0; bb < P_MAXB; ++bb) pa[bb] = 0.f;
+    for (int l0 = 0; l0 < L; l0 += P_LA) {
+      const int nl = min(P_LA, L - l0), li = l0 + wv;
+      float wv8[8], zv[P_LA];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        wv8[j] = wsrc[((long)min(li, L - 1) * Cd + min(j, Cd - 1 - 8 * kql)) * Cs];
+      sweep<P_LA>(a.zg, (unsigned)(((zn0 ? zb0 : 0) * L + l0) * 32 + (zn0 ? zk : 0)), 32u, nl, tag, zv, a.status);
+      if (tr && s == n - 1) tr[8 + L + 40 + l0 / P_LA] = wall_clock64();
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (li >= L || 8 * kql + j >= Cd || scol >= Cs) wv8[j] = 0.f;
+      __syncthreads();   // the previous round's readers are done
+#pragma unroll
+      for (int i = 0; i < P_LA; ++i) ZS[i * 512 + tid] = (zn0 && i < nl) ? zv[i] : 0.f;
+      __syncthreads();
+      if (tr && s == n - 1) tr[8 + L + 80 + l0 / P_LA] = wall_clock64();
+      const float* zr = ZS + wv * 512 + 8 * kql;
+#pragma unroll
+      for (int bb = 0; bb < P_MAXB; ++bb) {
+        if ((bb & 3) == 0) __builtin_amdgcn_sched_barrier(0);   // 4 streams' reads in flight at a time
+        if (bb < B) {
+          const floatx4 z0 = *(const floatx4*)(zr + bb * 32), z1 = *(const floatx4*)(zr + bb * 32 + 4);
+          float x = pa[bb];
+          x = fmaf(z0[0], wv8[0], x);
+          x = fmaf(z0[1], wv8[1], x);
+          x = fmaf(z0[2], wv8[2], x);
+          x = fmaf(z0[3], wv8[3], x);
+          x = fmaf(z1[0], wv8[4], x);
+          x = fmaf(z1[1], wv8[5], x);
+          x = fmaf(z1[2], wv8[6], x);
+          x = fmaf(z1[3], wv8[7], x);
+          pa[bb] = x;
+        }
+      }
+      if (tr && s == n - 1) tr[8 + L + l0 / P_LA] = wall_clock64();
+    }
+    // reduce the 32 per-thread partials of each (stream, column) through LDS (no shuffles:
+    // their dependent LDS round trips cost ~2 us per phase)
+#pragma unroll
+    for (int bb = 0; bb < P_MAXB; ++bb)
+      if (bb < B) HP[(kg * 16 + bb) * 16 + c] = pa[bb];
+    __syncthreads();
+    {
+      const int sb = tid >> 4;   // (column c, stream sb)
+      if (sb < B && scol < Cs) {
+        float v[32], x = 0.f;
+#pragma unroll
+        for (int g = 0; g < 32; ++g) v[g] = HP[(g * 16 + sb) * 16 + c];
+#pragma unroll
+        for (int g = 0; g < 32; ++g) x += v[g];
+        put_granule(a.sg + (long)sb * Cs + scol, tag, x);   // B. publish this block's skip columns
+      }
+    }
+    if (tr && s == n - 1) tr[2] = wall_clock64();
+    // B. gather the whole skip vector: thread k = tid polls column k of every stream
+    if (tid < Cs) {
+      float v[P_MAXB];
+      sweep<P_MAXB>(a.sg, (unsigned)tid, (unsigned)Cs, B, tag, v, a.status);
+      const float bs = a.bsum ? a.bsum[tid] : 0.f;
+#pragma unroll
+      for (int bb = 0; bb < P_MAXB; ++bb)
+        if (bb < B) RS[bb * 512 + tid] = fmaxf(v[bb] + bs, 0.f);
+    }
+    __syncthreads();
+    if (tr && s == n - 1) tr[3] = wall_clock64();
+    // C. post1 partial over rows 16kg..16kg+15 of column hcol, 4 streams at a time (independent
+    //    chains), the 32 row groups summed through LDS
+    {
+      floatx4 w4[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w4[q] = *(const floatx4*)(P1T + c * 516 + 16 * kg + 4 * q);
+      for (int g0 = 0; g0 < B; g0 += 4) {
+        floatx4 x[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x[j][q] = *(const floatx4*)(RS + min(g0 + j, P_MAXB - 1) * 512 + 16 * kg + 4 * q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float pp = 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            pp = fmaf(x[j][q][0], w4[q][0], pp);
+            pp = fmaf(x[j][q][1], w4[q][1], pp);
+            pp = fmaf(x[j][q][2], w4[q][2], pp);
+            pp = fmaf(x[j][q][3], w4[q][3], pp);
+          }
+          if (g0 + j < B) HP[(kg * 16 + g0 + j) * 16 + c] = pp;
+        }
+      }
+    }
+    if (tr && s == n - 1) tr[8 + L + 120] = wall_clock64();
+    __syncthreads();
+    if (tr && s == n - 1) tr[8 + L + 121] = wall_clock64();
+    {
+      const int sb = tid >> 4;
+      if (sb < B) {
+        float v[32], h = 0.f;
+#pragma unroll
+        for (int g = 0; g < 32; ++g) v[g] = HP[(g * 16 + sb) * 16 + c];
+#pragma unroll
+        for (int g = 0; g < 32; ++g) h += v[g];
+        HS[sb * 16 + c] = hcol < Cp ? fmaxf(h + b1, 0.f) : 0.f;
+      }
+    }
+    __syncthreads();
+    if (tr && s == n - 1) tr[8 + L + 122] = wall_clock64();
+    // partial logits over this block's 16 h rows: column q = tid, 4 streams at a time
+    if (tid < Q) {
+      float p2[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) p2[r] = P2S[r * Q + tid];
+      for (int g0 = 0; g0 < B; g0 += 4) {
+        floatx4 hv[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) hv[j][q] = *(const floatx4*)(HS + min(g0 + j, P_MAXB - 1) * 16 + 4 * q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float lp = 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            lp = fmaf(hv[j][q][0], p2[4 * q], lp);
+            lp = fmaf(hv[j][q][1], p2[4 * q + 1], lp);
+            lp = fmaf(hv[j][q][2], p2[4 * q + 2], lp);
+            lp = fmaf(hv[j][q][3], p2[4 * q + 3], lp);
+          }
+          if (g0 + j < B) put_granule(a.lg + ((long)m * B + g0 + j) * Q + tid, tag, lp);
+        }
+      }
+    }
+    if (tr && s == n - 1) tr[4] = wall_clock64();
+  }
+}
+
+__global__ __launch_bounds__(512) void gen_persist_kernel(PersistK a) {
+  __shared__ __attribute__((aligned(16))) float sm[G_LDS];
+  if ((int)blockIdx.x < a.B) persist_chain(a, sm);
+  else persist_head(a, blockIdx.x - a.B, sm);
 }
 
 // gc_proj[l][b][o] = GC_EMBED[gc_id[b]] · [GC_SIGNAL_l | GC_GATE_l]  (imodel.py:53-56, :113-118)
@@ -629,9 +988,12 @@ __global__ void gen_gc_proj_kernel(const float* emb, const float* gsig, const fl
   }
 }
 
-__global__ void gen_reset_kernel(float* rings, long n_ring, int* code, int B, long long* step, int* status) {
+__global__ void gen_reset_kernel(float* rings, long n_ring, unsigned long long* gran, long n_gran, int* code, int B,
+                                 long long* step, int* status) {
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n_ring; e += (long)gridDim.x * blockDim.x)
     rings[e] = 0.f;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n_gran; e += (long)gridDim.x * blockDim.x)
+    gran[e] = 0ull;   // tags restart at 1 with the step counter
   if (blockIdx.x == 0) {
     for (int b = threadIdx.x; b < B; b += blockDim.x) code[b] = -1;
     if (threadIdx.x == 0) {
@@ -651,9 +1013,11 @@ struct lbwn_gen_plan {
   lbwn_arch a;
   int B, L, nbl, Cr, Cd, Cs, Cp, Q;
   long long max_steps;
-  size_t oRING, oZG, oSKP, oHP, oLGP, oLOG, oSTEP, oCODE, oTEACH, oSAMP, oWAV, oGCP, oBSUM, oGIMG, oTRACE, total;
-  bool trace;
-  int lg_skip, ks_skip, ks_h, ks_lg;
+  size_t oRING, oZCAT, oSKP, oHP, oLGP, oLOG, oSTEP, oCODE, oTEACH, oSAMP, oWAV, oGCP, oBSUM, oGIMG, oTRACE, total;
+  size_t oGRAN;   // persistent form: granules [zg B·L·32 | sg B·Cs | lg P_NH·B·Q]
+  long n_gran;
+  bool trace, persist;
+  int ksl_skip, ks_skip, ks_h, ks_lg;
   long n_ring;
   long long n_teacher, max_teacher;
   unsigned long long seed;
@@ -670,11 +1034,10 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
                                     lbwn_gen_plan** out) {
   LBWN_REQUIRE(a && out && B >= 1 && max_steps >= 1 && max_teacher >= 0, "gen_plan_create: bad arguments");
   LBWN_REQUIRE(a->n_res <= 32 && a->n_dil <= 32, "gen: n_res/n_dil must be <= 32");
-  LBWN_REQUIRE(a->n_skip <= 512, "gen: n_skip must be <= 512 (one skip column per helper thread)");
-  LBWN_REQUIRE(a->n_quant <= 512, "gen: n_quant must be <= 512");
   LBWN_REQUIRE(a->n_blocks * a->n_block_layers <= G_MAXL, "gen: more than %d layers (tap cache)", G_MAXL);
   LBWN_REQUIRE(a->n_lc_out == 0, "gen: local conditioning is not supported by the cached generator "
                                  "(imodel.py has no LC path)");
+  LBWN_REQUIRE(a->n_quant <= 512, "gen: n_quant must be <= 512");
   lbwn_gen_plan* p = new lbwn_gen_plan();
   p->a = *a;
   p->B = B;
@@ -687,10 +1050,10 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
   p->n_ring = dsum * B * p->Cr;
   size_t cur = 0;
   p->oRING = gcarve(cur, 4 * (size_t)p->n_ring);
-  p->oZG = gcarve(cur, 8 * (size_t)B * p->L * 32);   // z granules {z, step+1}
+  p->oZCAT = gcarve(cur, 4 * (size_t)B * p->L * p->Cd);
   // K-split GEMV partials: skip (K = L·Cd, 64-row slices), post1 and post2 (32-row slices)
-  p->lg_skip = 2;                                    // layers per skip helper block
-  p->ks_skip = (p->L + p->lg_skip - 1) / p->lg_skip;
+  p->ksl_skip = 64;
+  p->ks_skip = (p->L * p->Cd + p->ksl_skip - 1) / p->ksl_skip;
   p->ks_h = (p->Cs + 31) / 32;
   p->ks_lg = (p->Cp + 31) / 32;
   p->oSKP = gcarve(cur, 4 * (size_t)p->ks_skip * B * p->Cs);
@@ -705,8 +1068,18 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
   p->oGCP = gcarve(cur, 4 * (size_t)p->L * B * 64);
   p->oBSUM = gcarve(cur, 4 * (size_t)p->Cs);
   p->oGIMG = gcarve(cur, 4 * (size_t)p->L * GIMG);
-  p->oTRACE = gcarve(cur, 8 * (size_t)(2 * p->L + 40 + 3 * p->B));
+  p->oTRACE = gcarve(cur, 8 * (size_t)(2 * p->L + 8 + 128));
   p->trace = getenv("LBWN_GEN_TRACE") != nullptr;
+  // persistent form: every block resident (one 512-thread block per CU), phase A maps
+  // (16 skip columns × B streams) onto the threads, the draw's logits fit the tap table's tail
+  int dev = 0, ncu = 0;
+  const bool have_dev = hipGetDevice(&dev) == hipSuccess &&
+                        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess;
+  const char* pe = getenv("LBWN_GEN_PERSIST");
+  p->persist = (!pe || strcmp(pe, "0") != 0) && B <= P_MAXB && p->L <= P_MAXL && p->Q <= 256 && p->Cs <= 16 * P_NH &&
+               p->Cp <= 16 * P_NH && have_dev && B + P_NH <= ncu;
+  p->n_gran = (long)B * p->L * 32 + (long)B * p->Cs + (long)P_NH * B * p->Q;
+  p->oGRAN = gcarve(cur, 8 * (size_t)p->n_gran);
   p->total = cur;
   *out = p;
   return 0;
@@ -722,8 +1095,8 @@ extern "C" int lbwn_gen_tensor(const lbwn_gen_plan* p, const char* name, size_t*
   else if (!strcmp(name, "wav")) { *off = p->oWAV; *bytes = 4 * B * p->max_steps; }
   else if (!strcmp(name, "logits")) { *off = p->oLOG; *bytes = 4 * B * p->Q; }
   else if (!strcmp(name, "step")) { *off = p->oSTEP; *bytes = 8; }
-  else if (!strcmp(name, "status")) { *off = p->oSTEP + 8; *bytes = 4; }   // 0, or 5: a skip helper's granule poll timed out
-  else if (!strcmp(name, "trace")) { *off = p->oTRACE; *bytes = 8 * (size_t)(2 * p->L + 40 + 3 * p->B); }
+  else if (!strcmp(name, "status")) { *off = p->oSTEP + 8; *bytes = 4; }   // 0, or 5: a persistent hand-off timed out
+  else if (!strcmp(name, "trace")) { *off = p->oTRACE; *bytes = 8 * (size_t)(2 * p->L + 8 + 128); }
   else if (!strcmp(name, "rings")) { *off = p->oRING; *bytes = 4 * (size_t)p->n_ring; }
   else if (!strcmp(name, "teacher")) { *off = p->oTEACH; *bytes = 4 * (size_t)std::max<long long>(1, p->n_teacher); }
   else LBWN_REQUIRE(false, "gen_tensor: unknown tensor '%s'", name);
@@ -745,8 +1118,9 @@ extern "C" int lbwn_gen_start(lbwn_gen_plan* p, const lbwn_params* P, void* ws, 
   p->n_teacher = teacher ? n_teacher : 0;
   p->seed = seed;
   p->pre_bias = pre_bias;
-  gen_reset_kernel<<<256, 256, 0, st>>>(gat<float>(ws, p->oRING), p->n_ring, gat<int>(ws, p->oCODE), p->B,
-                                        gat<long long>(ws, p->oSTEP), gat<int>(ws, p->oSTEP + 8));
+  gen_reset_kernel<<<256, 256, 0, st>>>(gat<float>(ws, p->oRING), p->n_ring, gat<unsigned long long>(ws, p->oGRAN),
+                                        p->n_gran, gat<int>(ws, p->oCODE), p->B, gat<long long>(ws, p->oSTEP),
+                                        gat<int>(ws, p->oSTEP + 8));
   LBWN_CHECK_LAUNCH();
   if (p->n_teacher > 0) {
     hipError_t e = hipMemcpyAsync(gat<int>(ws, p->oTEACH), teacher, 4 * (size_t)p->n_teacher, hipMemcpyDeviceToDevice,
@@ -767,53 +1141,72 @@ extern "C" int lbwn_gen_start(lbwn_gen_plan* p, const lbwn_params* P, void* ws, 
   return 0;
 }
 
+extern "C" int lbwn_gen_is_persistent(const lbwn_gen_plan* p) { return p && p->persist ? 1 : 0; }
+
 extern "C" int lbwn_gen_run(lbwn_gen_plan* p, const lbwn_params* P, void* ws, int n_steps, void* stream) {
   LBWN_REQUIRE(p && P && ws && n_steps >= 0, "gen_run: bad arguments");
   hipStream_t st = (hipStream_t)stream;
-  WaveK c;
-  memset(&c, 0, sizeof(c));
-  c.pre = P->pre; c.pre_b = P->pre_b; c.img = gat<float>(ws, p->oGIMG);
-  c.gc_proj = p->a.n_gc_embed > 0 ? gat<float>(ws, p->oGCP) : nullptr;
-  c.rings = gat<float>(ws, p->oRING);
-  c.step = gat<long long>(ws, p->oSTEP); c.code = gat<int>(ws, p->oCODE);
-  c.trace = p->trace ? gat<long long>(ws, p->oTRACE) : nullptr;
-  c.B = p->B; c.L = p->L; c.nbl = p->nbl; c.Cr = p->Cr; c.Cd = p->Cd; c.pre_bias = p->pre_bias;
-  c.zg = gat<unsigned long long>(ws, p->oZG); c.skipw = P->skip; c.skip_part = gat<float>(ws, p->oSKP);
-  c.Cs = p->Cs; c.LG = p->lg_skip; c.status = gat<int>(ws, p->oSTEP + 8);
-  // skip = Σ helper partials (+Σb, relu: post1's input), h = relu(relu(skip)·POST1 + b1),
-  // logits = h·POST2 + b2 (summed by the draw); post1 advances the step counter
-  GemvK p1, p2;
-  memset(&p1, 0, sizeof(p1));
-  p1.in_part = c.skip_part; p1.in_parts = p->ks_skip; p1.in_bias = P->skip_b ? gat<float>(ws, p->oBSUM) : nullptr;
-  p1.relu_in = 1; p1.W = P->post1; p1.ldw = p->Cp; p1.out_part = gat<float>(ws, p->oHP);
-  p1.B = p->B; p1.K = p->Cs; p1.N = p->Cp; p1.KSL = 32;
-  p1.step_advance = gat<long long>(ws, p->oSTEP);
-  p2 = p1;
-  p2.step_advance = nullptr;
-  p2.in_part = p1.out_part; p2.in_parts = p->ks_h; p2.in_bias = P->post1_b; p2.relu_in = 1;
-  p2.W = P->post2; p2.ldw = p->Q; p2.out_part = gat<float>(ws, p->oLGP); p2.K = p->Cp; p2.N = p->Q; p2.KSL = 32;
-  DrawK& d = c.draw;
-  d.part = p2.out_part; d.parts = p->ks_lg; d.bias = P->post2_b; d.Q = p->Q; d.B = p->B;
+  DrawK d;
+  memset(&d, 0, sizeof(d));
+  d.Q = p->Q; d.B = p->B; d.bias = P->post2_b;
   d.logits = gat<float>(ws, p->oLOG); d.samples = gat<int>(ws, p->oSAMP); d.wav = gat<float>(ws, p->oWAV);
   d.max_steps = p->max_steps; d.teacher = gat<int>(ws, p->oTEACH); d.n_teacher = p->n_teacher; d.seed = p->seed;
   d.code = gat<int>(ws, p->oCODE);
-  const dim3 gp1((p1.N + 63) / 64, (p1.K + 31) / 32), gp2((p2.N + 63) / 64, (p2.K + 31) / 32);
-  if (p->trace) {   // GEMV stamps after the wave kernel's: [unused | post1 | post2] × 8
-    long long* tb = gat<long long>(ws, p->oTRACE) + 2 * p->L + 8;
-    p1.trace = tb + 8; p2.trace = tb + 16;
+  if (p->persist) {
+    if (n_steps == 0) return 0;
+    PersistK k;
+    memset(&k, 0, sizeof(k));
+    k.pre = P->pre; k.pre_b = P->pre_b; k.img = gat<float>(ws, p->oGIMG);
+    k.gc_proj = p->a.n_gc_embed > 0 ? gat<float>(ws, p->oGCP) : nullptr;
+    k.rings = gat<float>(ws, p->oRING); k.step = gat<long long>(ws, p->oSTEP); k.code_in = gat<int>(ws, p->oCODE);
+    k.B = p->B; k.L = p->L; k.nbl = p->nbl; k.Cr = p->Cr; k.Cd = p->Cd; k.pre_bias = p->pre_bias; k.n_steps = n_steps;
+    unsigned long long* g = gat<unsigned long long>(ws, p->oGRAN);
+    k.zg = g; k.sg = g + (long)p->B * p->L * 32; k.lg = k.sg + (long)p->B * p->Cs;
+    k.Cs = p->Cs; k.Cp = p->Cp; k.Q = p->Q;
+    k.skipw = P->skip; k.bsum = P->skip_b ? gat<float>(ws, p->oBSUM) : nullptr;
+    k.post1 = P->post1; k.post1_b = P->post1_b; k.post2 = P->post2;
+    k.draw = d;
+    k.status = gat<int>(ws, p->oSTEP + 8);
+    k.trace = p->trace ? gat<long long>(ws, p->oTRACE) : nullptr;
+    gen_persist_kernel<<<p->B + P_NH, 512, 0, st>>>(k);
+    LBWN_CHECK_LAUNCH();
+    return 0;
   }
-  // per step: gen_wave (chains + skip helpers; from the second step of the run on, it first
-  // draws the previous step), post1, post2; the run's last step is drawn by gen_sample
+  WaveK c;
+  c.pre = P->pre; c.pre_b = P->pre_b; c.img = gat<float>(ws, p->oGIMG);
+  c.gc_proj = p->a.n_gc_embed > 0 ? gat<float>(ws, p->oGCP) : nullptr;
+  c.rings = gat<float>(ws, p->oRING); c.zcat = gat<float>(ws, p->oZCAT);
+  c.step = gat<long long>(ws, p->oSTEP); c.code = gat<int>(ws, p->oCODE);
+  c.trace = p->trace ? gat<long long>(ws, p->oTRACE) : nullptr;
+  c.B = p->B; c.L = p->L; c.nbl = p->nbl; c.Cr = p->Cr; c.Cd = p->Cd; c.pre_bias = p->pre_bias;
+  // skip = z_cat·SKIPcat (+Σb and relu applied by the consumer), h = relu(relu(skip)·POST1 + b1),
+  // logits = h·POST2 + b2 (summed in the sampler)
+  GemvK sk = {}, p1 = {}, p2 = {};
+  memset(&sk, 0, sizeof(sk));
+  sk.in = c.zcat; sk.ldin = (long)p->L * p->Cd; sk.W = P->skip; sk.ldw = p->Cs; sk.out_part = gat<float>(ws, p->oSKP);
+  sk.B = p->B; sk.K = p->L * p->Cd; sk.N = p->Cs; sk.KSL = p->ksl_skip;
+  sk.step_advance = gat<long long>(ws, p->oSTEP);   // the sampler reads step - 1
+  p1 = sk;
+  p1.step_advance = nullptr;
+  p1.in = nullptr; p1.in_part = sk.out_part; p1.in_parts = p->ks_skip; p1.in_bias = P->skip_b ? gat<float>(ws, p->oBSUM) : nullptr;
+  p1.relu_in = 1; p1.W = P->post1; p1.ldw = p->Cp; p1.out_part = gat<float>(ws, p->oHP); p1.K = p->Cs; p1.N = p->Cp; p1.KSL = 32;
+  p2 = p1;
+  p2.in_part = p1.out_part; p2.in_parts = p->ks_h; p2.in_bias = P->post1_b; p2.relu_in = 1;
+  p2.W = P->post2; p2.ldw = p->Q; p2.out_part = gat<float>(ws, p->oLGP); p2.K = p->Cp; p2.N = p->Q; p2.KSL = 32;
+  d.part = p2.out_part; d.parts = p->ks_lg;
+  const dim3 gsk((sk.N + 63) / 64, p->ks_skip), gp1((p1.N + 63) / 64, (p1.K + 31) / 32), gp2((p2.N + 63) / 64, (p2.K + 31) / 32);
+  if (p->trace) {   // GEMV stamps after the wave kernel's: [skip | post1 | post2] × 8
+    long long* tb = gat<long long>(ws, p->oTRACE) + 2 * p->L + 8;
+    sk.trace = tb; p1.trace = tb + 8; p2.trace = tb + 16;
+  }
   for (int i = 0; i < n_steps; ++i) {
-    c.fuse_draw = i > 0;
-    gen_wave_kernel<<<p->B + p->ks_skip, 512, 0, st>>>(c);
+    gen_wave_kernel<<<p->B, 512, 0, st>>>(c);
+    gen_gemv_kernel<<<gsk, 256, 0, st>>>(sk);
     gen_gemv_kernel<<<gp1, 256, 0, st>>>(p1);
     gen_gemv_kernel<<<gp2, 256, 0, st>>>(p2);
-    LBWN_CHECK_LAUNCH();
-  }
-  if (n_steps > 0) {
-    gen_sample_kernel<<<p->B, 64, 0, st>>>(c.draw, c.step);
+    gen_sample_kernel<<<p->B, 64, 0, st>>>(d, c.step);
     LBWN_CHECK_LAUNCH();
   }
   return 0;
 }
+

@@ -57,6 +57,7 @@ _SIGS = {
     'lbwn_gen_start': (c_int, [c_void_p, ctypes.POINTER(Params), c_fp, c_fp, c_fp, c_int64, ctypes.c_uint64, c_int,
                                c_void_p]),
     'lbwn_gen_run': (c_int, [c_void_p, ctypes.POINTER(Params), c_fp, c_int, c_void_p]),
+    'lbwn_gen_is_persistent': (c_int, [c_void_p]),
     'lbwn_mulaw_encode': (c_int, [c_fp, c_fp, c_int64, c_int, c_int, c_void_p]),
     'lbwn_mulaw_decode': (c_int, [c_fp, c_fp, c_int64, c_int, c_void_p]),
     'lbwn_gemm_f32': (c_int, [c_fp, c_int64, c_int, c_fp, c_int64, c_int, c_fp, c_int64, c_int, c_int, c_int,

@@ -91,6 +91,11 @@ class WaveNetGen:
         self._graph = None
         return self
 
+    @property
+    def persistent(self):
+        """True when the plan runs each gen_run as one persistent launch (B <= 32)."""
+        return bool(self._plan is not None and self.lib.lbwn_gen_is_persistent(self._plan))
+
     def tensor(self, name, dtype=torch.float32):
         off, nb = _lib.c_size_t(), _lib.c_size_t()
         _lib.check(self.lib.lbwn_gen_tensor(self._plan, name.encode(), ctypes.byref(off), ctypes.byref(nb)))

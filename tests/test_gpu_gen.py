@@ -16,6 +16,17 @@ from tests.conftest import ROOT
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=['persistent', 'per_step'])
+def form(request, monkeypatch):
+    """Both execution forms: the persistent one-launch kernel (default for B <= 32) and the
+    per-step launches (LBWN_GEN_PERSIST=0, the form every B > 32 runs)."""
+    if request.param == 'per_step':
+        monkeypatch.setenv('LBWN_GEN_PERSIST', '0')
+    else:
+        monkeypatch.delenv('LBWN_GEN_PERSIST', raising=False)
+    return request.param
+
+
 def small(gc=0):
     return normalize_arch(dict(n_blocks=2, n_block_layers=4, n_quant=256, n_res=32, n_dil=32, n_skip=64,
                                n_post=32, n_gc_embed=8 if gc else 0, n_gc_category=gc, use_bias=True))
@@ -36,19 +47,20 @@ def make_gen(arch, B, chunk, seed=7, teacher=None, pre_bias=True, graph=True):
 
 
 @pytest.mark.parametrize('pre_bias', [True, False])
-def test_gen_free_running_matches_oracle(pre_bias):
+def test_gen_free_running_matches_oracle(pre_bias, form):
     arch = small()
     B, n = 3, 48
     g, P = make_gen(arch, B, chunk=16, pre_bias=pre_bias)
     _, wav, _ = g.run(n)
     torch.cuda.synchronize()
+    assert g.persistent == (form == 'persistent')
     s_ref, w_ref = R.generate(arch, P, B, n, seed=7, pre_bias=pre_bias)
     assert int(g.tensor('status', torch.int32).item()) == 0     # no hand-off spin timed out
     np.testing.assert_array_equal(g.samples().cpu().numpy()[:, :n], s_ref)
     np.testing.assert_allclose(wav.cpu().numpy(), w_ref[:, :wav.shape[1]], rtol=1e-6, atol=1e-6)
 
 
-def test_gen_teacher_forced_and_gc():
+def test_gen_teacher_forced_and_gc(form):
     arch = small(gc=5)
     B, n = 2, 40
     teacher_q = np.random.default_rng(1).integers(0, 256, 25).astype(np.int32)
@@ -58,17 +70,20 @@ def test_gen_teacher_forced_and_gc():
     gc = [2, 5]
     g.run(n, gc_ids=gc)
     torch.cuda.synchronize()
+    assert g.persistent == (form == 'persistent')
+    assert int(g.tensor('status', torch.int32).item()) == 0
     s_ref, _, lg_ref = R.generate(arch, P, B, n, seed=7, teacher_q=teacher_q, gc_ids=gc, return_logits=True)
     np.testing.assert_array_equal(g.samples().cpu().numpy()[:, :n], s_ref)
     np.testing.assert_allclose(g.logits().cpu().numpy(), lg_ref[:, -1], rtol=0, atol=2e-4 * np.abs(lg_ref).max())
 
 
-def test_gen_arch3_b10_graph_replay():
+def test_gen_arch3_b10_graph_replay(form):
     arch = load_arch(os.path.join(ROOT, 'par', 'arch3.json'))
     B, n = 10, 300
     g, P = make_gen(arch, B, chunk=100)
     n_out, wav, _ = g.run(n)
     torch.cuda.synchronize()
+    assert g.persistent == (form == 'persistent')
     assert wav.shape == (B, 300)
     s_ref, w_ref = R.generate(arch, P, B, n, seed=7)
     got = g.samples().cpu().numpy()[:, :n]
@@ -76,3 +91,26 @@ def test_gen_arch3_b10_graph_replay():
     assert mism == 0, '%d / %d draws differ' % (mism, got.size)
     assert int(g.tensor('step', torch.int64).item()) == n
     assert int(g.tensor('status', torch.int32).item()) == 0
+
+
+def test_gen_rerun_and_large_batch():
+    """A second run on the same plan restarts the tags with the step counter (stale granules
+    from the first run must not be taken), and B = 40 > 32 runs the per-step form."""
+    arch = small(gc=5)
+    B, n = 40, 24
+    g, P = make_gen(arch, B, chunk=8)
+    gc = [1 + b % 5 for b in range(B)]
+    g.run(n, gc_ids=gc)
+    g.run(n, gc_ids=gc)
+    torch.cuda.synchronize()
+    assert not g.persistent
+    s_ref, _ = R.generate(arch, P, B, n, seed=7, gc_ids=gc)
+    np.testing.assert_array_equal(g.samples().cpu().numpy()[:, :n], s_ref)
+    g2, P2 = make_gen(arch, 12, chunk=8)
+    g2.run(n, gc_ids=gc[:12])
+    g2.run(n, gc_ids=gc[:12])
+    torch.cuda.synchronize()
+    assert g2.persistent
+    s2, _ = R.generate(arch, P2, 12, n, seed=7, gc_ids=gc[:12])
+    np.testing.assert_array_equal(g2.samples().cpu().numpy()[:, :n], s2)
+    assert int(g2.tensor('status', torch.int32).item()) == 0

@@ -1,5 +1,7 @@
-"""Cycle-stamp trace of one cached-generation step (stream 0): prologue (weights + taps),
-step input, then per layer conv+gate and residual.  Needs LBWN_GEN_TRACE=1 (set here)."""
+"""Wall-clock trace of one cached-generation step (LBWN_GEN_TRACE=1, set here), arch3, B
+streams.  Persistent form (default for B <= 32): the run's last step as seen by chain block 0
+and the last head block; per-step form (LBWN_GEN_PERSIST=0): per-layer cycles of stream 0's
+gen_wave and the GEMV stamps.  Usage: python tools/gen_trace.py [B]"""
 import os
 import sys
 
@@ -19,38 +21,39 @@ g = WaveNetGen(arch['n_blocks'], arch['n_block_layers'], arch['n_quant'], arch['
                arch['n_skip'], arch['n_post'], arch['n_gc_embed'], arch['n_gc_category'], arch['use_bias'],
                B, 200, None, seed=1, graph=False)
 g.load_params(net)
-g.build_graph(2000)
+g.build_graph(4000)
 g.init_buffers(list(range(1, B + 1)) if arch['n_gc_embed'] else None)
 g.step(1000)
 torch.cuda.synchronize()
 L = arch['n_blocks'] * arch['n_block_layers']
-rows, gv, ps = [], [], []
+runs = []
 for _ in range(5):
-    g.step(2)   # the second launch draws the first step itself (the fused path)
+    g.step(20)
     torch.cuda.synchronize()
-    full = g.tensor('trace', torch.int64).cpu().numpy()
-    tr = full[:4 + 2 * L]
-    rows.append(np.diff(np.concatenate([tr[:3], tr[4:4 + 2 * L]])))
-    gv.append(full[2 * L + 8:2 * L + 8 + 24].reshape(3, 8).astype(np.int64))
-    ps.append(full[2 * L + 40:2 * L + 40 + 3 * B].reshape(B, 3).astype(np.int64))
-d = np.median(np.array(rows), axis=0)
-print('cycles: input %d  wait for taps+layer 0 %d  first-conv %d' % (d[0], d[1], d[2]))
-conv, res = d[4::2], d[3::2][:L]
-print('per layer (median over layers): conv+gate %.0f  residual %.0f   total %.0f cycles' %
-      (np.median(conv), np.median(res), np.median(conv) + np.median(res)))
-print('layers:', ' '.join('%d/%d' % (c, r) for c, r in zip(d[2::2][:L], d[3::2][:L])))
-print('total kernel cycles (stamps): %d' % (np.sum(d)))
-gm = np.median(np.array(gv), axis=0)
-w = gm[0]
-print('wall (us from chain block 0 start): chain end %.2f; last skip helper start %.2f, end %.2f'
-      % ((w[1] - w[0]) / 100.0, (w[2] - w[0]) / 100.0, (w[3] - w[0]) / 100.0))
-print('  last helper: layer-a poll done %.2f, layer-b poll done %.2f, accumulated %.2f'
-      % ((w[4] - w[0]) / 100.0, (w[6] - w[0]) / 100.0, (w[5] - w[0]) / 100.0))
-for name, s in zip(['post1', 'post2'], gm[1:]):
-    print('gemv %-5s block0 %5.2f us (staged %d cyc, compute+store %d cyc); last block starts +%.2f us, ends +%.2f us'
-          % (name, (s[1] - s[0]) / 100.0, s[3] - s[2], s[4] - s[3], (s[6] - s[0]) / 100.0, (s[7] - s[0]) / 100.0))
-print('gap: post1->post2 start %.2f us' % ((gm[2][0] - gm[1][0]) / 100.0))
-pm = np.median(np.array(ps) - np.array(gv)[:, :1, :1], axis=0) / 100.0
-print('per stream (us from chain block 0 start): start / input ready / chain end')
-for b in range(B):
-    print('  stream %2d  %6.2f %6.2f %6.2f' % (b, pm[b, 0], pm[b, 1], pm[b, 2]))
+    runs.append(g.tensor('trace', torch.int64).cpu().numpy().astype(np.int64).copy())
+tr = np.median(np.array(runs), axis=0)
+if g.persistent:
+    us = lambda x: (x - tr[0]) / 100.0   # noqa: E731  (wall_clock64: 100 MHz)
+    print('persistent, B=%d; us from chain block 0 starting step n-1 (after its draw):' % B)
+    lay = np.diff(np.concatenate([[tr[0]], tr[8:8 + L]])) / 100.0
+    print('  chain 0: layers end %.2f  (per layer median %.3f us, first %.3f)' % (us(tr[1]), np.median(lay), lay[0]))
+    hl = us(tr[8 + L:8 + L + (L + 7) // 8])
+    nr = (L + 7) // 8
+    print('  chain 0 layer ends: ' + ' '.join('%.2f' % x for x in us(tr[8:8 + L])[7::8]) + ' (every 8th)')
+    print('  last head, thread 0 (stream 0) sweep done:  ' + ' '.join('%.2f' % x for x in us(tr[8 + L + 40:8 + L + 40 + nr])))
+    print('  last head, round barrier passed:            ' + ' '.join('%.2f' % x for x in us(tr[8 + L + 80:8 + L + 80 + nr])))
+    print('  last head: 8-layer rounds accumulated at    ' + ' '.join('%.2f' % x for x in hl))
+    print('  last head: phase A done %.2f, skip gathered %.2f, partial logits published %.2f'
+          % (us(tr[2]), us(tr[3]), us(tr[4])))
+    print('  last head C: post1 partials %.2f, barrier %.2f, h %.2f' % tuple(us(tr[8 + L + 120:8 + L + 123])))
+    print('  chain 0: logits gathered %.2f, draw done %.2f' % (us(tr[5]), us(tr[6])))
+    print('  step period ~ %.2f us (draw done - start of the step it drew)' % us(tr[6]))
+else:
+    rows = np.diff(np.concatenate([tr[:3], tr[4:4 + 2 * L]]))
+    conv, res = rows[4::2], rows[3::2][:L]
+    print('per-step form, B=%d: input %d cyc, taps+layer 0 wait %d cyc; per layer conv+gate %.0f, residual %.0f cycles'
+          % (B, rows[0], rows[1], np.median(conv), np.median(res)))
+    gm = tr[2 * L + 8:2 * L + 8 + 24].reshape(3, 8)
+    for name, s in zip(['skip', 'post1', 'post2'], gm):
+        print('gemv %-5s block0 %5.2f us (staged %d cyc, compute+store %d cyc); last block ends +%.2f us'
+              % (name, (s[1] - s[0]) / 100.0, s[3] - s[2], s[4] - s[3], (s[7] - s[0]) / 100.0))
