@@ -416,6 +416,41 @@ struct DrawK {
   const int* teacher; long long n_teacher; unsigned long long seed; int* code;
 };
 
+// wave-wide max / min / inclusive scan on DPP (row ops + row_bcast, GFX9): one VALU latency
+// per step instead of a ds_bpermute round trip per __shfl step
+template <int CTRL, int ROWS = 0xF>
+LBWN_DEV int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xF, true); }
+LBWN_DEV float wave_max(float v) {
+  v = fmaxf(v, __int_as_float(dpp_i<0xB1>(__float_as_int(v))));    // quad_perm xor 1
+  v = fmaxf(v, __int_as_float(dpp_i<0x4E>(__float_as_int(v))));    // quad_perm xor 2
+  v = fmaxf(v, __int_as_float(dpp_i<0x141>(__float_as_int(v))));   // row_half_mirror
+  v = fmaxf(v, __int_as_float(dpp_i<0x140>(__float_as_int(v))));   // row_mirror: every row uniform
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+}
+LBWN_DEV int wave_min(int v) {
+  v = min(v, dpp_i<0xB1>(v));
+  v = min(v, dpp_i<0x4E>(v));
+  v = min(v, dpp_i<0x141>(v));
+  v = min(v, dpp_i<0x140>(v));
+  return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+// inclusive prefix sum over the 64 lanes: Hillis-Steele within rows (row_shr 1, 2, 4, 8), then
+// row 15's total into rows 1, 3 and lane 31's into rows 2, 3
+LBWN_DEV float wave_scan(float x) {
+  x += __int_as_float(dpp_i<0x111>(__float_as_int(x)));
+  x += __int_as_float(dpp_i<0x112>(__float_as_int(x)));
+  x += __int_as_float(dpp_i<0x114>(__float_as_int(x)));
+  x += __int_as_float(dpp_i<0x118>(__float_as_int(x)));
+  x += __int_as_float(dpp_i<0x142, 0xA>(__float_as_int(x)));
+  x += __int_as_float(dpp_i<0x143, 0xC>(__float_as_int(x)));
+  return x;
+}
+
 LBWN_DEV uint64_t splitmix(uint64_t seed, uint64_t stream, uint64_t step) {
   uint64_t z = seed * 0x9E3779B97F4A7C15ULL + (stream << 32) + step + 0x632BE59BD9B4E019ULL;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -436,21 +471,15 @@ LBWN_DEV int draw_core(float (&v)[MP], const DrawK& a, int b, long long t, bool 
     if (ok) mx = fmaxf(mx, v[j]);
     if (ok && write) a.logits[(long)b * Q + c0 + j] = v[j];
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  mx = wave_max(mx);
   float e[MP], loc = 0.f;
 #pragma unroll
   for (int j = 0; j < MP; ++j) {
     e[j] = (j < per && c0 + j < Q) ? expf(v[j] - mx) : 0.f;
     loc += e[j];
   }
-  float incl = loc;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float s = __shfl_up(incl, o);
-    if (lane >= o) incl += s;
-  }
-  const float total = __shfl(incl, 63);
+  const float incl = wave_scan(loc);
+  const float total = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(incl), 63));
   const float excl = incl - loc;
   const uint64_t h = splitmix(a.seed, (uint64_t)b, (uint64_t)t);
   const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
@@ -467,8 +496,7 @@ LBWN_DEV int draw_core(float (&v)[MP], const DrawK& a, int b, long long t, bool 
     }
     if (found == Q) found = min(c0 + per, Q) - 1;
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) found = min(found, __shfl_xor(found, o));
+  found = wave_min(found);
   if (found >= Q) found = Q - 1;
   const int next = (t < a.n_teacher) ? a.teacher[t] : found;   // imodel.py:260-269
   if (write && lane == 0) {
@@ -796,8 +824,8 @@ LBWN_DEV void persist_head(const PersistK& a, int m, float* sm) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int B = a.B, L = a.L, Cd = a.Cd, Cs = a.Cs, Cp = a.Cp, Q = a.Q, n = a.n_steps;
   const long long t0 = *a.step;
-  float* ZS = sm;                  // [P_LA layers][16 b][32 k] z of a round
-  float* RS = ZS + P_LA * 512;     // [16 b][512 k] relu(skip + Σb), zero-padded
+  float* ZS = sm;                  // [2][P_LA layers][16 b][32 k] z of a round (double-buffered)
+  float* RS = ZS + 2 * P_LA * 512; // [16 b][512 k] relu(skip + Σb), zero-padded
   float* HP = RS + P_MAXB * 512;   // [32 kg][16 b][16 c] per-thread partials (skip, then post1)
   float* HS = HP + 32 * 256;       // [16 b][16 c] h
   float* P1T = HS + 256;           // [16 c][516] POST1[:, 16m + c] (rows padded: conflict-free b128 reads)
@@ -841,12 +869,12 @@ LBWN_DEV void persist_head(const PersistK& a, int m, float* sm) {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (li >= L || 8 * kql + j >= Cd || scol >= Cs) wv8[j] = 0.f;
-      __syncthreads();   // the previous round's readers are done
+      float* Z = ZS + ((l0 / P_LA) & 1) * (P_LA * 512);   // the other buffer's readers finished last round
 #pragma unroll
-      for (int i = 0; i < P_LA; ++i) ZS[i * 512 + tid] = (zn0 && i < nl) ? zv[i] : 0.f;
+      for (int i = 0; i < P_LA; ++i) Z[i * 512 + tid] = (zn0 && i < nl) ? zv[i] : 0.f;
       __syncthreads();
       if (tr && s == n - 1) tr[8 + L + 80 + l0 / P_LA] = wall_clock64();
-      const float* zr = ZS + wv * 512 + 8 * kql;
+      const float* zr = Z + wv * 512 + 8 * kql;
 #pragma unroll
       for (int bb = 0; bb < P_MAXB; ++bb) {
         if ((bb & 3) == 0) __builtin_amdgcn_sched_barrier(0);   // 4 streams' reads in flight at a time
