@@ -53,6 +53,9 @@ struct lbwn_plan {
   // run beside the MFMA-bound dSKIP on the main stream instead of in front of it
   hipStream_t aux2 = nullptr;
   hipEvent_t ev_chain = nullptr, ev_join2 = nullptr;
+  // forward prologue: the per-step weight packs run on aux2 beside embed / cond / D-sep
+  hipEvent_t ev_pfork = nullptr, ev_pjoin = nullptr;
+  bool wpk_valid = false;        // the f32 layer images were packed this step
   size_t oSPLIT_AUX = 0;
   // Weights pre-split into bf16 planes once per step for the bf16-split GEMMs (gemm.hip):
   // [W3_SKIP_F] SKIPcat as skip-fwd B, [W3_POST1_F] POST1 as post1-fwd B, [W3_POST2_F] POST2 as
@@ -66,6 +69,8 @@ struct lbwn_plan {
     if (ev_join2) (void)hipEventDestroy(ev_join2);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
+    if (ev_pfork) (void)hipEventDestroy(ev_pfork);
+    if (ev_pjoin) (void)hipEventDestroy(ev_pjoin);
   }
   // one-shot event probe
   char probe[32];
@@ -428,6 +433,8 @@ int ensure_device(lbwn_plan* p) {
     LBWN_HIP(hipStreamCreateWithPriority(&p->aux2, hipStreamNonBlocking, greatest));
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_chain, hipEventDisableTiming));
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_join2, hipEventDisableTiming));
+    LBWN_HIP(hipEventCreateWithFlags(&p->ev_pfork, hipEventDisableTiming));
+    LBWN_HIP(hipEventCreateWithFlags(&p->ev_pjoin, hipEventDisableTiming));
   }
   return 0;
 }
@@ -586,20 +593,31 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   float* R2 = at<float>(ws, p->oR2);
   float* LOG = at<float>(ws, p->oLOG);
   float* bsum = at<float>(ws, p->oBSUM);
-  // per-layer weights -> padded LDS images (once per step; reused by the backward)
+  // Weight packs (once per step, reused by the backward) on aux2, forked here and joined before
+  // the chain: they depend only on the weights, so they overlap embed / cond / D-sep below.
+  const bool x3 = lbwn_gemm_mode() == 1;
+  hipStream_t pst = st;
+  if (p->aux2) {
+    LBWN_HIP(hipEventRecord(p->ev_pfork, st));
+    LBWN_HIP(hipStreamWaitEvent(p->aux2, p->ev_pfork, 0));
+    pst = p->aux2;
+  }
+  // per-layer weights -> padded f32 LDS images: the per-layer kernels and the f32 chains (the
+  // bf16-split chains read their own images below)
   float* WPK = at<float>(ws, p->oWPK);
-  if ((e = lbwn_pack_layers_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b, WPK, L, Cr, Cd, st)))
+  p->wpk_valid = !(x3 && p->chain && p->oSG);
+  if (p->wpk_valid &&
+      (e = lbwn_pack_layers_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b, WPK, L, Cr, Cd, pst)))
     return e;
   // skip/head weights -> bf16 planes for the split GEMMs, forward and backward, and the split
-  // per-layer images of the forward chain (once per step)
-  const bool x3 = lbwn_gemm_mode() == 1;
+  // per-layer images of the forward chain
   if (x3 && p->chain &&
       (e = lbwn_pack_layers_x3_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b,
-                                      at<unsigned short>(ws, p->oWPKX), L, Cr, Cd, st)))
+                                      at<unsigned short>(ws, p->oWPKX), L, Cr, Cd, pst)))
     return e;
   // ... and the backward chain's split images (dx weights + f32 residual image)
   if (x3 && p->chain &&
-      (e = lbwn_pack_layers_bx3_launch(P->sig, P->gate, P->res, at<float>(ws, p->oWPKB), L, Cr, Cd, st)))
+      (e = lbwn_pack_layers_bx3_launch(P->sig, P->gate, P->res, at<float>(ws, p->oWPKB), L, Cr, Cd, pst)))
     return e;
   if (x3) {
     const float* wsrc[6] = {P->skip, P->post1, P->post2, P->post2, P->post1, P->skip};
@@ -614,14 +632,16 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
       jo[nj] = at<unsigned short>(ws, p->oW3[i]);
       ++nj;
     }
-    if (nj && (e = lbwn_split_planes_launch(nj, jw, jld, jr, jk, jt, jo, st))) return e;
+    if (nj && (e = lbwn_split_planes_launch(nj, jw, jld, jr, jk, jt, jo, pst))) return e;
   }
+  if (pst != st) LBWN_HIP(hipEventRecord(p->ev_pjoin, pst));
   // one-hot·PRE + PRE_BIAS == row gather (tmodel.py:53-66, :86-102)
   if ((e = lbwn_embed_launch(wav_q, P->pre, P->pre_b, X, B, T, H, Cr, p->Q, st))) return e;
   Cond cd;
   if ((e = cond_forward(p, P, ws, mel, cd, st))) return e;
   // D-separation prepend for every layer (tmodel.py:122-127)
   if ((e = lbwn_dsep_prepend_launch(X, p->x_layer_stride, save, L, p->nbl, B, T, H, Cr, st))) return e;
+  if (pst != st) LBWN_HIP(hipStreamWaitEvent(st, p->ev_pjoin, 0));   // the packs joined
   if (p->chain) {
     // all layers in one persistent launch (tmodel.py:313-325)
     lbwn_chain_args c;
@@ -809,6 +829,13 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     cd.dv_out = at<float>(ws, p->oDVALL);
   }
   const float* WPK = at<float>(ws, p->oWPK);
+  if (!p->wpk_valid && !(p->chain && p->fwd_x3 && lbwn_gemm_mode() == 1)) {
+    // the forward skipped the f32 images (bf16-split chains) but this backward takes an f32 path
+    if ((e = lbwn_pack_layers_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b,
+                                     at<float>(ws, p->oWPK), L, Cr, Cd, st)))
+      return e;
+    p->wpk_valid = true;
+  }
   const int sstr = lbwn_layer_slab_stride();
   float* SLABS = at<float>(ws, p->oSLAB);
   if (p->chain) {
