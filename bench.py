@@ -90,8 +90,9 @@ def gen_bytes_per_step(arch, B):
     return w + B * per_stream
 
 
-def _gen(net, arch, B, chunk, env=None):
-    import torch
+def _gen(net, arch, B, chunk, max_steps, env=None):
+    """A generator with the benchmark net's weights and its plan built (the plan reads
+    LBWN_GEN_* at creation, so `env` applies there)."""
     from lbwn.imodel import WaveNetGen
     old = {k: os.environ.get(k) for k in (env or {})}
     os.environ.update(env or {})
@@ -100,6 +101,7 @@ def _gen(net, arch, B, chunk, env=None):
                        arch['n_skip'], arch['n_post'], arch['n_gc_embed'], arch['n_gc_category'], arch['use_bias'],
                        B, chunk, None, seed=1, graph=True)
         g.load_params(net)
+        g.build_graph(max_steps)
         return g
     finally:
         for k, v in old.items():
@@ -110,9 +112,8 @@ def _gen(net, arch, B, chunk, env=None):
 
 
 def _gen_rate(g, arch, B, n, chunk):
-    """us per step over n steps (graph replay of chunk-step runs), after a warm chunk."""
+    """wall time of n steps (graph replay of chunk-step runs), after a warm chunk."""
     import torch
-    g.build_graph(n + chunk)
     gc = [1 + b % max(1, arch['n_gc_category']) for b in range(B)] if arch['n_gc_embed'] else None
     g.init_buffers(gc)
     g.step(chunk)   # capture + warm
@@ -131,8 +132,8 @@ def gen_layer_latency(net, arch, B):
     residual), from the persistent kernel's in-kernel stamps (LBWN_GEN_TRACE plan)."""
     import torch
     from lbwn.arch import n_layers
-    g = _gen(net, arch, B, 50, env={'LBWN_GEN_TRACE': '1'})
-    if not (g.build_graph(400) and g.persistent):
+    g = _gen(net, arch, B, 50, 400, env={'LBWN_GEN_TRACE': '1'})
+    if not g.persistent:
         return None
     g.init_buffers([1 + b % max(1, arch['n_gc_category']) for b in range(B)] if arch['n_gc_embed'] else None)
     g.step(300)
@@ -149,7 +150,7 @@ def bench_gen(net, arch, B=10, seconds=3.0, sr=16000, chunk=1000, sweep=(16, 64,
     the step time against the latency floor of its dependent chain."""
     from lbwn.arch import n_layers
     n = int(seconds * sr)
-    g = _gen(net, arch, B, chunk)
+    g = _gen(net, arch, B, chunk, n + chunk)
     dt = _gen_rate(g, arch, B, n, chunk)
     us = dt / n * 1e6
     bps = gen_bytes_per_step(arch, B)
@@ -174,7 +175,7 @@ def bench_gen(net, arch, B=10, seconds=3.0, sr=16000, chunk=1000, sweep=(16, 64,
     rows = []
     for Bs in sweep:
         ns = 2000
-        gs = _gen(net, arch, Bs, 500)
+        gs = _gen(net, arch, Bs, 500, ns + 500)
         dts = _gen_rate(gs, arch, Bs, ns, 500)
         bs = gen_bytes_per_step(arch, Bs)
         rows.append({'batch': Bs, 'us_per_step': dts / ns * 1e6, 'samples_per_s': Bs * ns / dts,

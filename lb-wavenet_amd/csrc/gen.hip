@@ -858,22 +858,26 @@ LBWN_DEV void persist_head(const PersistK& a, int m, float* sm) {
     float pa[P_MAXB];
 #pragma unroll
     for (int bb = 0; bb < P_MAXB; ++bb) pa[bb] = 0.f;
-    for (int l0 = 0; l0 < L; l0 += P_LA) {
-      const int nl = min(P_LA, L - l0), li = l0 + wv;
+    // rounds are aligned to the END of the stack: the last round is layer L-1 alone, so the
+    // round before it finishes while the chains run their last layer and the tail after the
+    // chains is one poll + one layer (the first round takes the remainder)
+    const int first = (L - 1) % P_LA == 0 ? P_LA : (L - 1) % P_LA;
+    for (int l0 = 0, r = 0; l0 < L; l0 += (l0 == 0 ? first : P_LA), ++r) {
+      const int nl = l0 == L - 1 ? 1 : (l0 == 0 ? min(first, L) : P_LA), li = l0 + wv;
       float wv8[8], zv[P_LA];
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         wv8[j] = wsrc[((long)min(li, L - 1) * Cd + min(j, Cd - 1 - 8 * kql)) * Cs];
       sweep<P_LA>(a.zg, (unsigned)(((zn0 ? zb0 : 0) * L + l0) * 32 + (zn0 ? zk : 0)), 32u, nl, tag, zv, a.status);
-      if (tr && s == n - 1) tr[8 + L + 40 + l0 / P_LA] = wall_clock64();
+      if (tr && s == n - 1) tr[8 + L + 40 + r] = wall_clock64();
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (li >= L || 8 * kql + j >= Cd || scol >= Cs) wv8[j] = 0.f;
-      float* Z = ZS + ((l0 / P_LA) & 1) * (P_LA * 512);   // the other buffer's readers finished last round
+      float* Z = ZS + (r & 1) * (P_LA * 512);   // the other buffer's readers finished last round
 #pragma unroll
       for (int i = 0; i < P_LA; ++i) Z[i * 512 + tid] = (zn0 && i < nl) ? zv[i] : 0.f;
       __syncthreads();
-      if (tr && s == n - 1) tr[8 + L + 80 + l0 / P_LA] = wall_clock64();
+      if (tr && s == n - 1) tr[8 + L + 80 + r] = wall_clock64();
       const float* zr = Z + wv * 512 + 8 * kql;
 #pragma unroll
       for (int bb = 0; bb < P_MAXB; ++bb) {
@@ -892,7 +896,7 @@ LBWN_DEV void persist_head(const PersistK& a, int m, float* sm) {
           pa[bb] = x;
         }
       }
-      if (tr && s == n - 1) tr[8 + L + l0 / P_LA] = wall_clock64();
+      if (tr && s == n - 1) tr[8 + L + r] = wall_clock64();
     }
     // reduce the 32 per-thread partials of each (stream, column) through LDS (no shuffles:
     // their dependent LDS round trips cost ~2 us per phase)

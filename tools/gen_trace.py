@@ -37,8 +37,8 @@ if g.persistent:
     print('persistent, B=%d; us from chain block 0 starting step n-1 (after its draw):' % B)
     lay = np.diff(np.concatenate([[tr[0]], tr[8:8 + L]])) / 100.0
     print('  chain 0: layers end %.2f  (per layer median %.3f us, first %.3f)' % (us(tr[1]), np.median(lay), lay[0]))
-    hl = us(tr[8 + L:8 + L + (L + 7) // 8])
-    nr = (L + 7) // 8
+    nr = 1 + (L - 1 + 7) // 8
+    hl = us(tr[8 + L:8 + L + nr])
     print('  chain 0 layer ends: ' + ' '.join('%.2f' % x for x in us(tr[8:8 + L])[7::8]) + ' (every 8th)')
     print('  last head, thread 0 (stream 0) sweep done:  ' + ' '.join('%.2f' % x for x in us(tr[8 + L + 40:8 + L + 40 + nr])))
     print('  last head, round barrier passed:            ' + ' '.join('%.2f' % x for x in us(tr[8 + L + 80:8 + L + 80 + nr])))
