@@ -13,7 +13,12 @@ M = 32768
 # name, M, N, K, a_kcontig, b_kcontig, split
 SHAPES = [('skip_fwd', M, 512, 1600, 1, 0, 1), ('dz', M, 1600, 512, 1, 1, 1), ('dskip', 1600, 512, M, 0, 0, 19),
           ('post1_fwd', M, 512, 512, 1, 0, 1), ('ds', M, 512, 512, 1, 1, 1), ('dpost1', 512, 512, M, 0, 0, 4),
-          ('post2_fwd', M, 256, 512, 1, 0, 1), ('dh', M, 512, 256, 1, 1, 1), ('dpost2', 512, 256, M, 0, 0, 8)]
+          ('post2_fwd', M, 256, 512, 1, 0, 1), ('dh', M, 512, 256, 1, 1, 1), ('dpost2', 512, 256, M, 0, 0, 8),
+          # arch5 local conditioning (M = B·T = 32768 at B = 8): COND = lc·LCcat, dlc = DV·LCcatᵀ,
+          # dLCCAT = lcᵀ·DV (K = 80 channels, or padded to 96)
+          ('lc_cond', M, 3200, 80, 1, 0, 1), ('lc_cond96', M, 3200, 96, 1, 0, 1),
+          ('lc_dlc', M, 80, 3200, 1, 1, 1), ('lc_dlc96', M, 96, 3200, 1, 1, 1),
+          ('lc_dcat', 80, 3200, M, 0, 0, 8), ('lc_dcat96', 96, 3200, M, 0, 0, 8)]
 
 
 def timeit(fn, reps=20):
