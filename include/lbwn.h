@@ -170,6 +170,22 @@ int lbwn_layer_forward(const float* x_in, float* x_out, float* z, int64_t ldz, c
                        int64_t ldcond, int B, int T, int H, int dilation, int n_res, int n_dil, float* wpack_ws,
                        void* stream);
 
+/* One residual layer backward: TF's autodiff of tmodel.py:117-184 for one layer (the SURVEY
+ * §8b lbwn_dilconv_gate_bwd).  Inputs as lbwn_layer_forward plus dz = dL/dz from the skip path
+ * ([M] rows, stride lddz) and dx_out = dL/dx_out of the layer's output x_{l+1} ([M][n_res], NULL
+ * for the last layer).  Recomputes the gate from x_in.  Writes dx_in = dL/d(x_in) over the whole
+ * [B][H+T][n_res] halo buffer (rows [H-d, H) are the SAVE rows' share; earlier rows 0), the
+ * weight and bias gradients in the reference layouts (overwritten), dcond = dL/d(cond) ([M] rows
+ * of 2·n_dil, stride lddcond) when cond is given, and adds into gc_dtab [ncat+1][2·n_dil] (per
+ * voice id) when given.  ws: 16-B aligned scratch of lbwn_layer_backward_ws_floats() floats. */
+int64_t lbwn_layer_backward_ws_floats(int B, int T, int n_res);
+int lbwn_layer_backward(const float* x_in, const float* dz, int64_t lddz, const float* dx_out, const float* w_sig,
+                        const float* w_gate, const float* b_sig, const float* b_gate, const float* w_res,
+                        const float* b_res, const float* gc_tab, const int* ids, const float* cond, int64_t ldcond,
+                        float* dx_in, float* dw_sig, float* dw_gate, float* db_sig, float* db_gate, float* dw_res,
+                        float* db_res, float* dcond, int64_t lddcond, float* gc_dtab, int B, int T, int H, int dilation,
+                        int n_res, int n_dil, float* ws, void* stream);
+
 /* D-separation prepend/save for all layers at once (tmodel.py:122-127, :165). */
 int lbwn_dsep_prepend(float* x_all, int64_t x_layer_stride, const float* save, int n_layers, int n_block_layers,
                       int B, int T, int H, int n_res, void* stream);

@@ -81,6 +81,54 @@ int lbwn_layer_forward(const float* x_in, float* x_out, float* z, int64_t ldz, c
   return lbwn_layer_fwd_launch(a, (hipStream_t)stream);
 }
 
+// workspace of lbwn_layer_backward: packed image | per-tile weight-gradient slabs | out_a | out_c0
+int64_t lbwn_layer_backward_ws_floats(int B, int T, int n_res) {
+  const long M = (long)B * T;
+  return (int64_t)lbwn_layer_image_floats() + (int64_t)lbwn_layer_bwd_grid(B, T) * lbwn_layer_slab_stride() +
+         2 * (int64_t)M * n_res + 64;
+}
+
+int lbwn_layer_backward(const float* x_in, const float* dz, int64_t lddz, const float* dx_out, const float* w_sig,
+                        const float* w_gate, const float* b_sig, const float* b_gate, const float* w_res,
+                        const float* b_res, const float* gc_tab, const int* ids, const float* cond, int64_t ldcond,
+                        float* dx_in, float* dw_sig, float* dw_gate, float* db_sig, float* db_gate, float* dw_res,
+                        float* db_res, float* dcond, int64_t lddcond, float* gc_dtab, int B, int T, int H, int dilation,
+                        int n_res, int n_dil, float* ws, void* stream) {
+  LBWN_REQUIRE(x_in && dz && w_sig && w_gate && w_res && dx_in && dw_sig && dw_gate && dw_res && ws,
+               "layer_backward: null argument");
+  LBWN_REQUIRE(!gc_tab || ids, "layer_backward: gc_tab needs ids");
+  LBWN_REQUIRE(!gc_dtab || gc_tab, "layer_backward: gc_dtab needs gc_tab");
+  LBWN_REQUIRE(!dcond || cond, "layer_backward: dcond needs cond");
+  LBWN_REQUIRE((((uintptr_t)ws) & 15) == 0, "layer_backward: workspace must be 16-B aligned");
+  hipStream_t st = (hipStream_t)stream;
+  const long M = (long)B * T;
+  float* img = ws;
+  float* slab = img + lbwn_layer_image_floats();
+  const int nblk = lbwn_layer_bwd_grid(B, T), sstr = lbwn_layer_slab_stride();
+  float* out_a = slab + (long)nblk * sstr;
+  out_a += (16 - ((uintptr_t)out_a & 15)) / 4 % 4;
+  float* out_c0 = out_a + M * n_res;
+  lbwn_layer_args a;
+  memset(&a, 0, sizeof(a));
+  a.x_in = x_in; a.dz_skip = dz; a.lddz = (long)lddz;
+  a.g_a = dx_out; a.g_c0 = nullptr; a.g_d = 0;   // the caller's dL/dx_{l+1}, already combined
+  a.w_sig = w_sig; a.w_gate = w_gate; a.b_sig = b_sig; a.b_gate = b_gate; a.w_res = w_res; a.b_res = b_res;
+  a.gc_tab = gc_tab; a.ids = ids; a.cond = cond; a.ldcond = (long)ldcond;
+  a.dv_out = dcond; a.lddv = (long)lddcond; a.gc_dtab = gc_dtab;
+  a.out_a = out_a; a.out_c0 = out_c0;
+  a.slab = slab; a.slab_stride = sstr;
+  a.B = B; a.T = T; a.H = H; a.d = dilation; a.Cr = n_res; a.Cd = n_dil;
+  a.wpack = img;
+  if (int e = lbwn_pack_layers_launch(w_sig, w_gate, b_sig, b_gate, w_res, b_res, img, 1, n_res, n_dil, st)) return e;
+  if (int e = lbwn_layer_bwd_launch(a, st)) return e;
+  lbwn_layer_red_args r;
+  memset(&r, 0, sizeof(r));
+  r.slab = slab; r.nparts = nblk; r.stride = sstr; r.Cr = n_res; r.Cd = n_dil;
+  r.dsig = dw_sig; r.dgate = dw_gate; r.dres = dw_res; r.dbsig = db_sig; r.dbgate = db_gate; r.dbres = db_res;
+  if (int e = lbwn_layer_reduce_launch(r, st)) return e;
+  return lbwn_layer_dx_combine_launch(out_a, out_c0, dx_in, B, T, H, dilation, n_res, st);
+}
+
 int lbwn_dsep_prepend(float* x_all, int64_t xls, const float* save, int n_layers, int nbl, int B, int T, int H,
                       int n_res, void* stream) {
   LBWN_REQUIRE(H >= (1 << (nbl - 1)), "dsep_prepend: halo %d < max dilation", H);

@@ -73,6 +73,8 @@ int lbwn_pack_layers_x3_launch(const float* sig, const float* gate, const float*
                                const float* res, const float* res_b, unsigned short* out, int L, int Cr, int Cd,
                                hipStream_t st);
 int lbwn_layer_image_floats();
+int lbwn_layer_dx_combine_launch(const float* out_a, const float* out_c0, float* dx, int B, int T, int H, int d, int C,
+                                 hipStream_t st);
 // backward split images (WD bf16 + Rs f32) for the bf16-split backward chain, floats per layer
 int lbwn_layer_image_bx3_floats();
 int lbwn_pack_layers_bx3_launch(const float* sig, const float* gate, const float* res, float* out, int L, int Cr,

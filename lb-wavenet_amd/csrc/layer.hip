@@ -203,9 +203,9 @@ LBWN_DEV void stage_g(float* G, const float* __restrict__ ga, const float* __res
       const int e = tid + 256 * i;
       const int r = e >> 3, c4 = (e & 7) * 4, t = t0 + r;
       v[i] = *(const floatx4*)(ga + (mb + min(t, T - 1)) * 32 + c4);       // clamped, then select
-      u[i] = *(const floatx4*)(gc + (mb + min(t + gd, T - 1)) * 32 + c4);
+      u[i] = gc ? *(const floatx4*)(gc + (mb + min(t + gd, T - 1)) * 32 + c4) : floatx4{0.f, 0.f, 0.f, 0.f};
       if (t >= T) v[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-      if (t + gd >= T) u[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if (t + gd >= T || !gc) u[i] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -218,7 +218,7 @@ LBWN_DEV void stage_g(float* G, const float* __restrict__ ga, const float* __res
       float v = 0.f;
       if (t < T && c < C) {
         v = ga[(mb + t) * C + c];
-        if (t + gd < T) v += gc[(mb + t + gd) * C + c];
+        if (gc && t + gd < T) v += gc[(mb + t + gd) * C + c];
       }
       G[r * XS + c] = v;
     }
@@ -1849,6 +1849,35 @@ BwdK to_bwd(const lbwn_layer_args& a) {
 
 int lbwn_layer_slab_stride() { return SLAB; }
 int lbwn_layer_image_floats() { return WIMG; }
+
+namespace {
+// dL/d(halo buffer) of one layer from its backward's two outputs: out_a[t] = dL/dx[t] (own tap
+// and residual) and out_c0[t] = dL/d(dilated tap input at t), which is halo row H + t - d.
+__global__ void layer_dx_combine_kernel(const float* __restrict__ a, const float* __restrict__ c0, float* __restrict__ dx,
+                                        int B, int T, int H, int d, int C) {
+  const long total = (long)B * (H + T) * C;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const long br = e / C;
+    const int row = (int)(br % (H + T)), b = (int)(br / (H + T));
+    const int s = row - H;
+    const long mb = (long)b * T;
+    float v = 0.f;
+    if (s >= 0) v = a[(mb + s) * C + c];
+    if (s + d >= 0 && s + d < T) v += c0[(mb + s + d) * C + c];
+    dx[e] = v;
+  }
+}
+}  // namespace
+
+int lbwn_layer_dx_combine_launch(const float* out_a, const float* out_c0, float* dx, int B, int T, int H, int d, int C,
+                                 hipStream_t st) {
+  const long total = (long)B * (H + T) * C;
+  layer_dx_combine_kernel<<<(int)std::min<long>((total + 255) / 256, 4096), 256, 0, st>>>(out_a, out_c0, dx, B, T, H,
+                                                                                          d, C);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
 int lbwn_layer_image_x3_elems() { return XIMG_US; }
 int lbwn_layer_image_bx3_floats() { return BIMG_F; }
 int lbwn_pack_layers_bx3_launch(const float* sig, const float* gate, const float* res, float* out, int L, int Cr,

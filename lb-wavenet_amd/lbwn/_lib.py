@@ -67,6 +67,10 @@ _SIGS = {
     'lbwn_layer_image_floats_abi': (c_int, []),
     'lbwn_layer_forward': (c_int, [c_fp, c_fp, c_fp, c_int64, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp,
                                    c_fp, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_fp, c_void_p]),
+    'lbwn_layer_backward_ws_floats': (c_int64, [c_int, c_int, c_int]),
+    'lbwn_layer_backward': (c_int, [c_fp, c_fp, c_int64, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp,
+                                    c_int64, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_int64, c_fp, c_int,
+                                    c_int, c_int, c_int, c_int, c_int, c_fp, c_void_p]),
     'lbwn_dsep_prepend': (c_int, [c_fp, c_int64, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     'lbwn_dsep_save': (c_int, [c_fp, c_int64, c_fp, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]),
     'lbwn_head_xent': (c_int, [c_fp, c_fp, c_fp, c_int, c_int, c_int, c_int, c_fp, c_fp, c_void_p]),

@@ -50,3 +50,25 @@ def test_plan_rejects_bad_arch_without_gpu():
     a.n_res, a.n_dil, a.n_skip, a.n_post = 3, 4, 8, 6
     assert lib.lbwn_plan_create(ctypes.byref(a), 2, 512, ctypes.byref(h)) == 0
     lib.lbwn_plan_destroy(h)
+
+
+def test_torch_ops_registered_device_only():
+    """lbwn::dilconv_gate / lbwn::dilconv_gate_bwd are torch.library ops with autograd; they have
+    no CPU kernel (the oracle is never a fallback), so CPU tensors fail loudly."""
+    import pytest
+    import torch
+    from lbwn import torch_ops  # noqa: F401  (registers the ops)
+    assert hasattr(torch.ops.lbwn, 'dilconv_gate') and hasattr(torch.ops.lbwn, 'dilconv_gate_bwd')
+    x = torch.zeros(1, 10, 32)
+    w = torch.zeros(2, 32, 32)
+    b = torch.zeros(32)
+    with pytest.raises((NotImplementedError, RuntimeError)):
+        torch.ops.lbwn.dilconv_gate(x, w, w, b, b, torch.zeros(32, 32), b, 2, 4)
+    # shapes through the fake (meta) kernels
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    with FakeTensorMode():
+        xf = torch.empty(2, 4 + 100, 32, device='cuda')
+        wf = torch.empty(2, 32, 16, device='cuda')
+        z, xo = torch.ops.lbwn.dilconv_gate(xf, wf, wf, torch.empty(16, device='cuda'), torch.empty(16, device='cuda'),
+                                            torch.empty(16, 32, device='cuda'), torch.empty(32, device='cuda'), 4, 4)
+        assert tuple(z.shape) == (2, 100, 16) and tuple(xo.shape) == (2, 100, 32)
