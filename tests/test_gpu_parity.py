@@ -249,10 +249,11 @@ def _run_oracle(arch, net, q, ids):
 
 
 @pytest.mark.parametrize('which,B,T,mode', [('small', 2, 256, 1), ('small', 3, 200, 1), ('arch3', 2, 512, 1),
-                                            ('arch3', 2, 512, 0)])
+                                            ('arch3', 2, 512, 0), ('arch3', 8, 4096, 1)])
 def test_plan_forward_backward(lib, gemm_mode, which, B, T, mode):
     """mode 1: GEMMs and the forward chain's conv/residual on the bf16 cores by exact splitting;
-    mode 0: every product on the f32 MFMA.  Same bars for both."""
+    mode 0: every product on the f32 MFMA.  Same bars for both.  ('arch3', 8, 4096) is the
+    benchmarked C2 shape itself: 256 tiles of the persistent chains, every gradient vs float64."""
     gemm_mode(mode)
     arch = arch3() if which == 'arch3' else small_arch()
     net = make_net(arch, B)
