@@ -135,6 +135,9 @@ size_t carve(size_t& cur, size_t bytes) {
   return o;
 }
 
+// rows of the SG buffer: whole 32-row blocks (sg_off in layer.hip)
+static long m32(long M) { return (M + 31) / 32 * 32; }
+
 // Split-K for the weight-gradient GEMMs (K = B·T positions).  One 4-wave block per CU
 // leaves the MFMA pipe latency-exposed, so aim for ~4 resident blocks per CU (1024 blocks)
 // with the slab traffic capped at 64 MB.
@@ -327,7 +330,7 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   const char* nc = getenv("LBWN_NO_CHAIN");
   p->chain = p->Cr == 32 && p->Cd == 32 && !(nc && nc[0] == '1');
   p->oOCG = p->chain ? carve(cur, sizeof(float) * (size_t)L * M * 32) : 0;
-  p->oSG = p->chain ? carve(cur, sizeof(float) * (size_t)L * M * 32) : 0;
+  p->oSG = p->chain ? carve(cur, sizeof(float) * (size_t)L * m32(M) * 32) : 0;   // sg_off: whole 32-row blocks
   const char* ov = getenv("LBWN_OVERLAP");
   p->overlap = p->chain && !(ov && ov[0] == '0');
   // dSKIP after the chain on the main stream at full rate (default): with the backward chain at
@@ -648,7 +651,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     memset(&c, 0, sizeof(c));
     c.X = X; c.xls = p->x_layer_stride; c.Z = Z; c.ldz = ldz; c.wpack = WPK; c.ids = ids;
     c.wpack_x3 = x3 ? at<unsigned short>(ws, p->oWPKX) : nullptr;
-    if (x3 && p->oSG) { c.SG = at<float>(ws, p->oSG); c.sgls = M * 32; }
+    if (x3 && p->oSG) { c.SG = at<float>(ws, p->oSG); c.sgls = m32(M) * 32; }
     p->fwd_x3 = c.SG != nullptr;
     c.gc_tab = cd.gc_tab; c.gc_ld = cd.gc_ld; c.cond = cd.cond; c.ldcond = cd.ldcond;
     c.flags = at<unsigned>(ws, p->oFLAGS); c.status = at<unsigned>(ws, p->oSTATUS);
@@ -844,7 +847,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     memset(&c, 0, sizeof(c));
     c.X = X; c.xls = p->x_layer_stride; c.DZ = DZ; c.ldz = ldz; c.wpack = WPK; c.ids = ids;
     if (p->fwd_x3 && lbwn_gemm_mode() == 1) {   // bf16-split backward: no gate recompute (SG)
-      c.Z = Z; c.SG = at<float>(ws, p->oSG); c.sgls = M * 32; c.bimg = at<float>(ws, p->oWPKB);
+      c.Z = Z; c.SG = at<float>(ws, p->oSG); c.sgls = m32(M) * 32; c.bimg = at<float>(ws, p->oWPKB);
     }
     c.slab = SLABS; c.ocg = at<float>(ws, p->oOCG); c.ocls = M * 32;
     c.gc_tab = cd.gc_tab; c.gc_ld = cd.gc_ld; c.cond = cd.cond; c.ldcond = cd.ldcond;

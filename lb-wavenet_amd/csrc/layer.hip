@@ -281,6 +281,11 @@ LBWN_DEV void conv_tile(const float* Xp, const float* Xc, const float* Ws, const
   }
 }
 
+// σ(v_gate) rows (SG) are stored in 32-row blocks laid out in the MFMA register order, [m/32][q][m%32][h][4]
+// (channel 8q + 4h + j), so that each wave-instruction of the forward's stores and of the backward's
+// loads covers one contiguous KiB instead of 32 partial lines
+LBWN_DEV long sg_off(long m, int q, int h) { return (((m >> 5) * 4 + q) * 32 + (m & 31)) * 8 + 4 * h; }
+
 LBWN_DEV void store_rows16(float* row, const floatx16& v, int C, int h) {
   if (C == 32) {
 #pragma unroll
@@ -376,7 +381,7 @@ struct ChainFK {
   int B, T, H, L, nbl, Cd;
   long long* trace; int trace_blk;   // debug stamps (null in production)
   const unsigned short* ximg;        // L split images (XIMG_US bf16 each): the bf16-split form
-  float* SG; long sgls;              // σ(v_gate) rows [L][M][32] for chain_bwd_x3_kernel, or null
+  float* SG; long sgls;              // σ(v_gate) rows [L][M32][32] (sg_off blocks) for chain_bwd_x3_kernel, or null
 };
 
 // GC + LC term of layer l for this lane's position, in acc layout: cv[q] = sig channels
@@ -664,7 +669,12 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
       __syncthreads();
       if (tid == 0 && l + 1 < a.L) publish_flag(a.flags + tile, (unsigned)(l + 1));
       if (valid) store_rows16(a.Z + m * a.ldz + (long)l * a.Cd, z, a.Cd, h);  // skip GEMM input
-      if (X3 && a.SG && valid) store_rows16(a.SG + (long)l * a.sgls + m * 32, sgv, 32, h);
+      if (X3 && a.SG && valid) {
+        float* sgl = a.SG + (long)l * a.sgls;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *(floatx4*)(sgl + sg_off(m, q, h)) = floatx4{sgv[4 * q], sgv[4 * q + 1], sgv[4 * q + 2], sgv[4 * q + 3]};
+      }
       FSTAMP(6);
       // 9. image of layer l+2 into IMG[l&1] (everyone is past this layer's reads of it)
       if (l + 2 < a.L) {
@@ -1294,7 +1304,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
       for (int q = 0; q < 4; ++q) {
         dzr[q] = *(const floatx4*)(a.DZ + mc * a.lddz + (long)l * 32 + 8 * q + 4 * h);
         zr[q] = *(const floatx4*)(a.Zf + mc * a.lddz + (long)l * 32 + 8 * q + 4 * h);
-        sgr[q] = *(const floatx4*)(a.SG + (long)l * a.sgls + mc * 32 + 8 * q + 4 * h);
+        sgr[q] = *(const floatx4*)(a.SG + (long)l * a.sgls + sg_off(mc, q, h));
       }
     };
     auto dma_image = [&](int l) {
@@ -1473,40 +1483,53 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
         gc_scatter_x3(a.gc_dtab + (long)l * 64, a.gc_ld, a.ids + mb, DVs, DVg, t0, a.T, w, lane, 32,
                       wave_uni ? wave_id : -1);
       XSTAMP(4);
-      // 6. dSIG / dGATE tile w: A[i=in][k=pos] = X[pos][in], B[k][j=o] = DV[pos][o]; positions of
-      //    k-step s: p = 16s + 2j + h (the lane halves read rows of opposite parity: no conflicts)
-      floatx16 accW;
+      // 6. dSIG / dGATE partials of ALL four tiles t (0 sig·prev, 1 sig·cur, 2 gate·prev, 3
+      //    gate·cur) over this wave's own 32 positions: A[i=in][k=pos] = X[pos][in], B[k][j=o] =
+      //    DV[pos][o], k-step s: p = 32w + 16s + 2j + h (the lane halves read rows of opposite
+      //    parity).  Every X and DV value is split once per layer (one tile per wave over all 128
+      //    positions split each twice); the four waves' partials are summed through LDS at the end.
+      floatx16 accT[4];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) accW[q] = 0.f;
+      for (int t4 = 0; t4 < 4; ++t4)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) accT[t4][q] = 0.f;
       {
-        const float* X = (w & 1) ? Xc : Xp;
-        const float* DP = (w >> 1) ? DVg : DVs;
-        float xa[2][8], da[2][8];
-        auto loadk = [&](int s2, int buf) {
+        const float* isrc = a.bimg + (long)(l > 0 ? l - 1 : 0) * BIMG_F + lane * 4;
+        // both k-steps' operands are read before the DMA issue (its asm is a compiler barrier for
+        // LDS reads), so that their latency is exposed once
+        float xp[2][8], xc[2][8], ds[2][8], dg[2][8];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const int p = 16 * s2 + 2 * j + h;
-            xa[buf][j] = X[p * 32 + pi];
-            da[buf][j] = DP[swz(p, pi)];
+            const int p = 32 * w + 16 * s2 + 2 * j + h;
+            xp[s2][j] = Xp[p * 32 + pi];
+            xc[s2][j] = Xc[p * 32 + pi];
+            ds[s2][j] = DVs[swz(p, pi)];
+            dg[s2][j] = DVg[swz(p, pi)];
           }
-        };
-        loadk(0, 0);
-        const float* isrc = a.bimg + (long)(l > 0 ? l - 1 : 0) * BIMG_F + lane * 4;
+        XSTAMP(8);
+        if (l > 0) {   // image pieces w, w+4, ... (30 of 1 KiB)
 #pragma unroll
-        for (int s2 = 0; s2 < LP / 16; ++s2) {
-          const int cb = s2 & 1;
-          if (s2 + 1 < LP / 16) loadk(s2 + 1, cb ^ 1);
-          if (l > 0) {
-            const int pc = w + 4 * s2;   // image pieces w, w+4, ... (30 of 1 KiB)
+          for (int i = 0; i < 8; ++i) {
+            const int pc = w + 4 * i;
             if (pc < BIMG_F / 256) dma16(isrc + pc * 256, IMG + pc * 256);
-            if (s2 == 2) load_regs(l - 1);
           }
-          bf16x8 fx[3], fd[3];
-          split8(floatx4{xa[cb][0], xa[cb][1], xa[cb][2], xa[cb][3]},
-                 floatx4{xa[cb][4], xa[cb][5], xa[cb][6], xa[cb][7]}, fx);
-          split8(floatx4{da[cb][0], da[cb][1], da[cb][2], da[cb][3]},
-                 floatx4{da[cb][4], da[cb][5], da[cb][6], da[cb][7]}, fd);
-          accW = mfma_x3(fx, fd, accW);
+          load_regs(l - 1);
+        }
+        XSTAMP(9);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 fxp[3], fxc[3], fds[3], fdg[3];
+          split8(floatx4{xp[s2][0], xp[s2][1], xp[s2][2], xp[s2][3]}, floatx4{xp[s2][4], xp[s2][5], xp[s2][6], xp[s2][7]}, fxp);
+          split8(floatx4{ds[s2][0], ds[s2][1], ds[s2][2], ds[s2][3]}, floatx4{ds[s2][4], ds[s2][5], ds[s2][6], ds[s2][7]}, fds);
+          accT[0] = mfma_x3(fxp, fds, accT[0]);
+          split8(floatx4{xc[s2][0], xc[s2][1], xc[s2][2], xc[s2][3]}, floatx4{xc[s2][4], xc[s2][5], xc[s2][6], xc[s2][7]}, fxc);
+          accT[1] = mfma_x3(fxc, fds, accT[1]);
+          split8(floatx4{dg[s2][0], dg[s2][1], dg[s2][2], dg[s2][3]}, floatx4{dg[s2][4], dg[s2][5], dg[s2][6], dg[s2][7]}, fdg);
+          accT[2] = mfma_x3(fxp, fdg, accT[2]);
+          accT[3] = mfma_x3(fxc, fdg, accT[3]);
+          if (s2 == 0) XSTAMP(10);
         }
       }
       XSTAMP(5);
@@ -1530,6 +1553,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
           for (int j = 0; j < 8; ++j) accR = __builtin_amdgcn_mfma_f32_16x16x4f32(za[j], ga[j], accR, 0, 0, 0);
         }
       }
+      XSTAMP(11);
       // 8. bias partials (column sums of DV and G) and the slab
       float* slab = a.slab + ((long)l * ntiles + tile) * SLAB;
       if (tid < 128) {
@@ -1546,8 +1570,6 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
         for (int p = 0; p < 16; ++p) s4 += *(const floatx4*)(G + swz(pc * 16 + p, c4));
         *(floatx4*)(part + pc * 96 + 64 + c4) = s4;
       }
-#pragma unroll
-      for (int q = 0; q < 16; ++q) slab[w * 1024 + acc_row(q, h) * 32 + pi] = accW[q];
       {
         const int i16 = lane & 15, kg = lane >> 4;
 #pragma unroll
@@ -1559,6 +1581,32 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 #pragma unroll
         for (int pc = 0; pc < 8; ++pc) s1 += part[pc * 96 + tid];
         slab[5120 + tid] = s1;
+      }
+      XSTAMP(12);
+      // dSIG / dGATE: partial of tile t to slot (wave, t) of Xp..DVs (64 KiB, dead until the next
+      // layer's G-build barrier), lane-linear in accumulator order; wave w sums tile w over waves
+      {
+        float* SCR = Xp;
+        const int wu = __builtin_amdgcn_readfirstlane(w);
+#pragma unroll
+        for (int t4 = 0; t4 < 4; ++t4)
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *(floatx4*)(SCR + (wu * 4 + t4) * 1024 + (g * 64 + lane) * 4) =
+                floatx4{accT[t4][4 * g], accT[t4][4 * g + 1], accT[t4][4 * g + 2], accT[t4][4 * g + 3]};
+        __syncthreads();
+        XSTAMP(13);
+        floatx16 accW;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          floatx4 v[4];
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) v[s4] = *(const floatx4*)(SCR + (s4 * 4 + wu) * 1024 + (g * 64 + lane) * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) accW[4 * g + e] = (v[0][e] + v[1][e]) + (v[2][e] + v[3][e]);
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) slab[w * 1024 + acc_row(q, h) * 32 + pi] = accW[q];
       }
       XSTAMP(6);
     }

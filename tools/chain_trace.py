@@ -51,6 +51,12 @@ if net.lib.lbwn_gemm_get_mode() == 1:      # chain_bwd_x3_kernel: XSTAMP(0..6)
         print('  %-26s %6d  (%4.1f %%)' % (n, m, 100.0 * m / per))
     print('  layer period               %6d  = %.2f us at 2.4 GHz;  whole tile %d cycles' %
           (per, per / 2400.0, tr[0, 6] - tr[L - 1, 0]))
+    sub = tr[order][1:-1]
+    if np.all(sub[:, 13] > 0):   # sub-stamps of dSIG (8 reads, 9 DMA issue, 10 k-step 0) and the tail
+        for n, i, j in [('dSIG: operand reads', 4, 8), ('dSIG: DMA + row issue', 8, 9), ('dSIG: k-step 0', 9, 10),
+                        ('dSIG: k-step 1', 10, 5), ('dRES', 5, 11), ('bias + dRES slab + bar', 11, 12),
+                        ('dSIG partials + bar', 12, 13), ('dSIG sum + slab', 13, 6)]:
+            print('    %-26s %6d' % (n, np.median(sub[:, j] - sub[:, i])))
     sys.exit(0)
 names = ['stage x/dz + bar', 'gate recompute', 'G wait+build', 'dz,dv,DV', 'dx MFMA+OC', 'publish bar',
          'dSIG MFMA', 'bar+dRES', 'bias+slab+bar', 'image+bar']

@@ -34,7 +34,9 @@ def timeit(fn, reps=20):
 
 
 only = os.environ.get('GEMM_ONLY')
-for name, m, n, k, akc, bkc, split in SHAPES:
+splits = os.environ.get('GEMM_SPLITS')   # e.g. "4,9,16": every listed split-K for the selected shapes
+runs = [(s[0], s[1], s[2], s[3], s[4], s[5], int(x)) for s in SHAPES for x in splits.split(',')] if splits else SHAPES
+for name, m, n, k, akc, bkc, split in runs:
     if only and name not in only.split(','):
         continue
     A = torch.randn(m, k, device='cuda') if akc else torch.randn(k, m, device='cuda')
