@@ -20,6 +20,7 @@ struct lbwn_plan {
   int Ge, ncat1, Li, Lo, nup, hop, up[8];   // conditioning (Ge = 0: no GC, Lo = 0: no LC)
   long M;
   // workspace carving (byte offsets)
+  size_t oCPART = 0;
   size_t oX, oZ, oS, oR2, oLOG, oDH, oDS, oDZ, oGA[2], oGC0[2], oSLAB, oSPLIT, oSPLIT2, oCOLS,
       oHEADP, oBSUM, oWPK, oWPKX, oFLAGS, oSTATUS, oOCG, oCTRACE;
   // bf16-split backward chain: σ(v_gate) rows from the forward chain [L][M][32], backward images
@@ -319,6 +320,8 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->oSPLIT2 = carve(cur, sizeof(float) * (size_t)lbwn_pre_grad_ws_floats(p->Q, p->Cr));   // dPRE partials
   // three column sums at once in the backward (dlogits, dH1, dS)
   p->oCOLS = carve(cur, sizeof(float) * 3 * (size_t)lbwn_colsum_ws_floats((int)M, std::max({p->Cs, p->Cp, p->Q, p->Cr})));
+  // dH1 / dS column partials from the GEMM epilogues (bias gradients of POST1 / SKIP)
+  p->oCPART = carve(cur, sizeof(float) * (size_t)lbwn_colpart_parts(M) * (p->Cp + p->Cs));
   // [status (16 B) | hand-off flags]: status zeroed once per step, flags before each chain
   p->oSTATUS = carve(cur, 16 + sizeof(unsigned) * (size_t)B * ((T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS));
   p->oFLAGS = p->oSTATUS + 16;
@@ -748,6 +751,10 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   g.A = LOG; g.lda = Q; g.B = P->post2; g.ldb = Q; g.C = DH; g.ldc = Cp; g.M = (int)M; g.N = Cp; g.K = Q;
   g.mask = R2; g.ldm = Cp;
   g.b3 = w3(p, ws, W3_POST2_B);
+  // bias-gradient column partials straight from the epilogues (bf16-split form)
+  float* CPART = at<float>(ws, p->oCPART);
+  const bool fcols = lbwn_gemm_mode() == 1;
+  if (fcols && G->post1_b) g.colpart = CPART;
   Probe(p, st, "dh");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
   Probe::end(p, st, "dh");
@@ -756,6 +763,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   g.A = DH; g.lda = Cp; g.B = P->post1; g.ldb = Cp; g.C = DS; g.ldc = Cs; g.M = (int)M; g.N = Cs; g.K = Cp;
   g.mask = S; g.ldm = Cs;
   g.b3 = w3(p, ws, W3_POST1_B);
+  if (fcols && G->skip_b) g.colpart = CPART + (long)lbwn_colpart_parts(M) * Cp;
   Probe(p, st, "ds");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
   Probe::end(p, st, "ds");
@@ -775,10 +783,27 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     int cn[3], cacc[3] = {0, 0, 0}, nj = 0;
     float* cout[3];
     auto job = [&](const float* x, int n, float* o) { cx[nj] = x; cld[nj] = n; cn[nj] = n; cout[nj] = o; ++nj; };
-    if (G->post2_b) job(LOG, Q, G->post2_b);
-    if (G->post1_b) job(DH, Cp, G->post1_b);
-    if (G->skip_b) job(DS, Cs, G->skip_b);
-    if (nj && (e = lbwn_colsum_multi_launch(nj, cx, cld, cn, cout, cacc, (int)M, COLS, st))) return e;
+    if (!fcols) {
+      if (G->post2_b) job(LOG, Q, G->post2_b);
+      if (G->post1_b) job(DH, Cp, G->post1_b);
+      if (G->skip_b) job(DS, Cs, G->skip_b);
+      if (nj && (e = lbwn_colsum_multi_launch(nj, cx, cld, cn, cout, cacc, (int)M, COLS, st))) return e;
+    } else {   // dlogits: first pass here; dH1 / dS partials came from the GEMM epilogues
+      float* fp[3];
+      float* fo[3];
+      int fn[3], fa[3] = {0, 0, 0}, np[3], nf = 0;
+      if (G->post2_b) {
+        int n0 = 0;
+        if ((e = lbwn_colsum_partial_launch(LOG, Q, (int)M, Q, COLS, &n0, st))) return e;
+        fp[nf] = COLS; fn[nf] = Q; fo[nf] = G->post2_b; np[nf] = n0; ++nf;
+      }
+      if (G->post1_b) { fp[nf] = CPART; fn[nf] = Cp; fo[nf] = G->post1_b; np[nf] = lbwn_colpart_parts(M); ++nf; }
+      if (G->skip_b) {
+        fp[nf] = CPART + (long)lbwn_colpart_parts(M) * Cp; fn[nf] = Cs; fo[nf] = G->skip_b;
+        np[nf] = lbwn_colpart_parts(M); ++nf;
+      }
+      if (nf && (e = lbwn_colsum_final_launch(nf, fp, fn, fo, fa, np, st))) return e;
+    }
     if (G->skip_b && (e = lbwn_bcast_rows_launch(G->skip_b, L, Cs, st))) return e;
   }
   // weight gradients of the head and skip GEMMs (dPOST2, dPOST1; dSKIP unless on the main

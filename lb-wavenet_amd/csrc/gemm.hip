@@ -377,10 +377,11 @@ struct X3Pre {
 // MI = 1 writes one 32-row band (rows m0 + 64·wm … +31) × 64 columns.
 template <int MI>
 LBWN_DEV void x3_epilogue_rows(const lbwn_gemm_args& g, floatx16 (&acc)[MI][2], int m0, int n0, int wm, int wn,
-                               int lane) {
+                               int lane, int nwm = 0, float* red = nullptr) {
   const int h = lane >> 5, ci = lane & 31;
   float* C = g.C + (long)gemm_split() * g.split_stride;
   const bool raw = g.split_stride != 0;
+  float cs[2] = {0.f, 0.f};   // column partials (g.colpart) of this wave's 64-row band, lane half h
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
@@ -408,12 +409,32 @@ LBWN_DEV void x3_epilogue_rows(const lbwn_gemm_args& g, floatx16 (&acc)[MI][2], 
           if (g.mask && !(mv[r] > 0.f)) v = 0.f;
           if (g.accumulate) v += cv[r];
         }
-        if (row < g.M) C[(long)row * g.ldc + col] = v;
+        if (row < g.M) {
+          C[(long)row * g.ldc + col] = v;
+          cs[ni] += v;
+        }
       }
     }
+  // column partials of the block's 256 rows (4 waves along M): lane halves, then waves in a
+  // fixed order through LDS (free after the k-loop's last barrier)
+  if (MI == 2 && red && g.colpart && !raw) {
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      cs[ni] += __shfl_xor(cs[ni], 32);
+      if (h == 0) red[wm * 128 + wn * 64 + ni * 32 + ci] = cs[ni];
+    }
+    __syncthreads();
+    const int t = threadIdx.x, col = n0 + t;
+    if (t < 128 && col < g.N) {
+      float s = 0.f;
+      for (int w = 0; w < nwm; ++w) s += red[w * 128 + t];
+      g.colpart[(long)(m0 >> 8) * g.N + col] = s;
+    }
+  }
 }
-LBWN_DEV void x3_epilogue(const lbwn_gemm_args& g, floatx16 (&acc)[2][2], int m0, int n0, int wm, int wn, int lane) {
-  x3_epilogue_rows<2>(g, acc, m0, n0, wm, wn, lane);
+LBWN_DEV void x3_epilogue(const lbwn_gemm_args& g, floatx16 (&acc)[2][2], int m0, int n0, int wm, int wn, int lane,
+                          int nwm, float* red) {
+  x3_epilogue_rows<2>(g, acc, m0, n0, wm, wn, lane, nwm, red);
 }
 
 // Block tile (64·WM) × 128, WM × 2 waves of 64 × 64 (2 × 2 accumulators of 32 × 32).
@@ -517,7 +538,7 @@ __global__ __launch_bounds__(128 * WM, (WM == 2 && STAGES == 1) ? X3_OCC : 1) vo
     }
   }
 
-  x3_epilogue(g, acc, m0, n0, wm, wn, lane);
+  x3_epilogue(g, acc, m0, n0, wm, wn, lane, WM, WM == 4 ? (float*)smem : nullptr);
 }
 
 // Pre-split planes of weights W (f32, row stride ldw): out[r][kc][plane][32] = split of
@@ -615,6 +636,7 @@ int gemm_launch_x3_t(const lbwn_gemm_args& g, const dim3& grid, int a_kcontig, i
 int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                    hipStream_t st) {
   LBWN_REQUIRE(a.a_codes == nullptr, "gemm (bf16 split): one-hot A not supported");
+  LBWN_REQUIRE(a.colpart == nullptr || split_k <= 1, "gemm (bf16 split): column partials need split_k = 1");
   LBWN_REQUIRE(a.b3 == nullptr || (a.K % X3_BK == 0 && (((uintptr_t)a.b3) & 15) == 0),
                "gemm (bf16 split): pre-split B needs K %% 32 == 0 and 16-B alignment");
   // 256-row tiles (8 waves, 2-stage pipeline) for the tall k-contiguous products with N <= 512
@@ -622,7 +644,7 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
   // the rest (the mn-contiguous weight gradients: 1.3-1.5x slower on 256-row tiles; dZ, N =
   // 1600).  LBWN_X3_WM=2|4 forces one.
   static const char* env = getenv("LBWN_X3_WM");
-  const int wm = env ? (env[0] == '4' ? 4 : 2) : (a_kcontig && a.N <= 512 && a.M >= 8192 ? 4 : 2);
+  const int wm = a.colpart ? 4 : env ? (env[0] == '4' ? 4 : 2) : (a_kcontig && a.N <= 512 && a.M >= 8192 ? 4 : 2);
   lbwn_gemm_args g;
   dim3 grid;
   int e = gemm_setup(a, a_kcontig, b_kcontig, split_k, slab_ws, X3_BK, 64 * wm, 128, g, grid);
@@ -676,6 +698,7 @@ int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int 
                      hipStream_t st) {
   if (lbwn_gemm_mode() == 1 && a.a_codes == nullptr && a.K >= 4 && a.M >= 4 && a.N >= 4)
     return gemm_launch_x3(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
+  LBWN_REQUIRE(a.colpart == nullptr, "gemm: column partials need the bf16-split form");
   // tall products (M = B·T positions): 256 × 128 block tiles, each wave 128 × 64
   static const char* env = getenv("LBWN_GEMM_TILE");
   const bool tall = (env && env[0] == '2') && a.M >= 8192 && split_k <= 1;   // measured slower: opt-in
@@ -687,6 +710,7 @@ int lbwn_gemm_launch_lean(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig,
                           hipStream_t st) {
   if (lbwn_gemm_mode() == 1 && a.a_codes == nullptr && a.K >= 4 && a.M >= 4 && a.N >= 4)
     return gemm_launch_x3(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
+  LBWN_REQUIRE(a.colpart == nullptr, "gemm: column partials need the bf16-split form");
   return gemm_launch_t<8, 128, 128>(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
 }
 

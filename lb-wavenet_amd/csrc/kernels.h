@@ -14,11 +14,16 @@ struct lbwn_gemm_args {
   int relu_a, relu_out, accumulate;
   const unsigned short* b3;  // nullable: B pre-split into bf16 planes [N][K/32][3][32] (lbwn_split_planes_launch)
   const int* a_codes;  // m-contiguous A only: A[k][m] = (a_codes[k] == m)  (one-hot, tmodel.py:64-65)
+  // nullable, bf16-split form without split-K only: column partial sums of the final C values
+  // (after bias/relu/mask), [ceil(M/256)][N] (one part per 256-row block tile), summed by
+  // lbwn_colsum_final_launch: the bias gradient without a second pass over C
+  float* colpart;
   int k_per_split;     // set by the launcher
   long split_stride;   // set by the launcher
 };
 int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                      hipStream_t st);
+inline int lbwn_colpart_parts(long M) { return (int)((M + 255) / 256); }
 // Pre-split planes of a weight for lbwn_gemm_args::b3: rows = N of the product it feeds,
 // W[r][k] (trans = 0) or W[k][r] (trans = 1), row stride ldw; up to 6 weights per launch.
 // Element count of one output:
@@ -143,6 +148,11 @@ int lbwn_colsum_multi_launch(int njobs, const float* const* X, const long* ldx, 
 int lbwn_colsum_launch(const float* X, long ldx, int M, int N, float* out, int accumulate, float* ws,
                        hipStream_t st);
 int lbwn_colsum_ws_floats(int M, int N);
+// the two passes apart: the first pass alone (*nparts = its partial row count; ws holds that ×
+// N floats), and the second over any partials (first-pass ones or a GEMM epilogue's colpart)
+int lbwn_colsum_partial_launch(const float* X, long ldx, int M, int N, float* ws, int* nparts, hipStream_t st);
+int lbwn_colsum_final_launch(int njobs, float* const* parts, const int* N, float* const* out, const int* accumulate,
+                             const int* nparts, hipStream_t st);
 int lbwn_sum_bias_launch(const float* b, int L, int N, float* out, hipStream_t st);
 int lbwn_fill_launch(float* p, float v, long n, hipStream_t st);
 

@@ -251,6 +251,7 @@ struct ColsumJobs {
   float* out[4];
   int accumulate[4];
   float* ws[4];
+  int nparts[4];   // partial rows per job (colsum_final_kernel)
 };
 __global__ __launch_bounds__(256) void colsum_partial_kernel(ColsumJobs jb, int M) {
   __shared__ floatx4 red[256];
@@ -278,9 +279,9 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(ColsumJobs jb, int 
 }
 // 256 threads (4 part lanes × 64 columns): a 1024-thread block needs 16 free wave slots on one
 // CU, which beside a resident layer chain and the aux-stream GEMMs it waited ~430 µs for
-__global__ __launch_bounds__(256) void colsum_final_kernel(ColsumJobs jb, int nparts) {
+__global__ __launch_bounds__(256) void colsum_final_kernel(ColsumJobs jb) {
   __shared__ float red[256];
-  const int j = blockIdx.y, N = jb.N[j];
+  const int j = blockIdx.y, N = jb.N[j], nparts = jb.nparts[j];
   const float* part = jb.ws[j];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), lane = threadIdx.x >> 6;  // 4 part lanes
   if (blockIdx.x * 64 >= N) return;   // block-uniform
@@ -452,11 +453,41 @@ int lbwn_colsum_multi_launch(int njobs, const float* const* X, const long* ldx, 
     LBWN_REQUIRE(N[j] % 4 == 0 && N[j] <= 1024 && ldx[j] % 4 == 0, "colsum: N %% 4 / N <= 1024 / ldx %% 4 required");
     jb.X[j] = X[j]; jb.ldx[j] = ldx[j]; jb.N[j] = N[j]; jb.out[j] = out[j]; jb.accumulate[j] = accumulate[j];
     jb.ws[j] = w;
+    jb.nparts[j] = np;
     w += (long)np * N[j];
     nmax = std::max(nmax, N[j]);
   }
   colsum_partial_kernel<<<dim3(np, njobs), 256, 0, st>>>(jb, M);
-  colsum_final_kernel<<<dim3((nmax + 63) / 64, njobs), 256, 0, st>>>(jb, np);
+  colsum_final_kernel<<<dim3((nmax + 63) / 64, njobs), 256, 0, st>>>(jb);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_colsum_partial_launch(const float* X, long ldx, int M, int N, float* ws, int* nparts, hipStream_t st) {
+  LBWN_REQUIRE(N % 4 == 0 && N <= 1024 && ldx % 4 == 0, "colsum: N %% 4 / N <= 1024 / ldx %% 4 required");
+  ColsumJobs jb;
+  memset(&jb, 0, sizeof(jb));
+  jb.X[0] = X; jb.ldx[0] = ldx; jb.N[0] = N; jb.ws[0] = ws;
+  const int np = (M + CS_ROWS - 1) / CS_ROWS;
+  colsum_partial_kernel<<<dim3(np, 1), 256, 0, st>>>(jb, M);
+  LBWN_CHECK_LAUNCH();
+  *nparts = np;
+  return 0;
+}
+
+int lbwn_colsum_final_launch(int njobs, float* const* parts, const int* N, float* const* out, const int* accumulate,
+                             const int* nparts, hipStream_t st) {
+  LBWN_REQUIRE(njobs >= 1 && njobs <= 4, "colsum_final: 1..4 jobs");
+  ColsumJobs jb;
+  memset(&jb, 0, sizeof(jb));
+  int nmax = 0;
+  for (int j = 0; j < njobs; ++j) {
+    LBWN_REQUIRE(nparts[j] >= 1, "colsum_final: nparts >= 1");
+    jb.N[j] = N[j]; jb.out[j] = out[j]; jb.accumulate[j] = accumulate[j]; jb.ws[j] = parts[j];
+    jb.nparts[j] = nparts[j];
+    nmax = std::max(nmax, N[j]);
+  }
+  colsum_final_kernel<<<dim3((nmax + 63) / 64, njobs), 256, 0, st>>>(jb);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
