@@ -602,8 +602,11 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   // Weight packs (once per step, reused by the backward) on aux2, forked here and joined before
   // the chain: they depend only on the weights, so they overlap embed / cond / D-sep below.
   const bool x3 = lbwn_gemm_mode() == 1;
+  // LBWN_PACK_SIDE=1: on aux2 (forked / joined by events: the event round trips cost more than
+  // the ~20 µs of packs they hide); default: in line on the main stream
+  static const char* pse = getenv("LBWN_PACK_SIDE");
   hipStream_t pst = st;
-  if (p->aux2) {
+  if (p->aux2 && pse && pse[0] == '1') {
     LBWN_HIP(hipEventRecord(p->ev_pfork, st));
     LBWN_HIP(hipStreamWaitEvent(p->aux2, p->ev_pfork, 0));
     pst = p->aux2;
@@ -617,13 +620,11 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     return e;
   // skip/head weights -> bf16 planes for the split GEMMs, forward and backward, and the split
   // per-layer images of the forward chain
+  // ... and the backward chain's split images (dx weights + f32 residual image), one launch
   if (x3 && p->chain &&
-      (e = lbwn_pack_layers_x3_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b,
-                                      at<unsigned short>(ws, p->oWPKX), L, Cr, Cd, pst)))
-    return e;
-  // ... and the backward chain's split images (dx weights + f32 residual image)
-  if (x3 && p->chain &&
-      (e = lbwn_pack_layers_bx3_launch(P->sig, P->gate, P->res, at<float>(ws, p->oWPKB), L, Cr, Cd, pst)))
+      (e = lbwn_pack_layers_fb_x3_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b,
+                                         at<unsigned short>(ws, p->oWPKX), at<float>(ws, p->oWPKB), L, Cr, Cd,
+                                         pst)))
     return e;
   if (x3) {
     const float* wsrc[6] = {P->skip, P->post1, P->post2, P->post2, P->post1, P->skip};

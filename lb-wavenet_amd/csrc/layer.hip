@@ -97,9 +97,8 @@ constexpr int XIMG_US = XB_OFF + 2 * 96;                       // bf16 elements 
 constexpr int XIMG_F = XIMG_US / 2;                            // = 8160 floats, multiple of 4
 static_assert(XIMG_F % 4 == 0 && XB_OFF % 8 == 0, "x3 image alignment");
 
-__global__ void pack_layers_x3_kernel(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
-                                      const float* res, const float* res_b, unsigned short* out, int Cr, int Cd) {
-  const int l = blockIdx.x;
+LBWN_DEV void pack_x3_body(int l, const float* sig, const float* gate, const float* sig_b, const float* gate_b,
+                          const float* res, const float* res_b, unsigned short* out, int Cr, int Cd) {
   const float* ws = sig + (long)l * 2 * Cr * Cd;
   const float* wg = gate + (long)l * 2 * Cr * Cd;
   const float* wr = res + (long)l * Cd * Cr;
@@ -1177,9 +1176,7 @@ constexpr int BIMG_F = (BD_US / 2 + 32 * XS + 255) / 256 * 256;   // 7680 floats
 constexpr int CBX_LDS = BIMG_F + 7 * LP * 32 + 8 * 96;            // IMG | Xp Xc ZT | DVs DVg G OC | part
 static_assert(CBX_LDS * 4 + 16 <= 160 * 1024, "chain bwd x3 LDS");
 
-__global__ void pack_layers_bx3_kernel(const float* sig, const float* gate, const float* res, float* out, int Cr,
-                                       int Cd) {
-  const int l = blockIdx.x;
+LBWN_DEV void pack_bx3_body(int l, const float* sig, const float* gate, const float* res, float* out, int Cr, int Cd) {
   const float* ws = sig + (long)l * 2 * Cr * Cd;
   const float* wg = gate + (long)l * 2 * Cr * Cd;
   const float* wr = res + (long)l * Cd * Cr;
@@ -1208,6 +1205,23 @@ __global__ void pack_layers_bx3_kernel(const float* sig, const float* gate, cons
     rs[e] = (c < Cd && o < Cr) ? wr[c * Cr + o] : 0.f;
   }
   for (int e = BD_US / 2 + 32 * XS + threadIdx.x; e < BIMG_F; e += blockDim.x) img[e] = 0.f;
+}
+
+__global__ void pack_layers_x3_kernel(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
+                                      const float* res, const float* res_b, unsigned short* out, int Cr, int Cd) {
+  pack_x3_body(blockIdx.x, sig, gate, sig_b, gate_b, res, res_b, out, Cr, Cd);
+}
+__global__ void pack_layers_bx3_kernel(const float* sig, const float* gate, const float* res, float* out, int Cr,
+                                       int Cd) {
+  pack_bx3_body(blockIdx.x, sig, gate, res, out, Cr, Cd);
+}
+// both chains' images in one launch (blocks [0, L): forward, [L, 2L): backward)
+__global__ void pack_layers_fb_x3_kernel(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
+                                         const float* res, const float* res_b, unsigned short* fout, float* bout,
+                                         int L, int Cr, int Cd) {
+  const int l = blockIdx.x;
+  if (l < L) pack_x3_body(l, sig, gate, sig_b, gate_b, res, res_b, fout, Cr, Cd);
+  else pack_bx3_body(l - L, sig, gate, res, bout, Cr, Cd);
 }
 
 // element (p, c) of a 32-float-row tile with the 4-float groups XOR-permuted by row pair
@@ -1936,6 +1950,15 @@ int lbwn_pack_layers_bx3_launch(const float* sig, const float* gate, const float
   return 0;
 }
 
+int lbwn_pack_layers_fb_x3_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
+                                  const float* res, const float* res_b, unsigned short* fout, float* bout, int L,
+                                  int Cr, int Cd, hipStream_t st) {
+  LBWN_REQUIRE(Cr <= 32 && Cd <= 32 && (((uintptr_t)fout) & 15) == 0 && (((uintptr_t)bout) & 15) == 0,
+               "pack_layers_fb_x3: bad arguments");
+  pack_layers_fb_x3_kernel<<<2 * L, 256, 0, st>>>(sig, gate, sig_b, gate_b, res, res_b, fout, bout, L, Cr, Cd);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
 int lbwn_pack_layers_x3_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                                const float* res, const float* res_b, unsigned short* out, int L, int Cr, int Cd,
                                hipStream_t st) {
