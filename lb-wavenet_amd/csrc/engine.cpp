@@ -20,7 +20,8 @@ struct lbwn_plan {
   int Ge, ncat1, Li, Lo, nup, hop, up[8];   // conditioning (Ge = 0: no GC, Lo = 0: no LC)
   long M;
   // workspace carving (byte offsets)
-  size_t oCPART = 0;
+  size_t oCPART = 0, nflag_bytes = 0;
+  bool bwd_flags_fresh = false;   // the step-start memset zeroed the backward flags, not yet used
   size_t oX, oZ, oS, oR2, oLOG, oDH, oDS, oDZ, oGA[2], oGC0[2], oSLAB, oSPLIT, oSPLIT2, oCOLS,
       oHEADP, oBSUM, oWPK, oWPKX, oFLAGS, oSTATUS, oOCG, oCTRACE;
   // bf16-split backward chain: σ(v_gate) rows from the forward chain [L][M][32], backward images
@@ -322,8 +323,10 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->oCOLS = carve(cur, sizeof(float) * 3 * (size_t)lbwn_colsum_ws_floats((int)M, std::max({p->Cs, p->Cp, p->Q, p->Cr})));
   // dH1 / dS column partials from the GEMM epilogues (bias gradients of POST1 / SKIP)
   p->oCPART = carve(cur, sizeof(float) * (size_t)lbwn_colpart_parts(M) * (p->Cp + p->Cs));
-  // [status (16 B) | hand-off flags]: status zeroed once per step, flags before each chain
-  p->oSTATUS = carve(cur, 16 + sizeof(unsigned) * (size_t)B * ((T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS));
+  // [status (16 B) | forward hand-off flags | backward hand-off flags], zeroed by ONE memset per
+  // step (each flag block padded to 16 B)
+  p->nflag_bytes = (sizeof(unsigned) * (size_t)B * ((T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS) + 15) / 16 * 16;
+  p->oSTATUS = carve(cur, 16 + 2 * p->nflag_bytes);
   p->oFLAGS = p->oSTATUS + 16;
   {
     const char* ct = getenv("LBWN_CHAIN_TRACE");
@@ -590,7 +593,8 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   P = &Ppad;
   // the sticky status word (chain spin timeouts OR their codes in) lives for one step:
   // zeroed here, read by the host after the step (lbwn_plan_tensor "status")
-  LBWN_HIP(hipMemsetAsync(at<char>(ws, p->oSTATUS), 0, 16, st));
+  LBWN_HIP(hipMemsetAsync(at<char>(ws, p->oSTATUS), 0, 16 + 2 * p->nflag_bytes, st));
+  p->bwd_flags_fresh = true;
   const int L = p->L, B = p->B, T = p->T, H = p->H, Cr = p->Cr, Cd = p->Cd;
   const long M = p->M, ldz = (long)L * Cd;
   float* X = at<float>(ws, p->oX);
@@ -659,6 +663,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     p->fwd_x3 = c.SG != nullptr;
     c.gc_tab = cd.gc_tab; c.gc_ld = cd.gc_ld; c.cond = cd.cond; c.ldcond = cd.ldcond;
     c.flags = at<unsigned>(ws, p->oFLAGS); c.status = at<unsigned>(ws, p->oSTATUS);
+    c.flags_zeroed = 1;   // zeroed with the status word at the step start
     if (p->ctrace_blk >= 0) { c.trace = at<long long>(ws, p->oCTRACE); c.trace_blk = p->ctrace_blk; }
     c.B = B; c.T = T; c.H = H; c.L = L; c.nbl = p->nbl; c.Cr = Cr; c.Cd = Cd; c.grid = p->chain_grid;
     Probe(p, st, "layer_fwd");
@@ -879,7 +884,9 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     c.gc_tab = cd.gc_tab; c.gc_ld = cd.gc_ld; c.cond = cd.cond; c.ldcond = cd.ldcond;
     c.gc_dtab = cd.gc_dtab; c.dv_out = cd.dv_out; c.lddv = cd.ldcond;
     c.dx0_a = at<float>(ws, p->oGA[0]); c.dx0_c = at<float>(ws, p->oGC0[0]);
-    c.flags = at<unsigned>(ws, p->oFLAGS); c.status = at<unsigned>(ws, p->oSTATUS);
+    c.flags = at<unsigned>(ws, p->oFLAGS + p->nflag_bytes); c.status = at<unsigned>(ws, p->oSTATUS);
+    c.flags_zeroed = p->bwd_flags_fresh ? 1 : 0;   // zeroed at the step start unless already used
+    p->bwd_flags_fresh = false;
     if (p->ctrace_blk >= 0) { c.trace = at<long long>(ws, p->oCTRACE); c.trace_blk = p->ctrace_blk; }
     c.B = B; c.T = T; c.H = p->H; c.L = L; c.nbl = p->nbl; c.Cr = Cr; c.Cd = Cd; c.grid = p->chain_grid;
     Probe(p, st, "layer_bwd");

@@ -103,7 +103,8 @@ struct lbwn_chain_args {
   const float* gc_tab; long gc_ld; const int* ids;   // GC table [ncat+1][L·2Cd] or null
   const float* cond; long ldcond;                     // LC term [M][L·2Cd] or null
   float* dv_out; long lddv; float* gc_dtab;           // backward: LC dv export, GC grad table
-  unsigned* flags;             // [B·ceil(T/128)] (zeroed by the launcher)
+  unsigned* flags;             // [B·ceil(T/128)] (zeroed by the launcher unless flags_zeroed)
+  int flags_zeroed;            // the caller zeroed flags on this stream (no memset here)
   unsigned* status;            // sticky error word (spin timeout)
   int B, T, H, L, nbl, Cr, Cd;
   int grid;                    // ≤ blocks resident at once (rounds of tiles)

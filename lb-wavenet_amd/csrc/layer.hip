@@ -2028,9 +2028,8 @@ int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   k.SG = c.SG; k.sgls = c.sgls;
   LBWN_REQUIRE(!c.wpack_x3 || (((uintptr_t)c.wpack_x3) & 15) == 0, "chain fwd: split images not 16-B aligned");
   const int tps = (c.T + LP - 1) / LP;
-  LBWN_REQUIRE((unsigned*)c.status + 4 == c.flags, "chain: status word must head the flag block");
   // hand-off flags only: the status word is sticky for the whole step
-  LBWN_HIP(hipMemsetAsync(c.flags, 0, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st));
+  if (!c.flags_zeroed) LBWN_HIP(hipMemsetAsync(c.flags, 0, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st));
   if (c.wpack_x3) chain_fwd_kernel<true><<<c.grid, 256, 0, st>>>(k);
   else chain_fwd_kernel<false><<<c.grid, 256, 0, st>>>(k);
   LBWN_CHECK_LAUNCH();
@@ -2054,9 +2053,8 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   if (x3) LBWN_REQUIRE((((uintptr_t)c.bimg) & 15) == 0 && (((uintptr_t)c.SG) & 15) == 0 && (c.ldz & 3) == 0,
                        "chain bwd x3: misaligned images / rows");
   const int tps = (c.T + LP - 1) / LP;
-  LBWN_REQUIRE((unsigned*)c.status + 4 == c.flags, "chain: status word must head the flag block");
   // hand-off flags only: the status word is sticky for the whole step
-  LBWN_HIP(hipMemsetAsync(c.flags, 0, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st));
+  if (!c.flags_zeroed) LBWN_HIP(hipMemsetAsync(c.flags, 0, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st));
   if (x3) chain_bwd_x3_kernel<<<c.grid, 256, 0, st>>>(k);
   else chain_bwd_kernel<<<c.grid, 256, 0, st>>>(k);
   LBWN_CHECK_LAUNCH();
