@@ -628,8 +628,9 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   if (x3 && p->chain &&
       (e = lbwn_pack_layers_fb_x3_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b,
                                          at<unsigned short>(ws, p->oWPKX), at<float>(ws, p->oWPKB), L, Cr, Cd,
-                                         pst)))
+                                         P->skip_b, p->Cs, bsum, pst)))
     return e;
+  const bool bsum_done = x3 && p->chain && P->skip_b;   // summed by the pack launch above
   if (x3) {
     const float* wsrc[6] = {P->skip, P->post1, P->post2, P->post2, P->post1, P->skip};
     const float* jw[6];
@@ -685,7 +686,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   // SAVE_l <- last d rows of [SAVE ++ x_l]  (tmodel.py:165)
   if ((e = lbwn_dsep_save_launch(X, p->x_layer_stride, save, L, p->nbl, B, T, H, Cr, st))) return e;
   // S = Σ_l (z_l·SKIP_l + b) as ONE GEMM over Zcat (tmodel.py:171-184, :316-320)
-  if (P->skip_b && (e = lbwn_sum_bias_launch(P->skip_b, L, p->Cs, bsum, st))) return e;
+  if (P->skip_b && !bsum_done && (e = lbwn_sum_bias_launch(P->skip_b, L, p->Cs, bsum, st))) return e;
   {
     lbwn_gemm_args g = gemm0();
     g.A = Z; g.lda = ldz; g.B = P->skip; g.ldb = p->Cs; g.C = S; g.ldc = p->Cs;

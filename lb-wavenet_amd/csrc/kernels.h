@@ -74,10 +74,11 @@ int lbwn_layer_bwd_launch(const lbwn_layer_args& a, hipStream_t st);
 int lbwn_layer_slab_stride();
 // split weight images for the forward chain's bf16-split products (bf16 elements per layer)
 int lbwn_layer_image_x3_elems();
-// lbwn_pack_layers_x3_launch + lbwn_pack_layers_bx3_launch in one launch
+// lbwn_pack_layers_x3_launch + lbwn_pack_layers_bx3_launch in one launch, plus (skip_b, bsum
+// non-null) bsum[n] = Σ_l skip_b[l·Cs + n] (lbwn_sum_bias_launch)
 int lbwn_pack_layers_fb_x3_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                                   const float* res, const float* res_b, unsigned short* fout, float* bout, int L,
-                                  int Cr, int Cd, hipStream_t st);
+                                  int Cr, int Cd, const float* skip_b, int Cs, float* bsum, hipStream_t st);
 int lbwn_pack_layers_x3_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                                const float* res, const float* res_b, unsigned short* out, int L, int Cr, int Cd,
                                hipStream_t st);

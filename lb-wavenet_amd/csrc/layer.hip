@@ -1215,13 +1215,25 @@ __global__ void pack_layers_bx3_kernel(const float* sig, const float* gate, cons
                                        int Cd) {
   pack_bx3_body(blockIdx.x, sig, gate, res, out, Cr, Cd);
 }
-// both chains' images in one launch (blocks [0, L): forward, [L, 2L): backward)
+// both chains' images in one launch (blocks [0, L): forward, [L, 2L): backward), and in the
+// blocks after them (if skip_b) the skip GEMM's bias Σ_l skip_b[l] (l in order)
 __global__ void pack_layers_fb_x3_kernel(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                                          const float* res, const float* res_b, unsigned short* fout, float* bout,
-                                         int L, int Cr, int Cd) {
+                                         int L, int Cr, int Cd, const float* skip_b, int Cs, float* bsum) {
   const int l = blockIdx.x;
-  if (l < L) pack_x3_body(l, sig, gate, sig_b, gate_b, res, res_b, fout, Cr, Cd);
-  else pack_bx3_body(l - L, sig, gate, res, bout, Cr, Cd);
+  if (l < L) {
+    pack_x3_body(l, sig, gate, sig_b, gate_b, res, res_b, fout, Cr, Cd);
+  } else if (l < 2 * L) {
+    pack_bx3_body(l - L, sig, gate, res, bout, Cr, Cd);
+  } else {
+    const int n = (l - 2 * L) * blockDim.x + threadIdx.x;
+    if (n < Cs) {
+      float s = 0.f;
+#pragma unroll 10
+      for (int k = 0; k < L; ++k) s += skip_b[(long)k * Cs + n];
+      bsum[n] = s;
+    }
+  }
 }
 
 // element (p, c) of a 32-float-row tile with the 4-float groups XOR-permuted by row pair
@@ -1952,10 +1964,12 @@ int lbwn_pack_layers_bx3_launch(const float* sig, const float* gate, const float
 
 int lbwn_pack_layers_fb_x3_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                                   const float* res, const float* res_b, unsigned short* fout, float* bout, int L,
-                                  int Cr, int Cd, hipStream_t st) {
+                                  int Cr, int Cd, const float* skip_b, int Cs, float* bsum, hipStream_t st) {
   LBWN_REQUIRE(Cr <= 32 && Cd <= 32 && (((uintptr_t)fout) & 15) == 0 && (((uintptr_t)bout) & 15) == 0,
                "pack_layers_fb_x3: bad arguments");
-  pack_layers_fb_x3_kernel<<<2 * L, 256, 0, st>>>(sig, gate, sig_b, gate_b, res, res_b, fout, bout, L, Cr, Cd);
+  const int nsum = (skip_b && bsum) ? (Cs + 255) / 256 : 0;
+  pack_layers_fb_x3_kernel<<<2 * L + nsum, 256, 0, st>>>(sig, gate, sig_b, gate_b, res, res_b, fout, bout, L, Cr, Cd,
+                                                         skip_b, Cs, bsum);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
