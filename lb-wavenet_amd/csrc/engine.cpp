@@ -910,12 +910,21 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     r.slab = SLABS; r.nparts = ntiles; r.stride = sstr; r.Cr = Cr; r.Cd = Cd;
     r.dsig = G->sig; r.dgate = G->gate; r.dres = G->res;
     r.dbsig = G->sig_b; r.dbgate = G->gate_b; r.dbres = G->res_b;
+    // LBWN_PG_ORDER: 1 (default) dPRE then the slab reduction on the side stream (the small
+    // scatter grid starts while dSKIP's blocks still leave room: step -0.5 %), 0 the reverse,
+    // 2 dPRE on the main stream ahead of dSKIP
+    static const char* pgo = getenv("LBWN_PG_ORDER");
+    const int pg_order = pgo ? pgo[0] - '0' : 1;
+    auto pre_grad = [&](hipStream_t s2) {
+      return lbwn_pre_grad_launch(wav_q, at<float>(ws, p->oGA[0]), at<float>(ws, p->oGC0[0]), 1, B, T, Cr, Q, G->pre,
+                                  G->pre_b, at<float>(ws, p->oSPLIT2), s2);
+    };
+    if (pg_order == 1 && (e = pre_grad(rst))) return e;
+    if (pg_order == 2 && (e = pre_grad(st))) return e;
     Probe(p, rst, "layer_reduce");
     if ((e = lbwn_layer_reduce_all_launch(r, L, (long)ntiles * sstr, rst))) return e;
     Probe::end(p, rst, "layer_reduce");
-    if ((e = lbwn_pre_grad_launch(wav_q, at<float>(ws, p->oGA[0]), at<float>(ws, p->oGC0[0]), 1, B, T, Cr, Q, G->pre,
-                                  G->pre_b, at<float>(ws, p->oSPLIT2), rst)))
-      return e;
+    if (pg_order != 1 && pg_order != 2 && (e = pre_grad(rst))) return e;
     if (p->aux2) LBWN_HIP(hipEventRecord(p->ev_join2, rst));
   } else {
       for (int l = L - 1; l >= 0; --l) {

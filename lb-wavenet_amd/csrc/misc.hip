@@ -3,6 +3,7 @@
 //   :86-102), the softmax-xent head with the invalid-window mask (tmodel.py:218-289),
 //   column sums for bias grads, TF1 Adam (train.py:178, :186) and the µ-law codec
 //   (ops.py:4-39).
+#include <cstdio>
 #include <math.h>
 
 #include <string.h>
@@ -77,23 +78,33 @@ __global__ void shift_add_kernel(float* out, const float* a, const float* c0, in
 // one-hot product (tmodel.py:64-66; tf.one_hot: a code outside [0, Q) has no row).  A scatter
 // into an LDS histogram, not a dense GEMM against the one-hot matrix (K = B·T, M = Q, N = Cr:
 // ~200 µs of tiles that are almost all zeros).  dx0 = g + shift(dprev) (layer 0's input
-// gradient, as shift_add forms it) is formed on the fly and never stored.  One wave per block
-// walks its chunk two positions per instruction (half-wave h takes h, h+2, ...) with
-// no-return LDS float atomics (ds_add_f32: no read-modify-write round trip); a single wave's
-// atomics are applied in program and lane order, so the sums are deterministic, and the
-// block partials are reduced in a fixed order.
-constexpr int PG_BLOCKS = 128;
+// gradient, as shift_add forms it) is formed on the fly and never stored.  Each wave of a block
+// owns an LDS histogram and a contiguous sub-chunk of the block's positions, walked two positions
+// per instruction (half-wave h takes h, h+2, ...) with no-return LDS float atomics (ds_add_f32:
+// no read-modify-write round trip); a single wave's atomics are applied in program and lane
+// order, the block's wave histograms are summed in wave order and the block partials are reduced
+// in a fixed order, so the sums are deterministic.  Default 256 one-wave blocks (32 KB of LDS
+// each, so they find room beside dSKIP's GEMM blocks; 128 x 1 and 256 x 2 measured slower);
+// LBWN_PG=<blocks>,<waves> selects up to PG_BLOCKS x PG_WAVES.
+constexpr int PG_BLOCKS = 256;
+constexpr int PG_WAVES = 2;
 constexpr int PG_BATCH = 32;
 
-__global__ __launch_bounds__(64) void pre_grad_part_kernel(const int* __restrict__ q, const float* __restrict__ g,
-                                                           const float* __restrict__ dprev, int gd, int B, int T,
-                                                           int Cr, int Q, float* part, float* bpart) {
-  extern __shared__ __attribute__((aligned(16))) float hist[];   // [Q][32]
-  const int lane = threadIdx.x, h = lane >> 5, c = lane & 31, cc = min(c, Cr - 1);
-  for (int i = lane; i < Q * 32 / 4; i += 64) ((float4*)hist)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+__global__ __launch_bounds__(64 * PG_WAVES) void pre_grad_part_kernel(const int* __restrict__ q,
+                                                                      const float* __restrict__ g,
+                                                                      const float* __restrict__ dprev, int gd, int B,
+                                                                      int T, int Cr, int Q, float* part, float* bpart) {
+  extern __shared__ __attribute__((aligned(16))) float hist_all[];   // [nw][Q][32]
+  __shared__ float bred[PG_WAVES][32];
+  const int nw = blockDim.x >> 6;   // PG_WAVES, or 1 when two histograms exceed 64 KB (Q > 256)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, h = lane >> 5, c = lane & 31, cc = min(c, Cr - 1);
+  float* hist = hist_all + (long)wv * Q * 32;
+  for (int i = threadIdx.x; i < nw * Q * 32 / 4; i += 64 * nw)
+    ((float4*)hist_all)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
   const long M = (long)B * T;
-  const long chunk = (M + gridDim.x - 1) / gridDim.x, m0 = blockIdx.x * chunk, m1 = min(M, m0 + chunk);
+  const long chunk = (M + gridDim.x - 1) / gridDim.x, b0 = blockIdx.x * chunk, b1 = min(M, b0 + chunk);
+  const long sub = (chunk + nw - 1) / nw, m0 = b0 + wv * sub, m1 = min(b1, m0 + sub);
   float bsum = 0.f;
   for (long mb = m0 + h; mb < m1; mb += 2 * PG_BATCH) {
     int cd[PG_BATCH];
@@ -116,14 +127,21 @@ __global__ __launch_bounds__(64) void pre_grad_part_kernel(const int* __restrict
         __hip_atomic_fetch_add(hist + cd[i] * 32 + c, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
+  const float bo = __shfl_xor(bsum, 32);
+  if (lane < 32) bred[wv][lane] = bsum + bo;
   __syncthreads();
   float* P = part + (long)blockIdx.x * Q * Cr;
-  for (int e = lane; e < Q * Cr; e += 64) {
+  for (int e = threadIdx.x; e < Q * Cr; e += 64 * nw) {
     const int qq = e / Cr, c2 = e % Cr;
-    P[e] = hist[qq * 32 + c2];
+    float s = hist_all[qq * 32 + c2];
+    for (int k = 1; k < nw; ++k) s += hist_all[(long)k * Q * 32 + qq * 32 + c2];
+    P[e] = s;
   }
-  const float bo = __shfl_xor(bsum, 32);
-  if (lane < Cr) bpart[(long)blockIdx.x * Cr + lane] = bsum + bo;
+  if (threadIdx.x < Cr) {
+    float s = bred[0][threadIdx.x];
+    for (int k = 1; k < nw; ++k) s += bred[k][threadIdx.x];
+    bpart[(long)blockIdx.x * Cr + threadIdx.x] = s;
+  }
 }
 
 __global__ __launch_bounds__(256) void pre_grad_reduce_kernel(const float* part, const float* bpart, int nparts,
@@ -406,12 +424,24 @@ int lbwn_pre_grad_ws_floats(int Q, int Cr) { return PG_BLOCKS * (Q * Cr + Cr); }
 int lbwn_pre_grad_launch(const int* q, const float* g, const float* dprev, int gd, int B, int T, int Cr, int Q,
                          float* dpre, float* dpre_b, float* ws, hipStream_t st) {
   LBWN_REQUIRE(Cr >= 1 && Cr <= 32 && Q >= 1 && Q * 32 * 4 <= 65536, "pre_grad: Cr <= 32 and Q <= 512 required");
+  // LBWN_PG=<blocks>,<waves> overrides the shape (blocks <= PG_BLOCKS, waves <= PG_WAVES)
+  static int cfg_blocks = -1, cfg_waves = -1;
+  if (cfg_blocks < 0) {
+    cfg_blocks = PG_BLOCKS; cfg_waves = 1;
+    if (const char* env = getenv("LBWN_PG")) {
+      int b = 0, w = 0;
+      if (sscanf(env, "%d,%d", &b, &w) == 2 && b >= 1 && b <= PG_BLOCKS && w >= 1 && w <= PG_WAVES) {
+        cfg_blocks = b; cfg_waves = w;
+      }
+    }
+  }
+  const int nb = cfg_blocks, nw = cfg_waves * Q * 32 * 4 <= 65536 ? cfg_waves : 1;
   float* part = ws;
   float* bpart = ws + (long)PG_BLOCKS * Q * Cr;
-  pre_grad_part_kernel<<<PG_BLOCKS, 64, Q * 32 * 4, st>>>(q, g, dprev, gd, B, T, Cr, Q, part, bpart);
+  pre_grad_part_kernel<<<nb, 64 * nw, nw * Q * 32 * 4, st>>>(q, g, dprev, gd, B, T, Cr, Q, part, bpart);
   LBWN_CHECK_LAUNCH();
   const int n = Q * Cr + Cr;
-  pre_grad_reduce_kernel<<<(n + 255) / 256, 256, 0, st>>>(part, bpart, PG_BLOCKS, Q, Cr, dpre, dpre_b);
+  pre_grad_reduce_kernel<<<(n + 255) / 256, 256, 0, st>>>(part, bpart, nb, Q, Cr, dpre, dpre_b);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
