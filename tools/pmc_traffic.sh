@@ -9,6 +9,6 @@ OUT=gpurun_out/pmc_traffic
 mkdir -p $OUT
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 240 rocprofv3 --pmc $C --output-format csv -d $OUT/$C -o run -- \
-      python bench.py --steps 4 --warmup 8 --no-gen --no-cpu-baseline "$@" > $OUT/$C.log 2>&1 || { echo "pass $C failed"; tail -5 $OUT/$C.log; exit 1; }
+      python bench.py --steps 4 --warmup 8 --no-gen --no-cpu-baseline --no-extras "$@" > $OUT/$C.log 2>&1 || { echo "pass $C failed"; tail -5 $OUT/$C.log; exit 1; }
 done
 python tools/pmc_traffic.py $OUT/FETCH_SIZE $OUT/WRITE_SIZE $OUT/pmc_traffic.json
