@@ -287,6 +287,10 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->split_post2 = pick_split(p->Cp, p->Q, M);
   p->split_post1 = pick_split(p->Cs, p->Cp, M);
   p->split_skip = pick_split(L * p->Cd, p->Cs, M);
+  if (const char* ss = getenv("LBWN_SPLIT_SKIP")) {   // dSKIP split-K override (A/B)
+    const int v = atoi(ss);
+    if (v >= 1 && v <= 32) p->split_skip = v;
+  }
   p->split_floats = std::max({(long)p->split_post2 * p->Cp * p->Q, (long)p->split_post1 * p->Cs * p->Cp,
                               (long)p->split_skip * ldz * p->Cs});
   if (p->Lo > 0) {
