@@ -639,12 +639,14 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
   LBWN_REQUIRE(a.colpart == nullptr || split_k <= 1, "gemm (bf16 split): column partials need split_k = 1");
   LBWN_REQUIRE(a.b3 == nullptr || (a.K % X3_BK == 0 && (((uintptr_t)a.b3) & 15) == 0),
                "gemm (bf16 split): pre-split B needs K %% 32 == 0 and 16-B alignment");
-  // 256-row tiles (8 waves, 2-stage pipeline) for the tall k-contiguous products with N <= 512
-  // (skip fwd, post1/post2 fwd, dH1, dS: 3-8 % faster); 128-row tiles at 2 blocks per CU for
-  // the rest (the mn-contiguous weight gradients: 1.3-1.5x slower on 256-row tiles; dZ, N =
-  // 1600).  LBWN_X3_WM=2|4 forces one.
+  // 256-row tiles (8 waves, 2-stage pipeline) for the tall k-contiguous products with N <= 2048
+  // (skip fwd, post1/post2 fwd, dH1, dS: 3-8 % faster; dZ, N = 1600: step -0.5 % in a same-box
+  // A/B since the epilogue and split changes); 128-row tiles at 2 blocks per CU for the rest
+  // (the mn-contiguous weight gradients: 1.3-1.5x slower on 256-row tiles).  LBWN_X3_WM=2|4
+  // forces one; LBWN_X3_WM_NMAX moves the N limit (512 = the round-2 v4 choice).
   static const char* env = getenv("LBWN_X3_WM");
-  const int wm = a.colpart ? 4 : env ? (env[0] == '4' ? 4 : 2) : (a_kcontig && a.N <= 512 && a.M >= 8192 ? 4 : 2);
+  static const int nmax = getenv("LBWN_X3_WM_NMAX") ? atoi(getenv("LBWN_X3_WM_NMAX")) : 2048;
+  const int wm = a.colpart ? 4 : env ? (env[0] == '4' ? 4 : 2) : (a_kcontig && a.N <= nmax && a.M >= 8192 ? 4 : 2);
   lbwn_gemm_args g;
   dim3 grid;
   int e = gemm_setup(a, a_kcontig, b_kcontig, split_k, slab_ws, X3_BK, 64 * wm, 128, g, grid);
