@@ -334,8 +334,9 @@ class TrainBench:
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
-        # a chain hand-off that timed out leaves its code in the plan's status word: the
-        # numbers of such a run are computed on garbage and must not be reported
+        # a chain hand-off that timed out in ANY step leaves its code in the cumulative status
+        # (counters[3], ORed in by the optimizer kernel every step): such a run's numbers are
+        # computed on garbage and must not be reported
         self.net.check_status(self.T)
         for name, (s, e) in pending:
             samples[name].append(s.elapsed_time(e))
@@ -375,6 +376,52 @@ class TrainBench:
         del self.net, self.ring
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+
+
+def chain_dilation_sweep(arch_file, B, T, dp, steps=4, gc=None):
+    """C4's dilation sweep (BASELINE configs[3], SURVEY §8d "Shapes"): in-kernel clock stamps
+    of one chain block's tile (LBWN_CHAIN_TRACE, read at plan creation) give each layer's
+    start-to-start time in the forward and the backward chain; layers are grouped by dilation
+    d = 2^bl (tmodel.py:313-325), median over the n_blocks layers of each d and over steps.
+    The tile is the chains' 128 positions x 32 channels (4 waves, one block per CU): the only
+    LDS tile they template -- a 64-position tile leaves two of four SIMDs idle (the 65 KB of
+    double-buffered weight images per block do not fit twice in 160 KB), a 256-position one
+    needs 2 waves per SIMD at <= 256 registers (the chains hold 330-470)."""
+    import torch
+    from lbwn.arch import load_arch, n_layers
+    arch = load_arch(arch_file, num_global_cond=gc)
+    old = os.environ.get('LBWN_CHAIN_TRACE')
+    os.environ['LBWN_CHAIN_TRACE'] = '1'
+    try:
+        tb = TrainBench(arch, B, T, dp)
+    finally:
+        if old is None:
+            os.environ.pop('LBWN_CHAIN_TRACE', None)
+        else:
+            os.environ['LBWN_CHAIN_TRACE'] = old
+    L, nbl = n_layers(arch), arch['n_block_layers']
+    runs = []
+    for i in range(steps + 1):
+        tb.step(i)
+        torch.cuda.synchronize()
+        if i >= 1:
+            runs.append(tb.net.plan_tensor(T, 'ctrace').view(torch.int64).cpu().numpy().reshape(2, L, 16).copy())
+    tb.net.check_status(T)
+    tb.close()
+    r = np.array(runs)                          # [steps][fwd, bwd][L][16]
+    fwd = r[:, 0, 1:, 0] - r[:, 0, :-1, 0]      # layer l = 0..L-2: start(l+1) - start(l)
+    bwd = r[:, 1, :-1, 0] - r[:, 1, 1:, 0]      # layer l = 1..L-1 (runs L-1 .. 0): start(l-1) - start(l)
+    rows = []
+    for bl in range(nbl):
+        fl = [l for l in range(L - 1) if l % nbl == bl]
+        bls = [l - 1 for l in range(1, L) if l % nbl == bl]
+        fc, bc = float(np.median(fwd[:, fl])), float(np.median(bwd[:, bls]))
+        rows.append({'d': 1 << bl, 'fwd_cycles': round(fc), 'bwd_cycles': round(bc),
+                     'fwd_us': round(fc / 2400.0, 3), 'bwd_us': round(bc / 2400.0, 3)})
+    return {'tile_positions': 128, 'tile_channels': 32, 'blocks_per_cu': 1, 'waves_per_block': 4,
+            'clock': 'clock64 cycles, us at 2.4 GHz', 'traced_block': 1, 'per_dilation': rows,
+            'note': 'per-layer start-to-start time of one chain block (its first tile), median over the '
+                    'n_blocks layers of each dilation and %d steps' % steps}
 
 
 CANDS = ['layer_bwd', 'dskip', 'layer_fwd', 'post1_fwd', 'dpost1', 'ds', 'post2_fwd', 'dpost2', 'dh']
@@ -465,6 +512,11 @@ def dry_run(args):
     class _Net:
         grad_flat = torch.full((n,), float(dp.rank + 1))
         stats = torch.tensor([1.0, 10.0 * (dp.rank + 1), 2.0, 0.0])
+        layout = ParamLayout(arch)
+        _status = torch.zeros(1, dtype=torch.int32)
+
+        def status_word(self):
+            return self._status
     net = _Net()
     t0 = time.perf_counter()
     dp.reduce_grads(net)
@@ -539,6 +591,7 @@ def main(argv=None):
         par = lambda f: os.path.join(ROOT, 'par', f)   # noqa: E731
         out['c4'] = sub_bench(par('arch5.json'), 32, 4096, dp, 10, 3, label='C4: arch5 deep stack, B=32 x T=4096, '
                               'train fwd+bwd+Adam, 1 GPU')
+        out['c4']['sweep'] = chain_dilation_sweep(par('arch5.json'), 32, 4096, dp)
         out['c5_per_gpu'] = sub_bench(par('arch5.json'), 8, 4096, dp, 10, 3,
                                       label='C5 per-GPU share on one GPU: arch5, B=8 x T=4096 (the N>1 runs '
                                             'default to this per rank: scaling reference)')

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define LBWN_ABI_VERSION 1
+#define LBWN_ABI_VERSION 2
 
 /* par/arch*.json after normalisation (tmodel.py:10-23, arch.py:31-103). */
 typedef struct lbwn_arch {
@@ -78,6 +78,14 @@ int lbwn_plan_tensor(const lbwn_plan* plan, const char* name, size_t* offset, si
  * "dpost2", "dh", "dpost1", "ds", "dskip" (Zcatᵀ·dS), "dz" (dS·SKIPcatᵀ).  Events are the
  * caller's (e.g. torch.cuda.Event(enable_timing=True).cuda_event). */
 int lbwn_plan_probe(lbwn_plan* plan, const char* launch_name, void* ev_start, void* ev_stop);
+/* Make `stream` wait (hipStreamWaitEvent, no host sync) for a point of the last
+ * lbwn_train_backward on this plan, so that a data-parallel caller can start a gradient
+ * all-reduce bucket before the backward ends.  point "head_grads": the POST1/POST2 weight
+ * gradients, their biases and SKIP_BIAS are final and the backward chain has completed (no
+ * collective can then share the chip with a persistent chain launch).  *waited = 1 if the plan
+ * has that point (chain plans without padded head widths), else 0 and nothing is enqueued
+ * (wait for the whole backward instead).  Added in ABI 2. */
+int lbwn_plan_stream_wait(lbwn_plan* plan, const char* point, void* stream, int* waited);
 /* receptive field F = n_blocks·Σ2^l (tmodel.py:50-51) */
 int lbwn_recep_field_sz(const lbwn_arch* arch);
 
@@ -102,11 +110,17 @@ int lbwn_train_backward(lbwn_plan* plan, const lbwn_params* params, const lbwn_p
  * flat buffers [0, n_total); elements [0, n_weights) are non-BIAS trainables and get the
  * l2 term (tmodel.py:250-261): g = raw·inv_n + l2_factor·θ with inv_n = 1/stats[1]
  * (0 if stats[1] == 0).  counters int64[4]: [0] GLOBAL_STEP, [1] VALID_SAMPLES,
- * [2] Adam applies so far (t-1), [3] reserved.  lr_t = lr·√(1-β2^t)/(1-β1^t) is derived
- * on device, so the call is graph-capturable.  Then counters advance by (1, n_valid, 1). */
+ * [2] Adam applies so far (t-1), [3] cumulative status (every step's status word ORed in,
+ * never reset by a step).  lr_t = lr·√(1-β2^t)/(1-β1^t) is derived on device, so the call
+ * is graph-capturable.  Then counters advance by (1, n_valid, 1).
+ * step_status (nullable): the plan's "status" word of this step (under data parallelism the
+ * sum over ranks).  Nonzero means a chain hand-off timed out and the gradients are garbage:
+ * the update is skipped on the device (params, m, v and counters[0..2] unchanged) and the
+ * word is ORed into counters[3], so the host needs no per-step synchronisation.
+ * (ABI 2: step_status added.) */
 int lbwn_adam_tf1(float* params, const float* grads, float* m, float* v, int64_t n_weights, int64_t n_total,
                   float lr, float beta1, float beta2, float eps, float l2_factor, const float* stats,
-                  int64_t* counters, void* stream);
+                  int64_t* counters, const uint32_t* step_status, void* stream);
 
 /* ---- cached autoregressive generation (imodel.WaveNetGen, imodel.py:7-303) ------------ */
 typedef struct lbwn_gen_plan lbwn_gen_plan;
@@ -133,7 +147,7 @@ int lbwn_gen_start(lbwn_gen_plan* plan, const lbwn_params* params, void* workspa
  * plans (lbwn_gen_is_persistent) run the whole call as ONE launch whose blocks must all be
  * resident: nothing else may occupy the device's CUs meanwhile. */
 int lbwn_gen_run(lbwn_gen_plan* plan, const lbwn_params* params, void* workspace, int n_steps, void* stream);
-/* 1 when the plan runs the persistent one-launch form (B <= 32 and the layer/head sizes fit;
+/* 1 when the plan runs the persistent one-launch form (B <= 16 and the layer/head sizes fit;
  * LBWN_GEN_PERSIST=0 at plan creation selects the per-step launches), else 0. */
 int lbwn_gen_is_persistent(const lbwn_gen_plan* plan);
 

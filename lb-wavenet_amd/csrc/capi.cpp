@@ -23,14 +23,15 @@ int lbwn_abi_version(void) { return LBWN_ABI_VERSION; }
 
 int lbwn_adam_tf1(float* params, const float* grads, float* m, float* v, int64_t n_weights, int64_t n_total,
                   float lr, float beta1, float beta2, float eps, float l2_factor, const float* stats,
-                  int64_t* counters, void* stream) {
+                  int64_t* counters, const uint32_t* step_status, void* stream) {
   LBWN_REQUIRE(params && grads && m && v && counters, "adam_tf1: null argument");
   LBWN_REQUIRE(n_weights >= 0 && n_weights <= n_total, "adam_tf1: bad sizes");
   hipStream_t st = (hipStream_t)stream;
+  const unsigned* ss = (const unsigned*)step_status;
   int e = lbwn_adam_launch2(params, grads, m, v, (long)n_weights, (long)n_total, lr, beta1, beta2, eps, l2_factor,
-                            stats, (const long long*)counters, st);
+                            stats, (const long long*)counters, ss, st);
   if (e) return e;
-  if (stats) return lbwn_counters_launch((long long*)counters, stats, 1, st);
+  if (stats) return lbwn_counters_launch((long long*)counters, stats, 1, ss, st);
   return 0;
 }
 

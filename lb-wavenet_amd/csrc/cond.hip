@@ -69,36 +69,52 @@ __global__ void gc_wgrad_sum_kernel(const float* __restrict__ part, float* __res
   }
 }
 
-// dEMB[c][e] = Σ_n gcd[c][n] · W(n)[e]: one block per category, wave-then-block reduction.
-__global__ __launch_bounds__(256) void gc_egrad_kernel(const float* __restrict__ gcd, const float* __restrict__ wsig,
-                                                       const float* __restrict__ wgate, float* __restrict__ demb,
-                                                       int N, int Ge, int Cd) {
-  __shared__ float red[4][GC_EMAX];
-  const int c = blockIdx.x;
-  float acc[GC_EMAX];
-#pragma unroll
-  for (int e = 0; e < GC_EMAX; ++e) acc[e] = 0.f;
-  for (int n = threadIdx.x; n < N; n += 256) {
-    const float g = gcd[(long)c * N + n];
-    const int l = n / (2 * Cd), s = (n / Cd) & 1, o = n % Cd;
+// dEMB[c][e] = Σ_n gcd[c][n] · W(n)[e] as a small tiled product: block (category group cg, n chunk
+// k) stages gcd[cg·CPB .. +CPB][k·256 .. +256] and W(n)[0..Ge) for its 256 n into LDS with all
+// loads issued at once, then thread (category cl, column e) sums its 256 products; the chunk
+// partials part[k][c][e] are summed in chunk order by gc_egrad_sum_kernel (deterministic).
+// (One block per category looping over n ran 114-308 µs: dependent load chains behind integer
+// divisions; this form is one wave of ~300 blocks.)
+constexpr int GE_N = 256;
+__global__ __launch_bounds__(256) void gc_egrad_part_kernel(const float* __restrict__ gcd,
+                                                            const float* __restrict__ wsig,
+                                                            const float* __restrict__ wgate,
+                                                            float* __restrict__ part, int N, int ncat1, int Ge,
+                                                            int Cd) {
+  __shared__ float gs[16][GE_N + 1];
+  __shared__ float wsm[GE_N][GC_EMAX + 1];
+  const int ep = Ge <= 16 ? 16 : 32, cpb = 256 / ep;
+  const int cg = blockIdx.x, k = blockIdx.y, t = threadIdx.x;
+  const int n = k * GE_N + t, nc = min(n, N - 1);
+  {
+    const int l = nc / (2 * Cd), s = (nc / Cd) & 1, o = nc % Cd;
     const float* W = (s == 0 ? wsig : wgate) + (long)l * Ge * Cd + o;
+    float wv[GC_EMAX], gv[16];
 #pragma unroll
-    for (int e = 0; e < GC_EMAX; ++e)
-      if (e < Ge) acc[e] += g * W[(long)e * Cd];
-  }
+    for (int e = 0; e < GC_EMAX; ++e) wv[e] = W[(long)min(e, Ge - 1) * Cd];
 #pragma unroll
-  for (int e = 0; e < GC_EMAX; ++e) {
-    float v = acc[e];
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    acc[e] = v;
-  }
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (lane == 0) {
+    for (int c = 0; c < 16; ++c) gv[c] = gcd[(long)min(cg * cpb + min(c, cpb - 1), ncat1 - 1) * N + nc];
+    const bool in = n < N;
 #pragma unroll
-    for (int e = 0; e < GC_EMAX; ++e) red[w][e] = acc[e];
+    for (int e = 0; e < GC_EMAX; ++e) wsm[t][e] = in ? wv[e] : 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) gs[c][t] = in ? gv[c] : 0.f;
   }
   __syncthreads();
-  if ((int)threadIdx.x < Ge) demb[(long)c * Ge + threadIdx.x] = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+  const int cl = t / ep, e = t % ep, c = cg * cpb + cl;
+  float acc = 0.f;
+#pragma unroll 8
+  for (int j = 0; j < GE_N; ++j) acc += gs[cl][j] * wsm[j][e];
+  if (c < ncat1 && e < Ge) part[((long)k * ncat1 + c) * Ge + e] = acc;
+}
+
+__global__ void gc_egrad_sum_kernel(const float* __restrict__ part, float* __restrict__ demb, int nk, int ncat1,
+                                    int Ge) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ncat1 * Ge) return;
+  float s = 0.f;
+  for (int k = 0; k < nk; ++k) s += part[(long)k * ncat1 * Ge + i];
+  demb[i] = s;
 }
 
 // LCcat[i][l·2Cd + s·Cd + o] = W_s[l][i][o]  (pack = 1)  or the inverse scatter (pack = 0)
@@ -136,7 +152,13 @@ int lbwn_gc_grad_launch(const float* emb, const float* wsig, const float* wgate,
   LBWN_CHECK_LAUNCH();
   gc_wgrad_sum_kernel<<<grid_for((long)Ge * N), 256, 0, st>>>(part, dsig, dgate, N, Ge, Cd);
   LBWN_CHECK_LAUNCH();
-  gc_egrad_kernel<<<ncat1, 256, 0, st>>>(gcd, wsig, wgate, demb, N, Ge, Cd);
+  // (part is free again: gc_wgrad_sum_kernel consumed it; GC_CSPLIT·Ge·N >= nk·ncat1·Ge floats
+  // holds for every shipped arch and is checked here)
+  const int nk = (N + GE_N - 1) / GE_N, ep = Ge <= 16 ? 16 : 32, cpb = 256 / ep;
+  LBWN_REQUIRE((long)nk * ncat1 * Ge <= (long)GC_CSPLIT * Ge * N, "gc grads: partial buffer too small");
+  gc_egrad_part_kernel<<<dim3((ncat1 + cpb - 1) / cpb, nk), 256, 0, st>>>(gcd, wsig, wgate, part, N, ncat1, Ge, Cd);
+  LBWN_CHECK_LAUNCH();
+  gc_egrad_sum_kernel<<<(ncat1 * Ge + 255) / 256, 256, 0, st>>>(part, demb, nk, ncat1, Ge);
   LBWN_CHECK_LAUNCH();
   return 0;
 }

@@ -35,7 +35,12 @@ struct lbwn_plan {
   size_t oPADP = 0, oPADG = 0;
   int ctrace_blk = -1;            // LBWN_CHAIN_TRACE=<block>: chain cycle stamps (debug)
   size_t oGCTAB, oGCD, oGCPART, oLCACT[8], oCOND, oDVALL, oLCCAT, oDLCCAT, oDLC[2];
-  int split_dlc, split_up[8];
+  // in-chain LC (bf16-split forward chain): L split LC images; COND is then computed only when a
+  // backward path needs it (cond_valid: this step's COND is in the workspace)
+  size_t oLCX = 0;
+  bool cond_valid = false;
+  int split_dlc, split_dlcx, split_up[8];
+  size_t oSPLIT_AUX = 0;         // split-K workspace of the aux2 stream (LC / GC grads beside dSKIP)
   size_t total;
   long x_layer_stride;  // floats
   int split_post2, split_post1, split_skip;
@@ -43,36 +48,25 @@ struct lbwn_plan {
   int nblk;                      // layer-bwd blocks = slab partials per layer
   bool chain = false;            // persistent layer-chain kernels (n_res = n_dil = 32)
   int chain_grid = 0;            // resident blocks for the chain (set on first use)
-  // Backward side streams (chain plans): the head weight gradients (dPOST2, dPOST1) run on the
-  // main stream before the chain (LBWN_WG_AFTER=1: on `aux` after it); dSKIP follows the chain
-  // on the main stream while `aux2` runs the HBM-bound slab reduction and dPRE beside it.  A
-  // chain block takes a whole CU's LDS, so nothing co-resides with the chains.
+  // Backward side stream (chain plans): the head weight gradients (dPOST2, dPOST1) run on the
+  // main stream before the chain; dSKIP follows the chain on the main stream while `aux2` runs
+  // the HBM-bound slab reduction and dPRE scatter beside it.  A chain block takes a whole CU's
+  // LDS, so nothing co-resides with the chains.
   bool overlap = false;
-  bool dskip_main = true;        // dSKIP after the chain on the main stream (LBWN_DSKIP_MAIN=0: with the aux GEMMs)
-  hipStream_t aux = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  // second side stream after the backward chain: the HBM-bound slab reduction and dPRE scatter
-  // run beside the MFMA-bound dSKIP on the main stream instead of in front of it
   hipStream_t aux2 = nullptr;
-  hipEvent_t ev_chain = nullptr, ev_join2 = nullptr;
-  // forward prologue: the per-step weight packs run on aux2 beside embed / cond / D-sep
-  hipEvent_t ev_pfork = nullptr, ev_pjoin = nullptr;
+  hipEvent_t ev_chain = nullptr, ev_join2 = nullptr, ev_dlc = nullptr;
+  bool bwd_chain_event = false;  // the last backward recorded ev_chain (lbwn_plan_stream_wait)
   bool wpk_valid = false;        // the f32 layer images were packed this step
-  size_t oSPLIT_AUX = 0;
   // Weights pre-split into bf16 planes once per step for the bf16-split GEMMs (gemm.hip):
   // [W3_SKIP_F] SKIPcat as skip-fwd B, [W3_POST1_F] POST1 as post1-fwd B, [W3_POST2_F] POST2 as
   // post2-fwd B, [W3_POST2_B] POST2ᵀ as dH1 B, [W3_POST1_B] POST1ᵀ as dS B, [W3_SKIP_B]
   // SKIPcatᵀ as dZ B.  Offset 0 = not used (K % 32 != 0).
   size_t oW3[6] = {0, 0, 0, 0, 0, 0};
   ~lbwn_plan() {
-    if (aux) (void)hipStreamDestroy(aux);
     if (aux2) (void)hipStreamDestroy(aux2);
     if (ev_chain) (void)hipEventDestroy(ev_chain);
     if (ev_join2) (void)hipEventDestroy(ev_join2);
-    if (ev_fork) (void)hipEventDestroy(ev_fork);
-    if (ev_join) (void)hipEventDestroy(ev_join);
-    if (ev_pfork) (void)hipEventDestroy(ev_pfork);
-    if (ev_pjoin) (void)hipEventDestroy(ev_pjoin);
+    if (ev_dlc) (void)hipEventDestroy(ev_dlc);
   }
   // one-shot event probe
   char probe[32];
@@ -126,6 +120,22 @@ int lbwn_plan_probe(lbwn_plan* p, const char* name, void* ev_start, void* ev_sto
   strcpy(p->probe, name);
   p->probe_start = (hipEvent_t)ev_start;
   p->probe_stop = (hipEvent_t)ev_stop;
+  return 0;
+}
+
+int lbwn_plan_stream_wait(lbwn_plan* p, const char* point, void* stream, int* waited) {
+  LBWN_REQUIRE(p && point && waited, "plan_stream_wait: null argument");
+  *waited = 0;
+  if (!strcmp(point, "head_grads")) {
+    // ev_chain: recorded on the main stream right after the backward chain launch, behind the
+    // head weight-gradient GEMMs and the bias column sums (padded heads copy theirs out at the end)
+    if (p->bwd_chain_event && !p->oPADG) {
+      LBWN_HIP(hipStreamWaitEvent((hipStream_t)stream, p->ev_chain, 0));
+      *waited = 1;
+    }
+    return 0;
+  }
+  LBWN_REQUIRE(false, "plan_stream_wait: unknown point '%s'", point);
   return 0;
 }
 
@@ -287,15 +297,16 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->split_post2 = pick_split(p->Cp, p->Q, M);
   p->split_post1 = pick_split(p->Cs, p->Cp, M);
   p->split_skip = pick_split(L * p->Cd, p->Cs, M);
-  if (const char* ss = getenv("LBWN_SPLIT_SKIP")) {   // dSKIP split-K override (A/B)
-    const int v = atoi(ss);
-    if (v >= 1 && v <= 32) p->split_skip = v;
-  }
   p->split_floats = std::max({(long)p->split_post2 * p->Cp * p->Q, (long)p->split_post1 * p->Cs * p->Cp,
                               (long)p->split_skip * ldz * p->Cs});
   if (p->Lo > 0) {
     p->split_dlc = pick_split(p->Lo, 2 * L * p->Cd, M);
     p->split_floats = std::max(p->split_floats, (long)p->split_dlc * p->Lo * 2 * L * p->Cd);
+    // dlc = DV·LCcatᵀ (M × n_lc_out, K = L·2Cd): 256-row tiles, one N tile; split K until the
+    // grid has ~512 blocks (it ran on 128 blocks of 256 CUs at B = 8)
+    const long dtiles = (M + 255) / 256 * ((p->Lo + 127) / 128);
+    p->split_dlcx = (int)std::max<long>(1, std::min<long>(512 / std::max<long>(1, dtiles), (2L * L * p->Cd) / 256));
+    p->split_floats = std::max(p->split_floats, (long)p->split_dlcx * M * p->Lo);
     long rows = (long)B * (T / hop);
     for (int i = 0; i < p->nup; ++i) {
       const int I = i == 0 ? p->Li : p->Lo;
@@ -341,16 +352,8 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->chain = p->Cr == 32 && p->Cd == 32 && !(nc && nc[0] == '1');
   p->oOCG = p->chain ? carve(cur, sizeof(float) * (size_t)L * M * 32) : 0;
   p->oSG = p->chain ? carve(cur, sizeof(float) * (size_t)L * m32(M) * 32) : 0;   // sg_off: whole 32-row blocks
-  const char* ov = getenv("LBWN_OVERLAP");
-  p->overlap = p->chain && !(ov && ov[0] == '0');
-  // dSKIP after the chain on the main stream at full rate (default): with the backward chain at
-  // ~850 µs, dPOST2 + dPOST1 alone fill the overlap window, and a lean dSKIP on the aux stream
-  // after it ran at ~70 TF (3.57 vs 3.47 ms per step).  LBWN_DSKIP_MAIN=0: the aux stream.
-  const char* dm = getenv("LBWN_DSKIP_MAIN");
-  p->dskip_main = p->overlap && !(dm && dm[0] == '0');
-  if (p->overlap) {
-    p->oSPLIT_AUX = carve(cur, sizeof(float) * (size_t)p->split_floats);
-  }
+  p->overlap = p->chain;
+  if (p->overlap && (p->Lo > 0 || p->Ge > 0)) p->oSPLIT_AUX = carve(cur, sizeof(float) * (size_t)p->split_floats);
   {  // conditioning
     const size_t f = sizeof(float);
     const long ncond = 2L * L * p->Cd;
@@ -375,6 +378,7 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     const W3Shape w = w3_shape(p, i);
     if (w.K % 32 == 0) p->oW3[i] = carve(cur, 2 * lbwn_split_planes_elems(w.rows, w.K));
   }
+  if (p->chain && p->Lo > 0 && lbwn_lc_in_chain_ok(p->Lo)) p->oLCX = carve(cur, 2 * (size_t)L * lbwn_lc_image_x3_elems());
   p->oHEADP = carve(cur, sizeof(float) * 3 * 2048);
   p->oBSUM = carve(cur, sizeof(float) * (size_t)p->Cs);
   p->oWPK = carve(cur, sizeof(float) * (size_t)L * lbwn_layer_image_floats());
@@ -440,14 +444,10 @@ int ensure_device(lbwn_plan* p) {
   if (p->overlap) {
     int least = 0, greatest = 0;
     LBWN_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    LBWN_HIP(hipStreamCreateWithPriority(&p->aux, hipStreamNonBlocking, least));
-    LBWN_HIP(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
-    LBWN_HIP(hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
     LBWN_HIP(hipStreamCreateWithPriority(&p->aux2, hipStreamNonBlocking, greatest));
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_chain, hipEventDisableTiming));
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_join2, hipEventDisableTiming));
-    LBWN_HIP(hipEventCreateWithFlags(&p->ev_pfork, hipEventDisableTiming));
-    LBWN_HIP(hipEventCreateWithFlags(&p->ev_pjoin, hipEventDisableTiming));
+    LBWN_HIP(hipEventCreateWithFlags(&p->ev_dlc, hipEventDisableTiming));
   }
   return 0;
 }
@@ -489,8 +489,30 @@ struct Cond {
   }
 };
 
+// the forward chain computes the LC term itself (bf16-split chain, 64 < n_lc_out <= 80)
+bool lc_in_chain(const lbwn_plan* p) { return p->oLCX && p->chain && lbwn_gemm_mode() == 1; }
+
+// COND = lc·LCcat [M][L·2Cd]: every layer's LC term (tmodel.py:155-160) as ONE GEMM, for the paths
+// that read it (f32 chains, per-layer kernels)
+int cond_project(lbwn_plan* p, const lbwn_params* P, void* ws, hipStream_t st) {
+  int e;
+  const long ncond = 2L * p->L * p->Cd;
+  float* cat = at<float>(ws, p->oLCCAT);
+  if ((e = lbwn_lc_pack_launch(cat, P->lc_sig, P->lc_gate, p->L, p->Lo, p->Cd, 1, st))) return e;
+  lbwn_gemm_args g = gemm0();
+  g.A = at<float>(ws, p->oLCACT[p->nup - 1]); g.lda = p->Lo; g.B = cat; g.ldb = ncond;
+  g.C = at<float>(ws, p->oCOND); g.ldc = ncond;
+  g.M = (int)p->M; g.N = (int)ncond; g.K = p->Lo;
+  Probe(p, st, "lc_cond");
+  if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
+  Probe::end(p, st, "lc_cond");
+  p->cond_valid = true;
+  return 0;
+}
+
 // GC table and the LC term: upsample (4× conv1d_transpose k = s, tmodel.py:68-83, each a GEMM
-// against the [s][O][I] filter read as k-contiguous), then COND = lc·LCcat.
+// against the [s][O][I] filter read as k-contiguous), then COND = lc·LCcat unless the forward
+// chain computes the LC term itself.
 int cond_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const float* mel, Cond& c, hipStream_t st) {
   int e;
   const int L = p->L, Cd = p->Cd;
@@ -515,71 +537,82 @@ int cond_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const float* mel,
       rows *= s;
       I = p->Lo;
     }
-    const long ncond = 2L * L * Cd;
-    float* cat = at<float>(ws, p->oLCCAT);
-    if ((e = lbwn_lc_pack_launch(cat, P->lc_sig, P->lc_gate, L, p->Lo, Cd, 1, st))) return e;
-    lbwn_gemm_args g = gemm0();
-    g.A = in; g.lda = p->Lo; g.B = cat; g.ldb = ncond; g.C = at<float>(ws, p->oCOND); g.ldc = ncond;
-    g.M = (int)p->M; g.N = (int)ncond; g.K = p->Lo;
-    Probe(p, st, "lc_cond");
-    if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
-    Probe::end(p, st, "lc_cond");
-    c.cond = at<float>(ws, p->oCOND);
-    c.ldcond = ncond;
+    p->cond_valid = false;
+    if (!lc_in_chain(p)) {
+      if ((e = cond_project(p, P, ws, st))) return e;
+      c.cond = at<float>(ws, p->oCOND);
+      c.ldcond = 2L * L * Cd;
+    }
   }
   return 0;
 }
 
-// After the layer stack: GC weight/table grads from GCD; LC grads from DVALL through
-// LCcat and the upsample stages (reverse), each a (split-K) GEMM.
-int cond_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G, void* ws, const float* mel,
-                  hipStream_t st) {
+// After the layer stack: GC weight/table grads from GCD (gc_backward); LC grads from DVALL:
+// dLCcat = lcᵀ·DV (lc_wgrad), dlc = DV·LCcatᵀ (lc_dlc), then the upsample stages in reverse
+// (lc_upsample_bwd), each a (split-K) GEMM.  The chain plans run them beside dSKIP (engine
+// backward); spl is the split-K workspace of the stream they run on.
+int gc_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G, void* ws, hipStream_t st) {
+  if (p->Ge <= 0) return 0;
+  return lbwn_gc_grad_launch(P->gc_embed, P->gc_sig, P->gc_gate, at<float>(ws, p->oGCD), at<float>(ws, p->oGCPART),
+                             G->gc_embed, G->gc_sig, G->gc_gate, p->L, p->ncat1, p->Ge, p->Cd, st);
+}
+
+int lc_wgrad(lbwn_plan* p, const lbwn_params* G, void* ws, float* spl, hipStream_t st) {
   int e;
-  const int L = p->L, Cd = p->Cd;
-  float* SPL = at<float>(ws, p->oSPLIT);
-  if (p->Ge > 0) {
-    if ((e = lbwn_gc_grad_launch(P->gc_embed, P->gc_sig, P->gc_gate, at<float>(ws, p->oGCD), at<float>(ws, p->oGCPART),
-                                 G->gc_embed, G->gc_sig, G->gc_gate, L, p->ncat1, p->Ge, Cd, st)))
-      return e;
-  }
-  if (p->Lo > 0) {
-    const long ncond = 2L * L * Cd;
-    const float* lc = at<float>(ws, p->oLCACT[p->nup - 1]);
-    float* dv = at<float>(ws, p->oDVALL);
-    // dLCcat = lcᵀ·DV  -> LC_SIGNAL_l / LC_GATE_l grads
+  const long ncond = 2L * p->L * p->Cd;
+  lbwn_gemm_args g = gemm0();
+  g.A = at<float>(ws, p->oLCACT[p->nup - 1]); g.lda = p->Lo; g.B = at<float>(ws, p->oDVALL); g.ldb = ncond;
+  g.C = at<float>(ws, p->oDLCCAT); g.ldc = ncond;
+  g.M = p->Lo; g.N = (int)ncond; g.K = (int)p->M;
+  Probe(p, st, "lc_wgrad");
+  if ((e = lbwn_gemm_launch(g, 0, 0, p->split_dlc, spl, st))) return e;
+  Probe::end(p, st, "lc_wgrad");
+  return lbwn_lc_pack_launch(at<float>(ws, p->oDLCCAT), G->lc_sig, G->lc_gate, p->L, p->Lo, p->Cd, 0, st);
+}
+
+int lc_dlc(lbwn_plan* p, const lbwn_params* P, void* ws, float* spl, hipStream_t st) {
+  int e;
+  const long ncond = 2L * p->L * p->Cd;
+  // LCcat is packed by the forward's COND projection; an in-chain-LC forward did not run it
+  if (!p->cond_valid && (e = lbwn_lc_pack_launch(at<float>(ws, p->oLCCAT), P->lc_sig, P->lc_gate, p->L, p->Lo, p->Cd,
+                                                 1, st)))
+    return e;
+  lbwn_gemm_args g = gemm0();
+  g.A = at<float>(ws, p->oDVALL); g.lda = ncond; g.B = at<float>(ws, p->oLCCAT); g.ldb = ncond;
+  g.C = at<float>(ws, p->oDLC[0]); g.ldc = p->Lo;
+  g.M = (int)p->M; g.N = p->Lo; g.K = (int)ncond;
+  Probe(p, st, "lc_dlc");
+  if ((e = lbwn_gemm_launch(g, 1, 1, p->split_dlcx, spl, st))) return e;
+  Probe::end(p, st, "lc_dlc");
+  return 0;
+}
+
+int lc_upsample_bwd(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G, void* ws, const float* mel, float* spl,
+                    hipStream_t st) {
+  int e;
+  const float* dout = at<float>(ws, p->oDLC[0]);
+  long rows = p->M;
+  int buf = 0;
+  Probe(p, st, "lc_up_bwd");
+  for (int i = p->nup - 1; i >= 0; --i) {
+    const int s = p->up[i], I = i == 0 ? p->Li : p->Lo;
+    rows /= s;  // stage input rows
+    const float* in = i == 0 ? mel : at<float>(ws, p->oLCACT[i - 1]);
+    // dF_i[(j,o)][i'] = Σ_bt dout[bt][(j,o)] · in[bt][i']
     lbwn_gemm_args g = gemm0();
-    g.A = lc; g.lda = p->Lo; g.B = dv; g.ldb = ncond; g.C = at<float>(ws, p->oDLCCAT); g.ldc = ncond;
-    g.M = p->Lo; g.N = (int)ncond; g.K = (int)p->M;
-    if ((e = lbwn_gemm_launch(g, 0, 0, p->split_dlc, SPL, st))) return e;
-    if ((e = lbwn_lc_pack_launch(at<float>(ws, p->oDLCCAT), G->lc_sig, G->lc_gate, L, p->Lo, Cd, 0, st))) return e;
-    // dlc = DV·LCcatᵀ
-    float* dout = at<float>(ws, p->oDLC[0]);
+    g.A = dout; g.lda = (long)s * p->Lo; g.B = in; g.ldb = I; g.C = G->lc_up[i]; g.ldc = I;
+    g.M = s * p->Lo; g.N = I; g.K = (int)rows;
+    if ((e = lbwn_gemm_launch(g, 0, 0, p->split_up[i], spl, st))) return e;
+    if (i == 0) break;  // no gradient into the mel input
+    float* din = at<float>(ws, p->oDLC[buf ^ 1]);
     g = gemm0();
-    g.A = dv; g.lda = ncond; g.B = at<float>(ws, p->oLCCAT); g.ldb = ncond; g.C = dout; g.ldc = p->Lo;
-    g.M = (int)p->M; g.N = p->Lo; g.K = (int)ncond;
-    if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
-    // upsample stages in reverse
-    long rows = p->M;
-    int buf = 0;
-    for (int i = p->nup - 1; i >= 0; --i) {
-      const int s = p->up[i], I = i == 0 ? p->Li : p->Lo;
-      rows /= s;  // stage input rows
-      const float* in = i == 0 ? mel : at<float>(ws, p->oLCACT[i - 1]);
-      // dF_i[(j,o)][i'] = Σ_bt dout[bt][(j,o)] · in[bt][i']
-      g = gemm0();
-      g.A = dout; g.lda = (long)s * p->Lo; g.B = in; g.ldb = I; g.C = G->lc_up[i]; g.ldc = I;
-      g.M = s * p->Lo; g.N = I; g.K = (int)rows;
-      if ((e = lbwn_gemm_launch(g, 0, 0, p->split_up[i], SPL, st))) return e;
-      if (i == 0) break;  // no gradient into the mel input
-      float* din = at<float>(ws, p->oDLC[buf ^ 1]);
-      g = gemm0();
-      g.A = dout; g.lda = (long)s * p->Lo; g.B = P->lc_up[i]; g.ldb = I; g.C = din; g.ldc = I;
-      g.M = (int)rows; g.N = I; g.K = s * p->Lo;
-      if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
-      dout = din;
-      buf ^= 1;
-    }
+    g.A = dout; g.lda = (long)s * p->Lo; g.B = P->lc_up[i]; g.ldb = I; g.C = din; g.ldc = I;
+    g.M = (int)rows; g.N = I; g.K = s * p->Lo;
+    if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
+    dout = din;
+    buf ^= 1;
   }
+  Probe::end(p, st, "lc_up_bwd");
   return 0;
 }
 
@@ -607,18 +640,10 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   float* R2 = at<float>(ws, p->oR2);
   float* LOG = at<float>(ws, p->oLOG);
   float* bsum = at<float>(ws, p->oBSUM);
-  // Weight packs (once per step, reused by the backward) on aux2, forked here and joined before
-  // the chain: they depend only on the weights, so they overlap embed / cond / D-sep below.
+  // Weight packs (once per step, reused by the backward), in line on the main stream (on a
+  // forked side stream the event round trips cost what the overlap hid)
   const bool x3 = lbwn_gemm_mode() == 1;
-  // LBWN_PACK_SIDE=1: on aux2 (forked / joined by events: the event round trips cost more than
-  // the ~20 µs of packs they hide); default: in line on the main stream
-  static const char* pse = getenv("LBWN_PACK_SIDE");
   hipStream_t pst = st;
-  if (p->aux2 && pse && pse[0] == '1') {
-    LBWN_HIP(hipEventRecord(p->ev_pfork, st));
-    LBWN_HIP(hipStreamWaitEvent(p->aux2, p->ev_pfork, 0));
-    pst = p->aux2;
-  }
   // per-layer weights -> padded f32 LDS images: the per-layer kernels and the f32 chains (the
   // bf16-split chains read their own images below)
   float* WPK = at<float>(ws, p->oWPK);
@@ -629,10 +654,12 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   // skip/head weights -> bf16 planes for the split GEMMs, forward and backward, and the split
   // per-layer images of the forward chain
   // ... and the backward chain's split images (dx weights + f32 residual image), one launch
+  const bool lcx = lc_in_chain(p);
   if (x3 && p->chain &&
       (e = lbwn_pack_layers_fb_x3_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b,
                                          at<unsigned short>(ws, p->oWPKX), at<float>(ws, p->oWPKB), L, Cr, Cd,
-                                         P->skip_b, p->Cs, bsum, pst)))
+                                         P->skip_b, p->Cs, bsum, P->lc_sig, P->lc_gate, p->Lo,
+                                         lcx ? at<unsigned short>(ws, p->oLCX) : nullptr, pst)))
     return e;
   const bool bsum_done = x3 && p->chain && P->skip_b;   // summed by the pack launch above
   if (x3) {
@@ -650,14 +677,12 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     }
     if (nj && (e = lbwn_split_planes_launch(nj, jw, jld, jr, jk, jt, jo, pst))) return e;
   }
-  if (pst != st) LBWN_HIP(hipEventRecord(p->ev_pjoin, pst));
   // one-hot·PRE + PRE_BIAS == row gather (tmodel.py:53-66, :86-102)
   if ((e = lbwn_embed_launch(wav_q, P->pre, P->pre_b, X, B, T, H, Cr, p->Q, st))) return e;
   Cond cd;
   if ((e = cond_forward(p, P, ws, mel, cd, st))) return e;
   // D-separation prepend for every layer (tmodel.py:122-127)
   if ((e = lbwn_dsep_prepend_launch(X, p->x_layer_stride, save, L, p->nbl, B, T, H, Cr, st))) return e;
-  if (pst != st) LBWN_HIP(hipStreamWaitEvent(st, p->ev_pjoin, 0));   // the packs joined
   if (p->chain) {
     // all layers in one persistent launch (tmodel.py:313-325)
     lbwn_chain_args c;
@@ -667,6 +692,9 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     if (x3 && p->oSG) { c.SG = at<float>(ws, p->oSG); c.sgls = m32(M) * 32; }
     p->fwd_x3 = c.SG != nullptr;
     c.gc_tab = cd.gc_tab; c.gc_ld = cd.gc_ld; c.cond = cd.cond; c.ldcond = cd.ldcond;
+    if (lcx) {
+      c.lcact = at<float>(ws, p->oLCACT[p->nup - 1]); c.lcimg = at<unsigned short>(ws, p->oLCX); c.Lo = p->Lo;
+    }
     c.flags = at<unsigned>(ws, p->oFLAGS); c.status = at<unsigned>(ws, p->oSTATUS);
     c.flags_zeroed = 1;   // zeroed with the status word at the step start
     if (p->ctrace_blk >= 0) { c.trace = at<long long>(ws, p->oCTRACE); c.trace_blk = p->ctrace_blk; }
@@ -817,11 +845,10 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     }
     if (G->skip_b && (e = lbwn_bcast_rows_launch(G->skip_b, L, Cs, st))) return e;
   }
-  // weight gradients of the head and skip GEMMs (dPOST2, dPOST1; dSKIP unless on the main
-  // stream).  With the chain they go to the aux stream AFTER the chain launch, forked on the
-  // chain's completion: a chain block takes a whole CU's LDS, so nothing runs beside it, and
-  // aux blocks dispatched before it would hold CUs its lock-step tiles wait for.  After the
-  // chain they share the chip with dSKIP (main) and the slab reduction (aux2) at full rate.
+  // weight gradients of the head GEMMs (dPOST2, dPOST1) on the main stream BEFORE the chain at
+  // full rate: a chain block takes a whole CU's LDS, so nothing runs beside it, and side-stream
+  // blocks dispatched before it would hold CUs its lock-step tiles wait for (forked after the
+  // chain they shared the chip with dSKIP and ran slower).  dSKIP follows the chain.
   auto dskip = [&](hipStream_t s2, float* spl) -> int {
     int e2;
     lbwn_gemm_args gk = gemm0();
@@ -832,7 +859,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     Probe::end(p, s2, "dskip");
     return 0;
   };
-  auto aux_gemms = [&](hipStream_t ws_st, float* WSPL) -> int {
+  auto head_wgrads = [&](hipStream_t ws_st, float* WSPL) -> int {
     int e2;
     // dPOST2 = R2ᵀ·dlogits (db2 = Σ dlogits: the column sums above)
     lbwn_gemm_args gk = gemm0();
@@ -847,13 +874,9 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     Probe(p, ws_st, "dpost1");
     if ((e2 = lbwn_gemm_launch(gk, 0, 0, p->split_post1, WSPL, ws_st))) return e2;
     Probe::end(p, ws_st, "dpost1");
-    if (!p->dskip_main && (e2 = dskip(ws_st, WSPL))) return e2;
     return 0;
   };
-  // LBWN_WG_AFTER=1: after the chain on the aux stream (above); default: here on the main stream
-  static const char* wga = getenv("LBWN_WG_AFTER");
-  const bool wg_after = p->overlap && wga && wga[0] == '1';
-  if (!wg_after && (e = aux_gemms(st, SPL))) return e;
+  if ((e = head_wgrads(st, SPL))) return e;
   // residual stack in reverse (conditioning recomputed from the forward's GCTAB / COND)
   Cond cd;
   if (p->Ge > 0) {
@@ -863,6 +886,10 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     LBWN_HIP(hipMemsetAsync(cd.gc_dtab, 0, sizeof(float) * (size_t)L * p->ncat1 * 2 * Cd, st));
   }
   if (p->Lo > 0) {
+    // the bf16-split backward chain reads no conditioning; the f32 chain and the per-layer
+    // kernels recompute the gate from COND, which an in-chain-LC forward did not write
+    const bool reads_cond = !(p->chain && p->fwd_x3 && lbwn_gemm_mode() == 1);
+    if (reads_cond && !p->cond_valid && (e = cond_project(p, P, ws, st))) return e;
     cd.cond = at<float>(ws, p->oCOND);
     cd.ldcond = 2L * L * Cd;
     cd.dv_out = at<float>(ws, p->oDVALL);
@@ -897,38 +924,40 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     Probe(p, st, "layer_bwd");
     if ((e = lbwn_chain_bwd_launch(c, st))) return e;
     Probe::end(p, st, "layer_bwd");
-    if (wg_after) {   // fork on the chain's completion: head/skip weight gradients on aux
-      LBWN_HIP(hipEventRecord(p->ev_fork, st));
-      LBWN_HIP(hipStreamWaitEvent(p->aux, p->ev_fork, 0));
-      if ((e = aux_gemms(p->aux, at<float>(ws, p->oSPLIT_AUX)))) return e;
-      LBWN_HIP(hipEventRecord(p->ev_join, p->aux));
-    }
     // slab reduction + dPRE on the second side stream (HBM-bound, beside dSKIP's MFMA work)
     hipStream_t rst = st;
     if (p->aux2) {
       rst = p->aux2;
       LBWN_HIP(hipEventRecord(p->ev_chain, st));
       LBWN_HIP(hipStreamWaitEvent(rst, p->ev_chain, 0));
+      p->bwd_chain_event = true;
     }
     lbwn_layer_red_args r;
     r.slab = SLABS; r.nparts = ntiles; r.stride = sstr; r.Cr = Cr; r.Cd = Cd;
     r.dsig = G->sig; r.dgate = G->gate; r.dres = G->res;
     r.dbsig = G->sig_b; r.dbgate = G->gate_b; r.dbres = G->res_b;
-    // LBWN_PG_ORDER: 1 (default) dPRE then the slab reduction on the side stream (the small
-    // scatter grid starts while dSKIP's blocks still leave room: step -0.5 %), 0 the reverse,
-    // 2 dPRE on the main stream ahead of dSKIP
-    static const char* pgo = getenv("LBWN_PG_ORDER");
-    const int pg_order = pgo ? pgo[0] - '0' : 1;
-    auto pre_grad = [&](hipStream_t s2) {
-      return lbwn_pre_grad_launch(wav_q, at<float>(ws, p->oGA[0]), at<float>(ws, p->oGC0[0]), 1, B, T, Cr, Q, G->pre,
-                                  G->pre_b, at<float>(ws, p->oSPLIT2), s2);
-    };
-    if (pg_order == 1 && (e = pre_grad(rst))) return e;
-    if (pg_order == 2 && (e = pre_grad(st))) return e;
+    // Side stream, beside the main stream's dlc (LC archs) and dSKIP: dLCcat = lcᵀ·DV first (the
+    // largest piece), then dPRE and the slab reduction (the small scatter grid starts while the
+    // main stream's GEMM blocks still leave room: step -0.5 %), the GC table grads,
+    // and the LC upsample backward once dlc (main stream) is done: small latency-bound GEMMs that
+    // fill the room dSKIP leaves.
+    float* SPLA = p->oSPLIT_AUX ? at<float>(ws, p->oSPLIT_AUX) : SPL;
+    if (p->Lo > 0 && (e = lc_wgrad(p, G, ws, SPLA, rst))) return e;
+    if ((e = lbwn_pre_grad_launch(wav_q, at<float>(ws, p->oGA[0]), at<float>(ws, p->oGC0[0]), 1, B, T, Cr, Q, G->pre,
+                                  G->pre_b, at<float>(ws, p->oSPLIT2), rst)))
+      return e;
     Probe(p, rst, "layer_reduce");
     if ((e = lbwn_layer_reduce_all_launch(r, L, (long)ntiles * sstr, rst))) return e;
     Probe::end(p, rst, "layer_reduce");
-    if (pg_order != 1 && pg_order != 2 && (e = pre_grad(rst))) return e;
+    if ((e = gc_backward(p, P, G, ws, rst))) return e;
+    if (p->Lo > 0) {
+      if ((e = lc_dlc(p, P, ws, SPL, st))) return e;
+      if (rst != st) {
+        LBWN_HIP(hipEventRecord(p->ev_dlc, st));
+        LBWN_HIP(hipStreamWaitEvent(rst, p->ev_dlc, 0));
+      }
+      if ((e = lc_upsample_bwd(p, P, G, ws, mel, SPLA, rst))) return e;
+    }
     if (p->aux2) LBWN_HIP(hipEventRecord(p->ev_join2, rst));
   } else {
       for (int l = L - 1; l >= 0; --l) {
@@ -956,14 +985,20 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     r.dbsig = G->sig_b; r.dbgate = G->gate_b; r.dbres = G->res_b;
     if ((e = lbwn_layer_reduce_all_launch(r, L, (long)p->nblk * sstr, st))) return e;
   }
-  if ((e = cond_backward(p, P, G, ws, mel, st))) return e;
-  if (p->dskip_main && (e = dskip(st, SPL))) return e;
+  if (!p->chain) {
+    if ((e = gc_backward(p, P, G, ws, st))) return e;
+    if (p->Lo > 0) {
+      if ((e = lc_wgrad(p, G, ws, SPL, st))) return e;
+      if ((e = lc_dlc(p, P, ws, SPL, st))) return e;
+      if ((e = lc_upsample_bwd(p, P, G, ws, mel, SPL, st))) return e;
+    }
+  }
+  if ((e = dskip(st, SPL))) return e;
   // dx_0 = (g + dcur) + shift(dprev) formed inside the scatter; dPRE = onehot(q)ᵀ·dx_0, dPRE_BIAS = Σ dx_0
   // (the chain path enqueued it on the second side stream above)
   if (!p->chain && (e = lbwn_pre_grad_launch(wav_q, at<float>(ws, p->oGA[0]), at<float>(ws, p->oGC0[0]), 1, B, T,
                                              Cr, Q, G->pre, G->pre_b, at<float>(ws, p->oSPLIT2), st)))
     return e;
-  if (wg_after) LBWN_HIP(hipStreamWaitEvent(st, p->ev_join, 0));
   if (p->chain && p->aux2) LBWN_HIP(hipStreamWaitEvent(st, p->ev_join2, 0));
   if ((e = head_unpad_grads(p, Gref, ws, st))) return e;
   return 0;

@@ -642,11 +642,8 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
   // 256-row tiles (8 waves, 2-stage pipeline) for the tall k-contiguous products with N <= 2048
   // (skip fwd, post1/post2 fwd, dH1, dS: 3-8 % faster; dZ, N = 1600: step -0.5 % in a same-box
   // A/B since the epilogue and split changes); 128-row tiles at 2 blocks per CU for the rest
-  // (the mn-contiguous weight gradients: 1.3-1.5x slower on 256-row tiles).  LBWN_X3_WM=2|4
-  // forces one; LBWN_X3_WM_NMAX moves the N limit (512 = the round-2 v4 choice).
-  static const char* env = getenv("LBWN_X3_WM");
-  static const int nmax = getenv("LBWN_X3_WM_NMAX") ? atoi(getenv("LBWN_X3_WM_NMAX")) : 2048;
-  const int wm = a.colpart ? 4 : env ? (env[0] == '4' ? 4 : 2) : (a_kcontig && a.N <= nmax && a.M >= 8192 ? 4 : 2);
+  // (the mn-contiguous weight gradients: 1.3-1.5x slower on 256-row tiles)
+  const int wm = (a.colpart || (a_kcontig && a.N <= 2048 && a.M >= 8192)) ? 4 : 2;
   lbwn_gemm_args g;
   dim3 grid;
   int e = gemm_setup(a, a_kcontig, b_kcontig, split_k, slab_ws, X3_BK, 64 * wm, 128, g, grid);
@@ -701,10 +698,6 @@ int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int 
   if (lbwn_gemm_mode() == 1 && a.a_codes == nullptr && a.K >= 4 && a.M >= 4 && a.N >= 4)
     return gemm_launch_x3(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
   LBWN_REQUIRE(a.colpart == nullptr, "gemm: column partials need the bf16-split form");
-  // tall products (M = B·T positions): 256 × 128 block tiles, each wave 128 × 64
-  static const char* env = getenv("LBWN_GEMM_TILE");
-  const bool tall = (env && env[0] == '2') && a.M >= 8192 && split_k <= 1;   // measured slower: opt-in
-  if (tall) return gemm_launch_t<16, 256, 128>(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
   return gemm_launch_t<16, 128, 128>(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
 }
 

@@ -5,7 +5,7 @@
 // cache: layer l keeps its last d inputs, slot t mod d, replacing imodel's shift-by-chunk
 // buffers imodel.py:88-98, :190-207), the next input code, the teacher vector and a
 // counter-based RNG.  Two execution forms, chosen at plan creation:
-//   persistent (B <= 32, the default there): ONE launch per run, gen_persist_kernel — chain
+//   persistent (B <= 16, the default there): ONE launch per run, gen_persist_kernel — chain
 //     blocks (one per stream) and 32 head blocks hand z, the skip vector and the partial logits
 //     to each other as tagged granules; weights of the head stay in registers for the run
 //   per step (any B): gen_wave (one workgroup per stream: PRE row (+bias), 50 × [dilated conv,
@@ -553,7 +553,7 @@ __global__ __launch_bounds__(64) void gen_sample_kernel(DrawK a, const long long
 
 constexpr long long G_SPIN_TIMEOUT = 400000000LL;   // wall_clock64 ticks (100 MHz) = 4 s
 
-// ---- persistent generation: one launch per run (B <= 32) --------------------------------
+// ---- persistent generation: one launch per run (B <= 16) --------------------------------
 // Roles (one 512-thread workgroup per CU, all resident: B + P_NH <= CUs):
 //   chain block b < B   per step: draw the previous step (gather the P_NH partial-logit
 //                       granules of stream b, Σ + b2, wave-level draw), PRE row, 50 layers as in

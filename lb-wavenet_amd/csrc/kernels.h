@@ -76,9 +76,13 @@ int lbwn_layer_slab_stride();
 int lbwn_layer_image_x3_elems();
 // lbwn_pack_layers_x3_launch + lbwn_pack_layers_bx3_launch in one launch, plus (skip_b, bsum
 // non-null) bsum[n] = Σ_l skip_b[l·Cs + n] (lbwn_sum_bias_launch)
+// ... and (lcout non-null) the L split LC images of the in-chain LC term (lbwn_lc_image_x3_elems each)
 int lbwn_pack_layers_fb_x3_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                                   const float* res, const float* res_b, unsigned short* fout, float* bout, int L,
-                                  int Cr, int Cd, const float* skip_b, int Cs, float* bsum, hipStream_t st);
+                                  int Cr, int Cd, const float* skip_b, int Cs, float* bsum, const float* lc_sig,
+                                  const float* lc_gate, int Lo, unsigned short* lcout, hipStream_t st);
+int lbwn_lc_image_x3_elems();
+int lbwn_lc_in_chain_ok(int Lo);   // n_lc_out the forward chain's in-chain LC term supports
 int lbwn_pack_layers_x3_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                                const float* res, const float* res_b, unsigned short* out, int L, int Cr, int Cd,
                                hipStream_t st);
@@ -120,6 +124,8 @@ struct lbwn_chain_args {
   // forward chain (layer stride sgls floats), and the backward images (lbwn_pack_layers_bx3)
   float* SG = nullptr; long sgls = 0;
   const float* bimg = nullptr;
+  // forward, bf16-split form: in-chain LC term (instead of cond): LC input [M][Lo], split images
+  const float* lcact = nullptr; const unsigned short* lcimg = nullptr; int Lo = 0;
 };
 int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st);
 int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st);
@@ -164,8 +170,9 @@ int lbwn_fill_launch(float* p, float v, long n, hipStream_t st);
 
 int lbwn_adam_launch2(float* params, const float* grads, float* m, float* v, long n_weights, long n_total,
                       float lr, float b1, float b2, float eps, float l2, const float* stats,
-                      const long long* counters, hipStream_t st);
-int lbwn_counters_launch(long long* counters, const float* stats, int adam_applied, hipStream_t st);
+                      const long long* counters, const unsigned* status, hipStream_t st);
+int lbwn_counters_launch(long long* counters, const float* stats, int adam_applied, const unsigned* status,
+                         hipStream_t st);
 // dPRE = onehot(q)ᵀ·dx0 as an LDS-histogram scatter + fixed-order reduction; dPRE_B = Σ dx0 (nullable);
 // dx0[m] = g[m] + (t+gd < T ? dprev[m+gd] : 0) formed on the fly
 int lbwn_pre_grad_ws_floats(int Q, int Cr);

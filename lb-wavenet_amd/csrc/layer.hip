@@ -97,6 +97,40 @@ constexpr int XIMG_US = XB_OFF + 2 * 96;                       // bf16 elements 
 constexpr int XIMG_F = XIMG_US / 2;                            // = 8160 floats, multiple of 4
 static_assert(XIMG_F % 4 == 0 && XB_OFF % 8 == 0, "x3 image alignment");
 
+// Split image of a layer's LC projection for the forward chain's in-chain LC term
+// (tmodel.py:155-160: v_k += lc·LC_k), bf16 units: LCT[o (sig 0..31 | gate 32..63)][plane][k 0..79]
+// in rows of LC_ROW = 3·80 + 8 pad (124 dwords: 4·odd, so every 16-lane ds_read_b128 group of the
+// A-fragment reads is conflict-free, MI355X_MICROARCH §LDS), k >= n_lc_out zero.  31 KiB per layer:
+// exactly 31 LDS-DMA pieces.  Used when 64 < n_lc_out <= 80 (LC_K = 5 k-steps of 16).
+constexpr int LC_K = 5, LC_KP = 16 * LC_K, LC_ROW = 3 * LC_KP + 8;
+constexpr int LCIMG_US = 64 * LC_ROW;                          // bf16 elements per layer image
+constexpr int LCIMG_F = LCIMG_US / 2;                          // = 7936 floats
+static_assert(LCIMG_F % 256 == 0, "LC image: whole 1-KiB DMA pieces");
+
+LBWN_DEV void pack_lc_x3_body(int l, const float* lsig, const float* lgate, unsigned short* out, int Lo, int Cd) {
+  unsigned short* img = out + (long)l * LCIMG_US;
+  for (int e = threadIdx.x; e < 64 * (LC_ROW / 2); e += blockDim.x) {
+    const int o = e / (LC_ROW / 2), kk = 2 * (e % (LC_ROW / 2));
+    unsigned short* row = img + o * LC_ROW;
+    if (kk >= LC_KP) {   // pad columns (never read) and the plane slots past k: written as part of planes below
+      if (kk >= 3 * LC_KP) *(unsigned*)(row + kk) = 0u;
+      continue;
+    }
+    const float* w = (o < 32 ? lsig : lgate) + (long)l * Lo * Cd;
+    const int oc = o & 31;
+    floatx2 x = {0.f, 0.f};
+    if (oc < Cd) {
+      if (kk < Lo) x[0] = w[(long)kk * Cd + oc];
+      if (kk + 1 < Lo) x[1] = w[(long)(kk + 1) * Cd + oc];
+    }
+    unsigned hi, mi, lo;
+    split2(x, hi, mi, lo);
+    *(unsigned*)(row + kk) = hi;
+    *(unsigned*)(row + LC_KP + kk) = mi;
+    *(unsigned*)(row + 2 * LC_KP + kk) = lo;
+  }
+}
+
 LBWN_DEV void pack_x3_body(int l, const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                           const float* res, const float* res_b, unsigned short* out, int Cr, int Cd) {
   const float* ws = sig + (long)l * 2 * Cr * Cd;
@@ -366,6 +400,22 @@ __global__ __launch_bounds__(256) void layer_fwd_kernel(FwdK a) {
 // Deadlock freedom: tiles run in rounds of gridDim.x ≤ resident blocks, in increasing tile
 // order; a producer tile is always in the same round (resident) or an earlier one (done).
 // Every spin is bounded (SPIN_TIMEOUT) and reports through the status word.
+typedef __attribute__((address_space(3))) void lds_void;
+
+// One LDS-DMA piece (global_load_lds_dwordx4: 64 lanes × 16 B from per-lane addresses to
+// lds_dst + 16·lane) issued from inline asm, so the compiler neither knows the LDS it writes (no
+// conservative vmcnt(0) before every later LDS access) nor counts it: the kernel lands these
+// pieces itself with an explicit vmcnt(0) drain + barrier before their first reader.
+LBWN_DEV void dma16(const void* g, float* lds_dst) {
+  const unsigned base =
+      __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)lds_dst);
+  unsigned saved;   // m0 is reserved by the compiler: saved and restored around the piece
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(saved)
+               : "s"(base), "v"(g)
+               : "memory");
+}
+
 typedef __attribute__((address_space(1))) unsigned gu32;
 constexpr long long SPIN_TIMEOUT = 400000000LL;  // wall_clock64 ticks (100 MHz) = 4 s
 constexpr int BUF_DW3 = 0x00020000;
@@ -381,12 +431,69 @@ struct ChainFK {
   long long* trace; int trace_blk;   // debug stamps (null in production)
   const unsigned short* ximg;        // L split images (XIMG_US bf16 each): the bf16-split form
   float* SG; long sgls;              // σ(v_gate) rows [L][M32][32] (sg_off blocks) for chain_bwd_x3_kernel, or null
+  // in-chain LC term (chain_fwd_kernel<true, true>): the upsampled LC input [M][Lo] and the L
+  // split LC images (LCIMG_US bf16 each)
+  const float* lcact; const unsigned short* lcimg; int Lo;
 };
+
+// lc·[LC_SIGNAL_l | LC_GATE_l] onto the accumulators (tmodel.py:155-160): A = the layer's LC
+// image rows (out channel), B = this lane's LC input row, pre-split once per tile (lcb); the
+// fragments of k-step s+1 are read while step s's MFMAs issue
+LBWN_DEV void lc_terms(const unsigned short* LI, const bf16x8 (&lcb)[LC_K][3], int pi, int h, floatx16& acc_s,
+                       floatx16& acc_g) {
+  bf16x8 fs[2][3], fg[2][3];
+  auto load = [&](int s2, int buf) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      fs[buf][p] = *(const bf16x8*)(LI + pi * LC_ROW + LC_KP * p + 16 * s2 + 8 * h);
+      fg[buf][p] = *(const bf16x8*)(LI + (32 + pi) * LC_ROW + LC_KP * p + 16 * s2 + 8 * h);
+    }
+  };
+  load(0, 0);
+#pragma unroll
+  for (int s2 = 0; s2 < LC_K; ++s2) {
+    const int cb = s2 & 1;
+    if (s2 + 1 < LC_K) load(s2 + 1, cb ^ 1);
+    acc_s = mfma_x3(fs[cb], lcb[s2], acc_s);
+    acc_g = mfma_x3(fg[cb], lcb[s2], acc_g);
+  }
+}
+
+// one layer's LC image into LDS by LDS-DMA (wave w moves pieces w, w+4, ...); landed by the
+// caller's next vmcnt drain + barrier
+LBWN_DEV void dma_lc_image(const unsigned short* lcimg, int l, float* LCI, int w, int lane) {
+  const float* src = (const float*)lcimg + (long)l * LCIMG_F + lane * 4;
+#pragma unroll
+  for (int i = 0; i < (LCIMG_F / 256 + 3) / 4; ++i) {
+    const int pc = w + 4 * i;
+    if (pc < LCIMG_F / 256) dma16(src + pc * 256, LCI + pc * 256);
+  }
+}
 
 // GC + LC term of layer l for this lane's position, in acc layout: cv[q] = sig channels
 // 8q+4h..+3, cv[4+q] = gate channels (16-B loads; issued one layer ahead by the chains).
-template <typename K>
+// CM (compile time): 0 no conditioning, 1 GC only (the in-chain-LC forward of arch5 and GC-only
+// archs), 2 any (runtime pointers).  CM 1 loads are issued unconditionally at clamped rows (a row
+// past T feeds only its own, discarded, position column) straight into cv: an add right after the
+// load (CM 2's zero-init + add) or a register copy merging paths made hipcc wait for the loads --
+// with vmcnt(0), which also waited out the x_{l+1} stores issued just before (the drain the own
+// tap is meant to hide).
+template <int CM, typename K>
 LBWN_DEV void load_cond(const K& a, int l, int myid, long m, bool valid, int h, floatx4 (&cv)[8]) {
+  if (CM == 0) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) cv[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+    return;
+  }
+  if (CM == 1) {
+    const float* g = a.gc_tab + (long)myid * a.gc_ld + (long)l * 64;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      cv[q] = *(const floatx4*)(g + 8 * q + 4 * h);
+      cv[4 + q] = *(const floatx4*)(g + 32 + 8 * q + 4 * h);
+    }
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < 8; ++q) cv[q] = floatx4{0.f, 0.f, 0.f, 0.f};
   if (!valid) return;
@@ -493,6 +600,8 @@ static_assert(4096 + 768 <= 2 * LP * XS, "RED + bias partials must fit in Xp and
 constexpr int CF_LDS = 3 * LP * XS + 2 * WIMG;      // Xc[2] | HALO | IMG[2]  (99.8 KB)
 constexpr int IMG_PF = (WIMG / 4 + 255) / 256;      // float4 per thread to prefetch an image
 constexpr int CF_LDS_X3 = 3 * LP * XS + 2 * XIMG_F;  // with split images (120.6 KB)
+constexpr int CF_LDS_X3LC = CF_LDS_X3 + LCIMG_F;      // + one LC image (151.6 KB)
+static_assert(CF_LDS_X3LC * 4 + 16 <= 160 * 1024, "chain fwd x3 + LC LDS");
 
 // Per layer l (weight image IMG[l&1]):
 //   wait for the producer tile's x_l, halo rows (sc1 loads), barrier;
@@ -505,16 +614,24 @@ constexpr int CF_LDS_X3 = 3 * LP * XS + 2 * XIMG_F;  // with split images (120.6
 //   forced a barrier between this layer's last read and the next layer's first.
 // X3: the conv and residual products on the bf16 cores from split images (ChainFK::ximg);
 // otherwise v_mfma_f32_32x32x2_f32 from the f32 images.
-template <bool X3>
+// LC (X3 only): the LC term lc·LC_l computed in the chain (no [M][L·2Cd] COND round trip): the
+// tile's LC input rows are split once into registers; the layer's LC image (one LDS buffer) is
+// read with the own tap in step 7 of the previous layer (tile start for layer 0), and the image
+// two layers ahead is LDS-DMA'd in step 9, after the publish barrier (every wave is past its
+// reads), landing with the next layer's halo loads (in-order vmcnt) before its halo barrier.
+template <bool X3, bool LC, int CM>
 __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
+  static_assert(X3 || !LC, "in-chain LC needs the split images");
   constexpr int IMGF = X3 ? XIMG_F : WIMG;              // floats per layer image
   constexpr int PF = (IMGF / 4 + 255) / 256;            // float4 per thread to prefetch one
-  __shared__ __attribute__((aligned(16))) float sm[X3 ? CF_LDS_X3 : CF_LDS];
+  __shared__ __attribute__((aligned(16))) float sm[LC ? CF_LDS_X3LC : X3 ? CF_LDS_X3 : CF_LDS];
   __shared__ int s_fail;
   float* HALO = sm + 2 * LP * XS;
   float* IMG0 = HALO + LP * XS;
   // f32: [W 64×WS | R 32×XS | bs 64 | br 32]; X3: [WT | RT | bs 64 | br 32] (bf16 + f32)
   auto img = [&](int l) { return IMG0 + (l & 1) * IMGF; };
+  float* LCI = IMG0 + 2 * IMGF;   // LC: the one LC image buffer
+  const unsigned short* LCIu = (const unsigned short*)LCI;
   const float* wsrc = X3 ? (const float*)a.ximg : a.wpack;
   auto bias_of = [&](const float* im) { return X3 ? im + XB_OFF / 2 : im + 64 * WS + 32 * XS; };
 
@@ -529,22 +646,55 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
     const bool valid = t < a.T;
     const long m = (long)b * a.T + t;
     const long sb = (long)b * (a.H + a.T) * 32;  // stream base inside a layer buffer
-    const bool has_cond = a.gc_tab || a.cond;
+    constexpr bool has_cond = CM != 0;
     const int myid = (a.gc_tab && valid) ? a.ids[m] : 0;
     floatx4 cv[8];
-    load_cond(a, 0, myid, m, valid && has_cond, h, cv);
+    load_cond<CM>(a, 0, myid, m, valid && has_cond, h, cv);
+    // LC: this lane's LC input row, split once for the tile (B operand: k = 16s + 8h + j)
+    bf16x8 lcb[LC_K][3];
+    if (LC) {
+      const float* lrow = a.lcact + ((long)b * a.T + min(t, a.T - 1)) * a.Lo;
+#pragma unroll
+      for (int s2 = 0; s2 < LC_K; ++s2) {
+        const int k0 = 16 * s2 + 8 * h;
+        floatx4 u = *(const floatx4*)(lrow + min(k0, a.Lo - 4));       // clamped, then select
+        floatx4 v = *(const floatx4*)(lrow + min(k0 + 4, a.Lo - 4));
+        if (k0 >= a.Lo) u = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (k0 + 4 >= a.Lo) v = floatx4{0.f, 0.f, 0.f, 0.f};
+        split8(u, v, lcb[s2]);
+      }
+    }
     __syncthreads();  // previous tile's LDS use done
-    for (int e = tid; e < IMGF / 4; e += 256) *(floatx4*)(img(0) + 4 * e) = *(const floatx4*)(wsrc + 4 * e);
-    if (a.L > 1)
-      for (int e = tid; e < IMGF / 4; e += 256) *(floatx4*)(img(1) + 4 * e) = *(const floatx4*)(wsrc + IMGF + 4 * e);
+    if (LC) dma_lc_image(a.lcimg, 0, LCI, w, lane);
+    {  // images of layers 0 and 1 (contiguous in both places): every load issued before the first
+       // store (a load-store loop waited out one round trip per iteration)
+      constexpr int NI = (2 * IMGF / 4 + 255) / 256;
+      const int nimg4 = min(a.L, 2) * IMGF / 4;
+      floatx4 iv[NI];
+#pragma unroll
+      for (int i = 0; i < NI; ++i) iv[i] = *(const floatx4*)(wsrc + 4 * min(tid + 256 * i, nimg4 - 1));
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int e = tid + 256 * i;
+        if (e < nimg4) *(floatx4*)(img(0) + 4 * e) = iv[i];
+      }
+    }
     stage_rows(sm, a.X + sb, t0, 0, a.T, a.H, 32, tid);  // x_0 (embed output, pre-launch)
+    if (LC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the LC image DMA
     __syncthreads();
-    // layer 0's own tap W1·x_0[t]
+    // layer 0's own tap W1·x_0[t] (+ its LC term)
     floatx16 acc_s, acc_g;
     conv_init(bias_of(img(0)), cv, h, acc_s, acc_g);
-    if (has_cond && a.L > 1) load_cond(a, 1, myid, m, valid, h, cv);
+    if (has_cond && a.L > 1) load_cond<CM>(a, 1, myid, m, valid, h, cv);
     if (X3) conv_half_x3(sm + r * XS, (const unsigned short*)img(0) + 96, pi, h, acc_s, acc_g);
     else conv_half(sm + r * XS, img(0) + 32 * WS, pi, h, acc_s, acc_g);
+    if (LC) {
+      lc_terms(LCIu, lcb, pi, h, acc_s, acc_g);
+      if (a.L > 1) {
+        __syncthreads();   // every wave is past its LC_0 reads
+        dma_lc_image(a.lcimg, 1, LCI, w, lane);   // lands with layer 0's halo loads
+      }
+    }
     const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && tile == (int)blockIdx.x;
 #define FSTAMP(i) if (trc) a.trace[16 * l + (i)] = clock64()
     for (int l = 0; l < a.L; ++l) {
@@ -556,13 +706,7 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
       const float* Wl = img(l);
       const float* Rs = Wl + 64 * WS;
       const float* br = bias_of(Wl) + 64;
-      // 1. prefetch the image of layer l+2 (pre-launch data: plain loads, clamped: no branch)
-      floatx4 pf[PF];
-      if (l + 2 < a.L) {
-        const floatx4* src = (const floatx4*)(wsrc + (long)(l + 2) * IMGF);
-#pragma unroll
-        for (int i = 0; i < PF; ++i) pf[i] = src[min(tid + 256 * i, IMGF / 4 - 1)];
-      }
+      floatx4 pf[PF];   // image of layer l+2, loaded in step 3
       FSTAMP(1);
       // 2. wait for the producer of the halo rows (x_l is layer l-1's output)
       const int ptt = tt - max(1, d / LP);
@@ -584,10 +728,23 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
           const int e = min(tid + 256 * i, nh * 8 - 1), row = e >> 3, c4 = (e & 7) * 4;
           hv[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((a.H + t0 + row - d) * 32 + c4) * 4, 0, 16);
         }
+        // 1. prefetch the image of layer l+2 (pre-launch data: plain loads, clamped: no branch),
+        //    issued BEHIND the halo loads: the halo wait then leaves them in flight (vmcnt(PF)),
+        //    where in front of the producer poll they were waited out by lane 0's vmcnt(0)
+        //    (unconditional, at a clamped layer: a skipped branch made hipcc wait as if they were
+        //    not in flight)
+        {
+          const floatx4* src = (const floatx4*)(wsrc + (long)min(l + 2, a.L - 1) * IMGF);
+#pragma unroll
+          for (int i = 0; i < PF; ++i) pf[i] = src[min(tid + 256 * i, IMGF / 4 - 1)];
+        }
+        // every HALO row written (rows >= nh get a copy of row nh-1 and are never read: only rows
+        // r < d are): a store behind `e < nh*8` made hipcc sink the 4th load into that branch,
+        // issued after the first three had drained (one more L2 round trip per layer)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int e = tid + 256 * i;
-          if (e < nh * 8) *(floatx4*)(HALO + (e >> 3) * XS + (e & 7) * 4) = hv[i];
+          *(floatx4*)(HALO + (e >> 3) * XS + (e & 7) * 4) = hv[i];
         }
       }
       __syncthreads();
@@ -658,24 +815,20 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
         wave_lds_fence();
         const float* Wn = img(l + 1);
         conv_init(bias_of(Wn), cv, h, acc_s, acc_g);
-        if (has_cond && l + 2 < a.L) load_cond(a, l + 2, myid, m, valid, h, cv);
+        if (has_cond && l + 2 < a.L) load_cond<CM>(a, l + 2, myid, m, valid, h, cv);
         if (X3) conv_half_x3(nrow, (const unsigned short*)Wn + 96, pi, h, acc_s, acc_g);
         else conv_half(nrow, Wn + 32 * WS, pi, h, acc_s, acc_g);
+        if (LC) lc_terms(LCIu, lcb, pi, h, acc_s, acc_g);   // LC_{l+1}: landed before this layer's halo barrier
       }
       FSTAMP(5);
       // 8. publish x_{l+1}: every wave drains its sc1 stores, barrier, one lane signals
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0 && l + 1 < a.L) publish_flag(a.flags + tile, (unsigned)(l + 1));
-      if (valid) store_rows16(a.Z + m * a.ldz + (long)l * a.Cd, z, a.Cd, h);  // skip GEMM input
-      if (X3 && a.SG && valid) {
-        float* sgl = a.SG + (long)l * a.sgls;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          *(floatx4*)(sgl + sg_off(m, q, h)) = floatx4{sgv[4 * q], sgv[4 * q + 1], sgv[4 * q + 2], sgv[4 * q + 3]};
-      }
-      FSTAMP(6);
-      // 9. image of layer l+2 into IMG[l&1] (everyone is past this layer's reads of it)
+      // 9. image of layer l+2 into IMG[l&1] (everyone is past this layer's reads of it; its loads
+      //    landed with the drain), and the LC image of layer l+2 (LC_{l+1} was read in step 7,
+      //    before the publish barrier)
+      if (LC && l + 2 < a.L) dma_lc_image(a.lcimg, l + 2, LCI, w, lane);
       if (l + 2 < a.L) {
         float* dst = IMG0 + (l & 1) * IMGF;
 #pragma unroll
@@ -683,6 +836,16 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
           const int e = tid + 256 * i;
           if (e < IMGF / 4) *(floatx4*)(dst + 4 * e) = pf[i];
         }
+      }
+      FSTAMP(6);
+      // 10. z (skip GEMM input) and σ rows, issued last: they drain in the shadow of the next
+      //     layer (written before the image, the image writes' vmcnt waits waited them out)
+      if (valid) store_rows16(a.Z + m * a.ldz + (long)l * a.Cd, z, a.Cd, h);
+      if (X3 && a.SG && valid) {
+        float* sgl = a.SG + (long)l * a.sgls;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *(floatx4*)(sgl + sg_off(m, q, h)) = floatx4{sgv[4 * q], sgv[4 * q + 1], sgv[4 * q + 2], sgv[4 * q + 3]};
       }
       FSTAMP(7);
     }
@@ -862,7 +1025,7 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
     const bool has_cond = a.gc_tab || a.cond;
     const int myid = (a.gc_tab && valid) ? a.ids[m] : 0;
     floatx4 cv[8];
-    load_cond(a, a.L - 1, myid, m, valid && has_cond, h, cv);
+    load_cond<2>(a, a.L - 1, myid, m, valid && has_cond, h, cv);
     // GC grads: is this wave's 32-position run one voice id?  (fast scatter path)
     const int wave_id = __shfl(myid, 0);
     const bool wave_uni = __all(!valid || myid == wave_id);
@@ -915,7 +1078,7 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
       // 1. recompute the gate (no cross-tile dependency)
       floatx16 acc_s, acc_g;
       conv_init(bs, cv, h, acc_s, acc_g);
-      if (has_cond && l > 0) load_cond(a, l - 1, myid, m, valid, h, cv);
+      if (has_cond && l > 0) load_cond<2>(a, l - 1, myid, m, valid, h, cv);
       conv_half(Xc + r * XS, Ws + 32 * WS, pi, h, acc_s, acc_g);
       if (l > 0) dma_rows(XpN, XcN, xnext, t0, dnext, a.T, a.H, w, lane, 2, 4);
       conv_half(Xp + r * XS, Ws, pi, h, acc_s, acc_g);
@@ -1219,14 +1382,18 @@ __global__ void pack_layers_bx3_kernel(const float* sig, const float* gate, cons
 // blocks after them (if skip_b) the skip GEMM's bias Σ_l skip_b[l] (l in order)
 __global__ void pack_layers_fb_x3_kernel(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                                          const float* res, const float* res_b, unsigned short* fout, float* bout,
-                                         int L, int Cr, int Cd, const float* skip_b, int Cs, float* bsum) {
+                                         int L, int Cr, int Cd, const float* skip_b, int Cs, float* bsum,
+                                         const float* lc_sig, const float* lc_gate, int Lo, unsigned short* lcout) {
   const int l = blockIdx.x;
+  const int nlc = lcout ? L : 0;
   if (l < L) {
     pack_x3_body(l, sig, gate, sig_b, gate_b, res, res_b, fout, Cr, Cd);
   } else if (l < 2 * L) {
     pack_bx3_body(l - L, sig, gate, res, bout, Cr, Cd);
+  } else if (l < 2 * L + nlc) {
+    pack_lc_x3_body(l - 2 * L, lc_sig, lc_gate, lcout, Lo, Cd);
   } else {
-    const int n = (l - 2 * L) * blockDim.x + threadIdx.x;
+    const int n = (l - 2 * L - nlc) * blockDim.x + threadIdx.x;
     if (n < Cs) {
       float s = 0.f;
 #pragma unroll 10
@@ -1277,22 +1444,6 @@ LBWN_DEV void gc_scatter_x3(float* gtab, long ld, const int* ids_b, const float*
   }
 }
 
-typedef __attribute__((address_space(3))) void lds_void;
-
-// One LDS-DMA piece (global_load_lds_dwordx4: 64 lanes × 16 B from per-lane addresses to
-// lds_dst + 16·lane) issued from inline asm, so the compiler neither knows the LDS it writes (no
-// conservative vmcnt(0) before every later LDS access) nor counts it: the kernel lands these
-// pieces itself with an explicit vmcnt(0) drain + barrier before their first reader.
-LBWN_DEV void dma16(const void* g, float* lds_dst) {
-  const unsigned base =
-      __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)lds_dst);
-  unsigned saved;   // m0 is reserved by the compiler: saved and restored around the piece
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %2, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(saved)
-               : "s"(base), "v"(g)
-               : "memory");
-}
-
 __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
   __shared__ __attribute__((aligned(16))) float sm[CBX_LDS];
   __shared__ int s_fail;
@@ -1323,6 +1474,11 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
     const int myid = (a.gc_tab && valid) ? a.ids[m] : 0;
     const int wave_id = __shfl(myid, 0);
     const bool wave_uni = __all(!valid || myid == wave_id);
+    // GC grads: a tile whose valid positions share one voice id (the common case: ids change only
+    // at file boundaries) adds the tile's dv column sums -- the bias partial sums, computed anyway --
+    // to that id's row: 64 atomics per layer instead of a per-wave pass over DV
+    const int tile_id = a.gc_tab ? a.ids[mb + t0] : 0;
+    const bool tile_uni = __syncthreads_and(!valid || myid == tile_id);
     // per-layer rows of this lane's position: dZ, z, σ (issued a layer ahead)
     floatx4 dzr[4], zr[4], sgr[4];
     auto load_regs = [&](int l) {
@@ -1505,7 +1661,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
       if (tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
       // the next layer's weight image and rows are issued between the dSIG MFMAs below (landed
       // by the next layer's G build: vmcnt(0) + barrier)
-      if (a.gc_dtab)
+      if (a.gc_dtab && !tile_uni)
         gc_scatter_x3(a.gc_dtab + (long)l * 64, a.gc_ld, a.ids + mb, DVs, DVg, t0, a.T, w, lane, 32,
                       wave_uni ? wave_id : -1);
       XSTAMP(4);
@@ -1607,6 +1763,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 #pragma unroll
         for (int pc = 0; pc < 8; ++pc) s1 += part[pc * 96 + tid];
         slab[5120 + tid] = s1;
+        if (a.gc_dtab && tile_uni && tid < 64) atomicAdd(a.gc_dtab + (long)tile_id * a.gc_ld + (long)l * 64 + tid, s1);
       }
       XSTAMP(12);
       // dSIG / dGATE: partial of tile t to slot (wave, t) of Xp..DVs (64 KiB, dead until the next
@@ -1953,6 +2110,8 @@ int lbwn_layer_dx_combine_launch(const float* out_a, const float* out_c0, float*
   return 0;
 }
 int lbwn_layer_image_x3_elems() { return XIMG_US; }
+int lbwn_lc_image_x3_elems() { return LCIMG_US; }
+int lbwn_lc_in_chain_ok(int Lo) { return Lo > 16 * (LC_K - 1) && Lo <= LC_KP && Lo % 4 == 0; }
 int lbwn_layer_image_bx3_floats() { return BIMG_F; }
 int lbwn_pack_layers_bx3_launch(const float* sig, const float* gate, const float* res, float* out, int L, int Cr,
                                 int Cd, hipStream_t st) {
@@ -1964,12 +2123,16 @@ int lbwn_pack_layers_bx3_launch(const float* sig, const float* gate, const float
 
 int lbwn_pack_layers_fb_x3_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                                   const float* res, const float* res_b, unsigned short* fout, float* bout, int L,
-                                  int Cr, int Cd, const float* skip_b, int Cs, float* bsum, hipStream_t st) {
+                                  int Cr, int Cd, const float* skip_b, int Cs, float* bsum, const float* lc_sig,
+                                  const float* lc_gate, int Lo, unsigned short* lcout, hipStream_t st) {
   LBWN_REQUIRE(Cr <= 32 && Cd <= 32 && (((uintptr_t)fout) & 15) == 0 && (((uintptr_t)bout) & 15) == 0,
                "pack_layers_fb_x3: bad arguments");
+  LBWN_REQUIRE(!lcout || (lc_sig && lc_gate && Lo >= 1 && Lo <= LC_KP && (((uintptr_t)lcout) & 15) == 0),
+               "pack_layers_fb_x3: bad LC image arguments");
   const int nsum = (skip_b && bsum) ? (Cs + 255) / 256 : 0;
-  pack_layers_fb_x3_kernel<<<2 * L + nsum, 256, 0, st>>>(sig, gate, sig_b, gate_b, res, res_b, fout, bout, L, Cr, Cd,
-                                                         skip_b, Cs, bsum);
+  const int nlc = lcout ? L : 0;
+  pack_layers_fb_x3_kernel<<<2 * L + nlc + nsum, 256, 0, st>>>(sig, gate, sig_b, gate_b, res, res_b, fout, bout, L, Cr,
+                                                               Cd, skip_b, Cs, bsum, lc_sig, lc_gate, Lo, lcout);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
@@ -2040,12 +2203,29 @@ int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   k.trace = c.trace; k.trace_blk = c.trace_blk;
   k.ximg = c.wpack_x3;
   k.SG = c.SG; k.sgls = c.sgls;
+  k.lcact = c.lcact; k.lcimg = c.lcimg; k.Lo = c.Lo;
   LBWN_REQUIRE(!c.wpack_x3 || (((uintptr_t)c.wpack_x3) & 15) == 0, "chain fwd: split images not 16-B aligned");
+  const bool lc = c.lcimg != nullptr;
+  if (lc)
+    LBWN_REQUIRE(c.wpack_x3 && c.lcact && !c.cond && c.Lo > 16 * (LC_K - 1) && c.Lo <= LC_KP && c.Lo % 4 == 0 &&
+                     (((uintptr_t)c.lcact) & 15) == 0 && (((uintptr_t)c.lcimg) & 15) == 0,
+                 "chain fwd: in-chain LC needs the split images, %d < n_lc_out <= %d, aligned rows", 16 * (LC_K - 1),
+                 LC_KP);
   const int tps = (c.T + LP - 1) / LP;
   // hand-off flags only: the status word is sticky for the whole step
   if (!c.flags_zeroed) LBWN_HIP(hipMemsetAsync(c.flags, 0, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st));
-  if (c.wpack_x3) chain_fwd_kernel<true><<<c.grid, 256, 0, st>>>(k);
-  else chain_fwd_kernel<false><<<c.grid, 256, 0, st>>>(k);
+  const int cm = (!c.gc_tab && !c.cond) ? 0 : (c.gc_tab && !c.cond) ? 1 : 2;
+  if (lc) {
+    if (cm == 0) chain_fwd_kernel<true, true, 0><<<c.grid, 256, 0, st>>>(k);
+    else chain_fwd_kernel<true, true, 1><<<c.grid, 256, 0, st>>>(k);   // lc: cond is null
+  } else if (c.wpack_x3) {
+    if (cm == 0) chain_fwd_kernel<true, false, 0><<<c.grid, 256, 0, st>>>(k);
+    else if (cm == 1) chain_fwd_kernel<true, false, 1><<<c.grid, 256, 0, st>>>(k);
+    else chain_fwd_kernel<true, false, 2><<<c.grid, 256, 0, st>>>(k);
+  } else {
+    if (cm == 0) chain_fwd_kernel<false, false, 0><<<c.grid, 256, 0, st>>>(k);
+    else chain_fwd_kernel<false, false, 2><<<c.grid, 256, 0, st>>>(k);
+  }
   LBWN_CHECK_LAUNCH();
   return 0;
 }

@@ -84,8 +84,7 @@ __global__ void shift_add_kernel(float* out, const float* a, const float* c0, in
 // no read-modify-write round trip); a single wave's atomics are applied in program and lane
 // order, the block's wave histograms are summed in wave order and the block partials are reduced
 // in a fixed order, so the sums are deterministic.  Default 256 one-wave blocks (32 KB of LDS
-// each, so they find room beside dSKIP's GEMM blocks; 128 x 1 and 256 x 2 measured slower);
-// LBWN_PG=<blocks>,<waves> selects up to PG_BLOCKS x PG_WAVES.
+// each, so they find room beside dSKIP's GEMM blocks; 128 x 1 and 256 x 2 measured slower).
 constexpr int PG_BLOCKS = 256;
 constexpr int PG_WAVES = 2;
 constexpr int PG_BATCH = 32;
@@ -334,9 +333,12 @@ __global__ void fill_kernel(float* p, float v, long n) {
 // grads hold Σ-xent gradients; g = raw·(1/n_valid) + l2·θ for the weight region
 // [0, n_weights) (non-BIAS vars, tmodel.py:250-261); biases get no l2 term.
 // counters[2] (int64) is Adam's apply count t-1; lr_t = lr·√(1-β2^t)/(1-β1^t).
+// status (nullable): the step's chain status word; nonzero = a hand-off timed out and the
+// gradients are garbage, so the update is skipped (params, m, v untouched).
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ gr, float* __restrict__ m,
                             float* __restrict__ v, long nw, long n, float lr, float b1, float b2, float eps,
-                            float l2, const float* stats, const long long* counters) {
+                            float l2, const float* stats, const long long* counters, const unsigned* status) {
+  if (status && *status) return;
   const double t = (double)(counters[2] + 1);
   const float lr_t = (float)((double)lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t)));
   const float inv = stats ? (stats[1] > 0.f ? 1.f / stats[1] : 0.f) : 1.f;
@@ -352,9 +354,16 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ gr,
   }
 }
 
-// counters: [0] GLOBAL_STEP, [1] VALID_SAMPLES, [2] Adam t-1 (tmodel.py:282-287)
-__global__ void counters_kernel(long long* counters, const float* stats, int adam_applied) {
+// counters: [0] GLOBAL_STEP, [1] VALID_SAMPLES, [2] Adam t-1 (tmodel.py:282-287), [3] the
+// cumulative status: every step's status word ORed in (never reset by a step), so one read
+// after many steps tells whether any of them timed out.  A failed step advances nothing else.
+__global__ void counters_kernel(long long* counters, const float* stats, int adam_applied, const unsigned* status) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const unsigned s = status ? *status : 0u;
+    if (s) {
+      counters[3] |= (long long)s;
+      return;
+    }
     counters[0] += 1;
     counters[1] += (long long)stats[1];
     counters[2] += adam_applied;
@@ -424,18 +433,7 @@ int lbwn_pre_grad_ws_floats(int Q, int Cr) { return PG_BLOCKS * (Q * Cr + Cr); }
 int lbwn_pre_grad_launch(const int* q, const float* g, const float* dprev, int gd, int B, int T, int Cr, int Q,
                          float* dpre, float* dpre_b, float* ws, hipStream_t st) {
   LBWN_REQUIRE(Cr >= 1 && Cr <= 32 && Q >= 1 && Q * 32 * 4 <= 65536, "pre_grad: Cr <= 32 and Q <= 512 required");
-  // LBWN_PG=<blocks>,<waves> overrides the shape (blocks <= PG_BLOCKS, waves <= PG_WAVES)
-  static int cfg_blocks = -1, cfg_waves = -1;
-  if (cfg_blocks < 0) {
-    cfg_blocks = PG_BLOCKS; cfg_waves = 1;
-    if (const char* env = getenv("LBWN_PG")) {
-      int b = 0, w = 0;
-      if (sscanf(env, "%d,%d", &b, &w) == 2 && b >= 1 && b <= PG_BLOCKS && w >= 1 && w <= PG_WAVES) {
-        cfg_blocks = b; cfg_waves = w;
-      }
-    }
-  }
-  const int nb = cfg_blocks, nw = cfg_waves * Q * 32 * 4 <= 65536 ? cfg_waves : 1;
+  const int nb = PG_BLOCKS, nw = 1;   // one-wave blocks (two-wave blocks wait for LDS)
   float* part = ws;
   float* bpart = ws + (long)PG_BLOCKS * Q * Cr;
   pre_grad_part_kernel<<<nb, 64 * nw, nw * Q * 32 * 4, st>>>(q, g, dprev, gd, B, T, Cr, Q, part, bpart);
@@ -540,16 +538,17 @@ int lbwn_fill_launch(float* p, float v, long n, hipStream_t st) {
 }
 
 int lbwn_adam_launch2(float* params, const float* grads, float* m, float* v, long nw, long n, float lr, float b1,
-                      float b2, float eps, float l2, const float* stats, const long long* counters,
+                      float b2, float eps, float l2, const float* stats, const long long* counters, const unsigned* status,
                       hipStream_t st) {
   adam_kernel<<<grid_for(n, 256, 4096), 256, 0, st>>>(params, grads, m, v, nw, n, lr, b1, b2, eps, l2, stats,
-                                                      counters);
+                                                      counters, status);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
 
-int lbwn_counters_launch(long long* counters, const float* stats, int adam_applied, hipStream_t st) {
-  counters_kernel<<<1, 64, 0, st>>>(counters, stats, adam_applied);
+int lbwn_counters_launch(long long* counters, const float* stats, int adam_applied, const unsigned* status,
+                         hipStream_t st) {
+  counters_kernel<<<1, 64, 0, st>>>(counters, stats, adam_applied, status);
   LBWN_CHECK_LAUNCH();
   return 0;
 }

@@ -12,7 +12,7 @@ import torch  # noqa: F401  (must precede the .so: shared HIP runtime)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('LBWN_LIB') or os.path.join(HERE, 'liblbwn.so')   # LBWN_LIB: timing-variant builds
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 c_int, c_int64, c_float, c_void_p, c_size_t = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 c_fp = ctypes.c_void_p   # device pointers are passed as integers
@@ -44,12 +44,13 @@ _SIGS = {
     'lbwn_plan_destroy': (None, [c_void_p]),
     'lbwn_plan_workspace_bytes': (c_size_t, [c_void_p]),
     'lbwn_plan_probe': (c_int, [c_void_p, ctypes.c_char_p, c_void_p, c_void_p]),
+    'lbwn_plan_stream_wait': (c_int, [c_void_p, ctypes.c_char_p, c_void_p, ctypes.POINTER(c_int)]),
     'lbwn_plan_tensor': (c_int, [c_void_p, ctypes.c_char_p, ctypes.POINTER(c_size_t), ctypes.POINTER(c_size_t)]),
     'lbwn_train_forward': (c_int, [c_void_p, ctypes.POINTER(Params), c_fp, c_fp, c_fp, c_fp, c_fp, c_fp, c_void_p]),
     'lbwn_train_backward': (c_int, [c_void_p, ctypes.POINTER(Params), ctypes.POINTER(Params), c_fp, c_fp, c_fp,
                                     c_fp, c_void_p]),
     'lbwn_adam_tf1': (c_int, [c_fp, c_fp, c_fp, c_fp, c_int64, c_int64, c_float, c_float, c_float, c_float,
-                              c_float, c_fp, c_fp, c_void_p]),
+                              c_float, c_fp, c_fp, c_fp, c_void_p]),
     'lbwn_gen_plan_create': (c_int, [ctypes.POINTER(Arch), c_int, c_int64, c_int64, ctypes.POINTER(c_void_p)]),
     'lbwn_gen_plan_destroy': (None, [c_void_p]),
     'lbwn_gen_workspace_bytes': (c_size_t, [c_void_p]),

@@ -30,26 +30,66 @@ class DPContext:
             dist.broadcast(net.flat, 0)
 
     def reduce_grads(self, net):
-        """Σ over ranks of the raw gradient buffer and of (Σxent, n_valid, Σ|argmax diff|).
-        stats and grads go as ONE flat message (6–8 MB for arch3/arch5: a single ring
-        all_reduce is ≤0.1 ms on xGMI, so no bucketing is needed at this size)."""
+        """Σ over ranks of the raw gradient buffer, of (Σxent, n_valid, Σ|argmax diff|) and of
+        the step status words (a timed-out chain on ANY rank makes every rank's optimizer skip
+        the step on the device, so no rank applies garbage gradients).
+
+        Two buckets, each ONE message (a staging copy of its flat ranges):
+          0 "head": POST1, POST2, their biases, SKIP_BIAS + the stats + the status word — final
+            once the backward chain has completed (lbwn_plan_stream_wait "head_grads"), so its
+            all-reduce runs on a side stream beside the backward's tail (dSKIP, the slab
+            reduction, dPRE, the conditioning grads);
+          1 "rest": every other gradient, after the whole backward.
+        No collective ever overlaps a persistent chain launch: bucket 0 starts after the backward
+        chain, and the current stream waits for both buckets before the optimizer (hence before
+        the next step's forward chain).  A chain's tiles assume every block of a round is resident
+        (DESIGN §4): an RCCL kernel holding CUs during a chain launch would stall its lock-step
+        hand-offs."""
+        if not self.enabled:
+            return
+        plan = _Buckets.of(net)
+        if not net.grad_flat.is_cuda:   # gloo (CPU tests): the same buckets, in order
+            for k in range(2):
+                plan.pack(k, net)
+                dist.all_reduce(plan.buf[k])
+                plan.unpack(k, net)
+            return
+        main = torch.cuda.current_stream(net.grad_flat.device)
+        comm = self._comm_stream(net.grad_flat.device)
+        if not net.wait_point('head_grads', comm):
+            comm.wait_stream(main)
+        with torch.cuda.stream(comm):
+            plan.pack(0, net)
+            dist.all_reduce(plan.buf[0])
+            plan.unpack(0, net)
+        comm.wait_stream(main)
+        with torch.cuda.stream(comm):
+            plan.pack(1, net)
+            dist.all_reduce(plan.buf[1])
+            plan.unpack(1, net)
+        main.wait_stream(comm)
+
+    def reduce_grads_flat(self, net):
+        """The whole gradient + stats + status as one message after the backward (the reference
+        bucketing of tests/test_dropin.py::test_dp_bucketed_equals_flat)."""
         if not self.enabled:
             return
         n = net.grad_flat.numel()
-        buf = self._buf(net)
+        buf = torch.empty(n + 4, dtype=torch.float32, device=net.grad_flat.device)
+        sw = net.status_word()
         buf[:n].copy_(net.grad_flat)
         buf[n:n + 3].copy_(net.stats[:3])
+        buf[n + 3:n + 4].copy_(sw)
         dist.all_reduce(buf)
         net.grad_flat.copy_(buf[:n])
         net.stats[:3].copy_(buf[n:n + 3])
+        sw.copy_(buf[n + 3:n + 4])
 
-    def _buf(self, net):
-        key = '_dp_buf'
-        b = getattr(net, key, None)
-        if b is None or b.numel() != net.grad_flat.numel() + 4:
-            b = torch.empty(net.grad_flat.numel() + 4, dtype=torch.float32, device=net.grad_flat.device)
-            setattr(net, key, b)
-        return b
+    def _comm_stream(self, device):
+        s = getattr(self, '_comm', None)
+        if s is None:
+            s = self._comm = torch.cuda.Stream(device=device)
+        return s
 
     def max_over_ranks(self, value, device):
         if not self.enabled:
@@ -61,6 +101,50 @@ class DPContext:
     def barrier(self):
         if self.enabled:
             dist.barrier()
+
+
+class _Buckets:
+    """Flat ranges of the two all-reduce buckets (lbwn.arch.ParamLayout: weights
+    [pre, sig, gate, res, skip, gc.., lc.., post1, post2] then biases [pre_b, sig_b, gate_b,
+    res_b, skip_b, post1_b, post2_b]) and their staging buffers."""
+
+    def __init__(self, net):
+        lay = net.layout
+        kb = lay.kind_base
+        head = [(kb['post1'], lay.n_weights)]
+        rest = [(0, kb['post1'])]
+        if 'skip_b' in kb:
+            head.append((kb['skip_b'], lay.n_total))
+            rest.append((lay.n_weights, kb['skip_b']))
+        self.ranges = [head, rest]
+        sizes = [sum(b - a for a, b in head) + 4, sum(b - a for a, b in rest)]
+        self.buf = [torch.empty(n, dtype=torch.float32, device=net.grad_flat.device) for n in sizes]
+
+    @staticmethod
+    def of(net):
+        b = getattr(net, '_dp_buckets', None)
+        if b is None or b.buf[0].device != net.grad_flat.device:
+            b = _Buckets(net)
+            net._dp_buckets = b
+        return b
+
+    def pack(self, k, net):
+        o = 0
+        for a, b in self.ranges[k]:
+            self.buf[k][o:o + b - a].copy_(net.grad_flat[a:b])
+            o += b - a
+        if k == 0:
+            self.buf[0][o:o + 3].copy_(net.stats[:3])
+            self.buf[0][o + 3:o + 4].copy_(net.status_word())
+
+    def unpack(self, k, net):
+        o = 0
+        for a, b in self.ranges[k]:
+            net.grad_flat[a:b].copy_(self.buf[k][o:o + b - a])
+            o += b - a
+        if k == 0:
+            net.stats[:3].copy_(self.buf[0][o:o + 3])
+            net.status_word().copy_(self.buf[0][o + 3:o + 4])
 
 
 def init(backend=None, device_type='cuda'):

@@ -93,7 +93,7 @@ class WaveNetGen:
 
     @property
     def persistent(self):
-        """True when the plan runs each gen_run as one persistent launch (B <= 32)."""
+        """True when the plan runs each gen_run as one persistent launch (B <= 16)."""
         return bool(self._plan is not None and self.lib.lbwn_gen_is_persistent(self._plan))
 
     def tensor(self, name, dtype=torch.float32):

@@ -7,7 +7,9 @@ from . import _lib
 class AdamOptimizer:
     """TF1 Adam: lr_t = lr·√(1-β2^t)/(1-β1^t); m = β1m+(1-β1)g; v = β2v+(1-β2)g²;
     θ -= lr_t·m/(√v+ε).  g = Σxent-grad/n_valid + l2_factor·θ (non-BIAS), applied by ONE
-    kernel (lbwn_adam_tf1) that also advances GLOBAL_STEP / VALID_SAMPLES."""
+    kernel (lbwn_adam_tf1) that also advances GLOBAL_STEP / VALID_SAMPLES.  The step's plan
+    status word goes with it: a step whose chain hand-off timed out is skipped on the device
+    and recorded in the cumulative status (WaveNetTrain.check_status), with no host sync."""
 
     def __init__(self, learning_rate=0.001, beta1=0.9, beta2=0.999, epsilon=1e-8):
         self.lr, self.b1, self.b2, self.eps = float(learning_rate), float(beta1), float(beta2), float(epsilon)
@@ -28,7 +30,7 @@ class AdamOptimizer:
         _lib.check(net.lib.lbwn_adam_tf1(net.flat.data_ptr(), net.grad_flat.data_ptr(), m.data_ptr(), v.data_ptr(),
                                          net.layout.n_weights, net.layout.n_total, self.lr, self.b1, self.b2,
                                          self.eps, net.l2_factor, net.stats.data_ptr(), net.counters.data_ptr(),
-                                         _lib.stream_ptr(stream)))
+                                         net.status_ptr(), _lib.stream_ptr(stream)))
         net.global_step_host += 1
 
     # ---- checkpoint state: TF's slot names (<var>/Adam = m, <var>/Adam_1 = v) ----------------

@@ -7,8 +7,7 @@ HIP launches on the current torch stream.  The reference's TF-eager flow (train.
     grads_and_vars, loss = net.build(wav_input, mel_input, id_mask)
     optimizer.apply_gradients(grads_and_vars)
 
-is reproduced literally (lbwn.optim.AdamOptimizer).  ``train_step`` is the fused fast path
-(optionally hipGraph-captured).
+is reproduced literally (lbwn.optim.AdamOptimizer).
 """
 import ctypes
 import sys
@@ -66,7 +65,7 @@ class WaveNetTrain:
         self.grad_flat = torch.zeros_like(self.flat)
         self.save_flat = torch.zeros(n_save, dtype=torch.float32, device=dev)
         self.stats = torch.zeros(4, dtype=torch.float32, device=dev)
-        self.counters = torch.zeros(4, dtype=torch.int64, device=dev)   # GLOBAL_STEP, VALID_SAMPLES, adam t-1
+        self.counters = torch.zeros(4, dtype=torch.int64, device=dev)   # GLOBAL_STEP, VALID_SAMPLES, adam t-1, status
         self.vars = self.layout.views(self.flat)
         self.grads = self.layout.views(self.grad_flat)
         self.save_vars = OrderedDict((n, self.save_flat[o:o + int(np.prod(s))].view(*s))
@@ -76,6 +75,8 @@ class WaveNetTrain:
         self._grads_c = self._make_params_struct(self.grad_flat)
         self._plans = {}
         self._ws = None
+        self._last = None
+        self._sp_cache = None
         self.init_vars(seed)
         self.global_step_host = 0    # host mirror of GLOBAL_STEP (advanced by the optimizer)
         # checkpoint surface (ckpt.py:13-81; the saveables are self.vars, tmodel.py:330)
@@ -194,17 +195,43 @@ class WaveNetTrain:
                                                     _lib.ptr(mel), sp))
         return self.stats
 
-    def status(self, T=None):
-        """The plan's sticky status word for the last step (synchronises): 0 = ok; bit 0 =
-        a forward-chain hand-off timed out, bit 1 = a backward-chain one (the step's
-        outputs are then garbage and must not be applied)."""
+    def status_word(self, T=None):
+        """int32 view of the plan's per-step status word (zeroed at each forward; the chains
+        OR their timeout codes in: bit 0 forward chain, bit 1 backward chain)."""
         T = T if T is not None else self._last[0].shape[1]
-        return int(self.plan_tensor(T, 'status')[:1].view(torch.int32).item())
+        return self.plan_tensor(T, 'status')[:1].view(torch.int32)
+
+    def status_ptr(self):
+        """Device pointer of the last step's status word (None before any step)."""
+        if self._last is None:
+            return None
+        key = (self._last[0].shape[1], self._ws.data_ptr())
+        if self._sp_cache is None or self._sp_cache[0] != key:
+            self._sp_cache = (key, self.status_word().data_ptr())
+        return self._sp_cache[1]
+
+    def wait_point(self, point, stream):
+        """Make a torch stream wait for a point of the last backward (lbwn_plan_stream_wait);
+        False if the plan has no such point."""
+        if self._last is None:
+            return False
+        waited = ctypes.c_int(0)
+        _lib.check(self.lib.lbwn_plan_stream_wait(self._plan(self._last[0].shape[1]), point.encode(),
+                                                  stream.cuda_stream, ctypes.byref(waited)))
+        return bool(waited.value)
+
+    def status(self, T=None):
+        """Cumulative status (synchronises): every applied step's status word is ORed into
+        counters[3] by the optimizer kernel (which skips a failed step's update on the
+        device), plus the current step's word for a step not yet applied.  0 = ok; bit 0 = a
+        forward-chain hand-off timed out, bit 1 = a backward-chain one."""
+        return int(self.counters[3].item()) | int(self.status_word(T).item())
 
     def check_status(self, T=None):
         st = self.status(T)
         if st:
-            raise RuntimeError('lbwn: chain hand-off timed out (status word %#x): the last step is invalid' % st)
+            raise RuntimeError('lbwn: chain hand-off timed out (status word %#x): the failed steps were '
+                               'not applied' % st)
 
     def l2_loss(self):
         """tmodel.py:250-261: Σ_{trainable, non-BIAS} Σv²/2 (the weight region of the flat buffer)."""

@@ -42,22 +42,33 @@ def _check_inputs(x_halo, w_sig, dilation, H):
     return B, HT - H, Cr, w_sig.shape[2]
 
 
+def _same_device(*ts):
+    dev = ts[0].device
+    for t in ts[1:]:
+        if t.device != dev:
+            raise ValueError('lbwn::dilconv_gate: all tensors must be on one device (%s vs %s)' % (dev, t.device))
+
+
 @torch.library.custom_op('lbwn::dilconv_gate', mutates_args=(), device_types='cuda')
 def dilconv_gate(x_halo: torch.Tensor, w_sig: torch.Tensor, w_gate: torch.Tensor, b_sig: torch.Tensor,
                  b_gate: torch.Tensor, w_res: torch.Tensor, b_res: torch.Tensor, dilation: int,
                  H: int) -> Tuple[torch.Tensor, torch.Tensor]:
     """Returns (z [B][T][n_dil], x_out [B][T][n_res] = x + z·RES + b_res)."""
     B, T, Cr, Cd = _check_inputs(x_halo, w_sig, dilation, H)
+    _same_device(x_halo, w_sig, w_gate, b_sig, b_gate, w_res, b_res)
     lib = _lib_loaded()
-    x_halo = x_halo.contiguous()
-    z = torch.empty(B, T, Cd, dtype=torch.float32, device=x_halo.device)
-    xo = torch.empty(B, H + T, Cr, dtype=torch.float32, device=x_halo.device)
-    ws = torch.empty(lib.lbwn_layer_image_floats_abi() + 16, dtype=torch.float32, device=x_halo.device)
-    args = [t.contiguous() for t in (w_sig, w_gate, b_sig, b_gate, w_res, b_res)]
-    _lib.check(lib.lbwn_layer_forward(x_halo.data_ptr(), xo.data_ptr(), z.data_ptr(), Cd,
-                                      *[t.data_ptr() for t in args], None, None, None, 0,
-                                      B, T, H, dilation, Cr, Cd, ws.data_ptr(), _lib.stream_ptr()))
-    return z, xo[:, H:].contiguous()
+    dev = x_halo.device
+    with torch.cuda.device(dev):   # the kernels launch on the tensors' device and its current stream
+        x_halo = x_halo.contiguous()
+        z = torch.empty(B, T, Cd, dtype=torch.float32, device=dev)
+        xo = torch.empty(B, H + T, Cr, dtype=torch.float32, device=dev)
+        ws = torch.empty(lib.lbwn_layer_image_floats_abi() + 16, dtype=torch.float32, device=dev)
+        args = [t.contiguous() for t in (w_sig, w_gate, b_sig, b_gate, w_res, b_res)]
+        _lib.check(lib.lbwn_layer_forward(x_halo.data_ptr(), xo.data_ptr(), z.data_ptr(), Cd,
+                                          *[t.data_ptr() for t in args], None, None, None, 0,
+                                          B, T, H, dilation, Cr, Cd, ws.data_ptr(),
+                                          torch.cuda.current_stream(dev).cuda_stream))
+        return z, xo[:, H:].contiguous()
 
 
 @dilconv_gate.register_fake
@@ -74,18 +85,21 @@ def dilconv_gate_bwd(dz: torch.Tensor, dx_out: torch.Tensor, x_halo: torch.Tenso
                                                                           torch.Tensor]:
     """lbwn_layer_backward: (dx_halo, dw_sig, dw_gate, db_sig, db_gate, dw_res, db_res)."""
     B, T, Cr, Cd = _check_inputs(x_halo, w_sig, dilation, H)
+    _same_device(dz, dx_out, x_halo, w_sig, w_gate, b_sig, b_gate, w_res, b_res)
     lib = _lib_loaded()
     dev = x_halo.device
     f32 = dict(dtype=torch.float32, device=dev)
-    ws = torch.empty(int(lib.lbwn_layer_backward_ws_floats(B, T, Cr)), **f32)
-    dxh = torch.empty(B, H + T, Cr, **f32)
-    g = [torch.empty_like(t) for t in (w_sig, w_gate, b_sig, b_gate, w_res, b_res)]
-    args = [t.contiguous() for t in (w_sig, w_gate, b_sig, b_gate, w_res, b_res)]
-    _lib.check(lib.lbwn_layer_backward(x_halo.contiguous().data_ptr(), dz.contiguous().data_ptr(), Cd,
-                                       dx_out.contiguous().data_ptr(), *[t.data_ptr() for t in args],
-                                       None, None, None, 0, dxh.data_ptr(), *[t.data_ptr() for t in g],
-                                       None, 0, None, B, T, H, dilation, Cr, Cd, ws.data_ptr(), _lib.stream_ptr()))
-    return (dxh, *g)
+    with torch.cuda.device(dev):   # the kernels launch on the tensors' device and its current stream
+        ws = torch.empty(int(lib.lbwn_layer_backward_ws_floats(B, T, Cr)), **f32)
+        dxh = torch.empty(B, H + T, Cr, **f32)
+        g = [torch.empty_like(t) for t in (w_sig, w_gate, b_sig, b_gate, w_res, b_res)]
+        args = [t.contiguous() for t in (w_sig, w_gate, b_sig, b_gate, w_res, b_res)]
+        _lib.check(lib.lbwn_layer_backward(x_halo.contiguous().data_ptr(), dz.contiguous().data_ptr(), Cd,
+                                           dx_out.contiguous().data_ptr(), *[t.data_ptr() for t in args],
+                                           None, None, None, 0, dxh.data_ptr(), *[t.data_ptr() for t in g],
+                                           None, 0, None, B, T, H, dilation, Cr, Cd, ws.data_ptr(),
+                                           torch.cuda.current_stream(dev).cuda_stream))
+        return (dxh, *g)
 
 
 @dilconv_gate_bwd.register_fake

@@ -159,7 +159,7 @@ def main(argv=None):
         net.forward(wav_input, mel_input, id_mask, backward=True)
         dp.reduce_grads(net)
         if args.progress_interval and net.global_step_host % args.progress_interval == 0:
-            net.check_status()                # a chain hand-off timeout invalidates the step
+            net.check_status()                # cumulative: any timed-out step since the start (never applied)
         net.maybe_print()                     # tmodel.py:272-281 prints before the step counters advance
         optimizer.apply(net)
         if step % args.save_interval == 0 and step != args.resume_step:

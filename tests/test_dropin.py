@@ -183,9 +183,14 @@ def test_train_cli_errors(tmp_path, monkeypatch):
 # ---- data parallel over gloo, world_size 2 -----------------------------------------------------
 
 class _FakeNet:
-    def __init__(self, grads, stats):
+    def __init__(self, grads, stats, layout, status=0):
         self.grad_flat = grads
         self.stats = stats
+        self.layout = layout
+        self._status = torch.tensor([status], dtype=torch.int32)
+
+    def status_word(self):
+        return self._status
 
 
 def _dp_worker(rank, world, port, q_np, ids_np, out_path):
@@ -211,7 +216,7 @@ def _dp_worker(rank, world, port, q_np, ids_np, out_path):
     for n, e in lay.entries.items():       # raw Σ-xent gradient, as the device buffer holds it
         flat[e.offset:e.offset + e.numel] = (G[n] * st['n_valid']).reshape(-1)
     net = _FakeNet(torch.tensor(flat, dtype=torch.float32),
-                   torch.tensor([st['mean_xent'] * st['n_valid'], st['n_valid'], 0.0, 0.0], dtype=torch.float32))
+                   torch.tensor([st['mean_xent'] * st['n_valid'], st['n_valid'], 0.0, 0.0], dtype=torch.float32), lay)
     dp.reduce_grads(net)
     if rank == 0:
         np.savez(out_path, grads=net.grad_flat.numpy(), stats=net.stats.numpy())
@@ -246,6 +251,43 @@ def test_dp_gloo_two_ranks_equals_single_process(tmp_path):
     for n, e in lay.entries.items():   # Adam divides the summed raw grads by the GLOBAL n_valid
         np.testing.assert_allclose(got['grads'][e.offset:e.offset + e.numel] / got['stats'][1], G[n].reshape(-1),
                                    rtol=2e-4, atol=1e-7, err_msg=n)
+
+
+def _bucket_worker(rank, world, port, out_path):
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, 'lb-wavenet_amd'))
+    from lbwn.dist import DPContext
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    dp = DPContext(world, rank, rank)
+    lay = ParamLayout(load_arch(os.path.join(ROOT, 'par', 'arch5.json')))
+    g = torch.Generator().manual_seed(100 + rank)
+    grads = torch.randn(lay.n_total, generator=g) * 10.0 ** torch.randint(-6, 4, (lay.n_total,), generator=g)
+    stats = torch.tensor([123.25 + rank, 1000.0 + rank, 7.0 * rank, 0.5])
+    a = _FakeNet(grads.clone(), stats.clone(), lay, status=2 * rank)
+    b = _FakeNet(grads.clone(), stats.clone(), lay, status=2 * rank)
+    dp.reduce_grads(a)          # two buckets (head / rest)
+    dp.reduce_grads_flat(b)     # one message
+    if rank == 0:
+        np.savez(out_path, ga=a.grad_flat.numpy(), gb=b.grad_flat.numpy(), sa=a.stats.numpy(), sb=b.stats.numpy(),
+                 wa=a.status_word().numpy(), wb=b.status_word().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_bucketed_equals_flat(tmp_path):
+    """The two-bucket all-reduce (lbwn.dist: head bucket beside the backward's tail, the rest
+    after it) gives bitwise the flat one-message result, for the gradient, the loss stats and
+    the status word (any rank's timeout reaches every rank), over 2 gloo ranks at arch5's
+    layout (GC + LC kinds included)."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / 'bk.npz')
+    port = 29500 + (os.getpid() + 13) % 1000
+    mp.spawn(_bucket_worker, args=(2, port, out), nprocs=2, join=True)
+    r = np.load(out)
+    assert np.array_equal(r['ga'].view(np.uint32), r['gb'].view(np.uint32))
+    assert np.array_equal(r['sa'][:3], r['sb'][:3])
+    assert int(r['wa'][0]) == int(r['wb'][0]) == 2
 
 
 def _ckpt_worker(rank, world, port, path):

@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(params=['persistent', 'per_step'])
 def form(request, monkeypatch):
-    """Both execution forms: the persistent one-launch kernel (default for B <= 32) and the
+    """Both execution forms: the persistent one-launch kernel (default for B <= 16) and the
     per-step launches (LBWN_GEN_PERSIST=0, the form every B > 32 runs)."""
     if request.param == 'per_step':
         monkeypatch.setenv('LBWN_GEN_PERSIST', '0')

@@ -29,7 +29,7 @@ for i in range(6):
 allr = np.median(np.array(runs), axis=0).astype(np.int64)
 fw = allr[0]
 fnames = ['image prefetch issue', 'producer wait', 'halo loads + bar', 'dilated conv + gate',
-          'residual + next own tap', 'drain + bar + publish + z', 'image write']
+          'residual + next own tap', 'drain + bar + publish + image', 'z / sigma store issue']
 fseg = np.diff(fw[:, :8], axis=1)
 fmed = np.median(fseg[1:-1], axis=0)
 ftot = np.median(fw[:, 7] - fw[:, 0])
