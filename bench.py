@@ -52,6 +52,30 @@ def chain_ceiling(name, arch, x3):
     return X3_PEAK
 
 
+def chain_fwd_latency_floor(arch, B, T, clock_ghz=2.4, ncu=256):
+    """Latency floor of the persistent forward chain (chain_fwd_kernel): per layer the
+    cross-tile dependency runs producer's x_{l+1} stores -> drain -> flag -> consumer poll -> halo
+    loads -> dilated tap -> gate -> residual -> stores, at MI355X_MICROARCH.md's constants:
+      * sc1 store drain 332 cyc ('L2-warm vmcnt(N) drain 156 -> 332 cyc'), one-way flag 0.3 us
+        (price table 'handoff-flag': 0.3-0.6 idle), halo payload read ~500 cyc (4 b128 loads per
+        lane from L2: 'global_load L2-hit latency ~180-225 cyc' + the in-order drain), two
+        workgroup barriers (20 cyc each, taken) and the halo LDS write/read (2 x 50);
+      * the dilated tap: 2 k-steps x 2 (sig, gate) x 6 split products = 24 v_mfma_f32_32x32x16_bf16
+        at 32 cyc; the residual 12 of them; the gate 16 x (exp, rcp, exp, rcp) at 8 cyc issue
+        + 6 VALU at 4 = 16 x 56; splitting z into bf16 terms 16 x 22 cyc (5.5 VALU each).
+    Rounds: tiles beyond one per CU run as further rounds of the whole chain."""
+    from lbwn.arch import n_layers
+    L = n_layers(arch)
+    handoff = 332 + 0.3 * clock_ghz * 1e3 + 500 + 2 * 20 + 2 * 50
+    compute = 24 * 32 + 12 * 32 + 16 * 56 + 16 * 22
+    layer = handoff + compute
+    tiles = B * ((T + 127) // 128)
+    rounds = (tiles + ncu - 1) // ncu
+    return {'layer_cycles': round(layer), 'handoff_cycles': round(handoff), 'compute_cycles': compute,
+            'layers': L, 'rounds': rounds, 'launch_us': rounds * L * layer / (clock_ghz * 1e3),
+            'clock_ghz': clock_ghz}
+
+
 def kernel_work(name, arch, M):
     """Algorithmic work per launch."""
     from lbwn.arch import n_layers
@@ -111,6 +135,12 @@ def _gen(net, arch, B, chunk, max_steps, env=None):
                 os.environ[k] = v
 
 
+def _gen_form(g, B):
+    if g.persistent:
+        return 'persistent (one launch per chunk)'
+    return 'per-step, head as MFMA GEMMs' if B > 16 else 'per-step, head as vector GEMVs'
+
+
 def _gen_rate(g, arch, B, n, chunk):
     """wall time of n steps (graph replay of chunk-step runs), after a warm chunk."""
     import torch
@@ -144,6 +174,30 @@ def gen_layer_latency(net, arch, B):
     return float(np.median(lay))
 
 
+def gen_latency_floor(arch, clock_ghz=2.4):
+    """Latency floor of one cached-generation step (imodel.py:214-272) for this design (one CU
+    per stream, the layer chain's dependent instructions on the critical path, three hand-offs to
+    and from the head), from MI355X_MICROARCH.md's constants:
+      * ds_read issue -> use 50 cyc (cycle table, 'ds_read_b32 latency'); a write made visible to
+        the other waves = its lgkmcnt drain (taken as 50) + s_barrier (taken as 20: one 4-wave
+        workgroup; the guide prices only grid barriers);
+      * dependent v_fma_f32 4 cyc ('Dependent-chain latency'); v_exp_f32 / v_rcp_f32 8 cyc
+        ('vector-instruction ISSUE cost'); a DPP / permlane step 8 cyc (one VALU + its nop);
+      * a granule hand-off 0.8 us (price table 'handoff-1to1', idle, 8 B).
+    Per layer: x and z LDS reads (2 x 50), two write->barrier hops (2 x 70), the conv dot chain (two
+    4-wide dot4 per lane: 8 dependent FMA + 1 add = 36), two DPP reduction steps + bias + the
+    gate pairing (2 x 12 + 4 + 8 = 36), tanh/sigmoid (mul, exp, add, rcp, fma, then z = t*s: 32),
+    the residual dot chain (8 FMA + add: 36) and its permlane32 half-swap + adds (24).
+    Per step: + three hand-offs (chain -> head skip columns, skip all-gather, partial logits ->
+    draw) and the draw's wave scans (~30 dependent DPP steps: 240 cyc)."""
+    from lbwn.arch import n_layers
+    L = n_layers(arch)
+    layer_cyc = 2 * 50 + 2 * (50 + 20) + 36 + 36 + 32 + 36 + 24
+    step_us = L * layer_cyc / (clock_ghz * 1e3) + 3 * 0.8 + 240 / (clock_ghz * 1e3)
+    return {'layer_cycles': layer_cyc, 'layer_us': layer_cyc / (clock_ghz * 1e3), 'layers': L,
+            'handoffs': 3, 'handoff_us': 0.8, 'step_us': step_us, 'clock_ghz': clock_ghz}
+
+
 def bench_gen(net, arch, B=10, seconds=3.0, sr=16000, chunk=1000, sweep=(16, 64, 256)):
     """imodel.py cached generation, arch3, B=10, 3 s @ 16 kHz (BASELINE configs[2]), graph
     replay of chunk-sized step sequences; weights = the benchmark net's.  Also a B sweep and
@@ -156,19 +210,19 @@ def bench_gen(net, arch, B=10, seconds=3.0, sr=16000, chunk=1000, sweep=(16, 64,
     bps = gen_bytes_per_step(arch, B)
     out = {'metric': 'cached autoregressive gen audio samples/s (B streams x steps / wall)',
            'value': B * n / dt, 'unit': 'audio samples/s', 'steps': n, 'batch': B, 'wall_s': dt,
-           'us_per_step': us, 'form': 'persistent (one launch per chunk)' if g.persistent else 'per-step launches',
+           'us_per_step': us, 'form': _gen_form(g, B),
            'config': 'imodel.py cached gen, par/arch3.json, B=%d, %.0f s @ %d Hz, chunk %d, hipGraph replay'
                      % (B, seconds, sr, chunk)}
     # latency roofline: a step is L dependent layers (conv -> gate -> residual on one CU per
-    # stream) plus the head's hand-offs; the floor counts the chain alone at its measured
-    # per-layer latency (stamps), so frac = the share of the step the unavoidable chain takes
+    # stream) plus the head's hand-offs; the floor is derived from instruction latencies
+    # (gen_latency_floor), not from this kernel's own timings
+    fl = gen_latency_floor(arch)
     t_layer = gen_layer_latency(net, arch, B)
-    L = n_layers(arch)
-    if t_layer is not None:
-        out['roofline'] = {'bound': 'latency', 'unit': 'us/step', 'achieved': us, 'peak': L * t_layer,
-                           'frac': L * t_layer / us, 'per_layer_us': t_layer,
-                           'note': 'peak = %d layers x the measured per-layer chain latency; the rest of the step is '
-                                   'the head (skip tail, skip all-gather, post-net, partial-logit gather, draw)' % L}
+    out['roofline'] = {'bound': 'latency', 'unit': 'us/step', 'achieved': us, 'peak': fl['step_us'],
+                       'frac': fl['step_us'] / us, 'floor': fl,
+                       'measured_per_layer_us': t_layer,
+                       'note': 'peak = the dependent chain of one step at MI355X_MICROARCH.md latencies '
+                               '(gen_latency_floor); frac = floor / measured step'}
     out['roofline_hbm'] = {'bound': 'hbm', 'bytes_per_step': bps, 'achieved': bps * n / dt / 1e9, 'peak': HBM_PEAK / 1e9,
                            'unit': 'GB/s', 'frac': bps * n / dt / HBM_PEAK,
                            'note': 'weights are L2/MALL- and LDS/register-resident across steps: not bandwidth-bound'}
@@ -180,7 +234,7 @@ def bench_gen(net, arch, B=10, seconds=3.0, sr=16000, chunk=1000, sweep=(16, 64,
         bs = gen_bytes_per_step(arch, Bs)
         rows.append({'batch': Bs, 'us_per_step': dts / ns * 1e6, 'samples_per_s': Bs * ns / dts,
                      'weight_and_state_GB_per_s': bs * ns / dts / 1e9,
-                     'form': 'persistent' if gs.persistent else 'per-step'})
+                     'form': _gen_form(gs, Bs)})
     out['sweep'] = rows
     return out
 
@@ -365,10 +419,19 @@ class TrainBench:
             out['frac_of_f32_peak'] = ach / FP32_MFMA_PEAK
         if name == 'layer_fwd':
             L, Cr, Cd = self.arch['n_blocks'] * self.arch['n_block_layers'], self.arch['n_res'], self.arch['n_dil']
-            fl = 10.0 * Cr * Cd * self.B * self.T * L
+            # conv + residual, + the in-chain LC term (2 Lo 2Cd per position) when the chain computes it
+            lo = self.arch['n_lc_out'] if 64 < self.arch['n_lc_out'] <= 80 and x3 else 0
+            fl = (10.0 * Cr * Cd + 4.0 * lo * Cd) * self.B * self.T * L
             cp = chain_ceiling(name, self.arch, x3)
             out['mfma'] = {'flop_per_launch': fl, 'achieved_tflops': fl / avg / 1e12, 'peak_tflops': cp / 1e12,
                            'frac': fl / avg / cp, 'floor_us': fl / cp * 1e6}
+            # the chain is bound by neither HBM nor MFMA but by its per-layer dependent path:
+            # quoted HBM (north_star) with the latency floor beside it
+            out['bound'] = 'latency'
+            out['hbm_frac'] = out['frac']
+            lf = chain_fwd_latency_floor(self.arch, self.B, self.T)
+            out['latency_floor'] = lf
+            out['latency_frac'] = lf['launch_us'] / (avg * 1e6)
         return out
 
     def close(self):

@@ -7,6 +7,10 @@
 //   dGC_SIGNAL_l = GC_EMBEDᵀ·GCD_l[:, :Cd],  dGC_EMBED = Σ_l GCD_l·[GC_SIGNAL_l | GC_GATE_l]ᵀ.
 // LC: the per-layer projections LC_SIGNAL_l / LC_GATE_l are packed side by side into one
 // [Clc][L·2Cd] matrix so the whole conditioning input is ONE GEMM lc·LCcat (engine.cpp).
+#include <string.h>
+
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -132,9 +136,296 @@ __global__ void lc_pack_kernel(float* __restrict__ cat, float* __restrict__ wsig
 
 int grid_for(long n) { return (int)std::min<long>((n + 255) / 256, 4096); }
 
+// ---- LC upsample fused over its stages (tmodel.py:68-83) ------------------------------------------
+// Stage i (conv1d_transpose, kernel = stride = s_i, SAME: non-overlapping) maps a frame's rows
+// [R_i][I_i] to [R_i·s_i][Lo]: out[s·t + j][o] = Σ_c in[t][c]·F_i[j][o][c].  A mel frame's whole
+// upsample (1 -> 4 -> 16 -> 64 -> 256 rows for arch5) is one block's work: one launch per
+// direction instead of a (split-K) GEMM per stage and direction (arch5 B = 8: 4 + 9 launches of
+// 20-40 µs each, latency-bound).  f32 FMA, 4 x s / 4 x 4 / 2 x 4 register micro-tiles over LDS
+// operands (b128 reads, filter rows padded to I + 4 floats: conflict-free).
+constexpr int UP_THREADS = 512;
+constexpr int UP_MAXS = 8;           // stride per stage
+constexpr int UP_LDS = 40448;        // floats (158 KiB)
+struct UpK {
+  const float* mel;                  // [frames][Li]
+  const float* F[4];                 // stage filters [s][Lo][I]
+  float* act[4];                     // stage outputs, [frames·R_{i+1}][Lo]
+  const float* dlc;                  // backward: d(last stage output) [frames·hop][Lo]
+  float* dpart;                      // backward: per-frame filter-gradient partials [frames][Σ_i s_i·Lo·I_i]
+  int nup, s[4], Li, Lo, frames;
+};
+
+// F_i rows [n0, n0 + nr) (n = j·Lo + o, each I floats) -> W[n - n0][I + 4]
+LBWN_DEV void up_load_rows(float* W, const float* F, int n0, int nr, int I, int tid) {
+  const int I4 = I / 4, tot = nr * I4;
+  for (int e0 = tid; e0 < tot; e0 += 8 * UP_THREADS) {
+    floatx4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = min(e0 + u * UP_THREADS, tot - 1);
+      v[u] = *(const floatx4*)(F + (long)(n0 + e / I4) * I + 4 * (e % I4));
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * UP_THREADS;
+      if (e < tot) *(floatx4*)(W + (e / I4) * (I + 4) + 4 * (e % I4)) = v[u];
+    }
+  }
+}
+// rows [R][C] of global src (row stride C) -> LDS [R][C + 4]
+LBWN_DEV void up_load_tile(float* dst, const float* src, int R, int C, int tid) {
+  const int C4 = C / 4, tot = R * C4;
+  for (int e0 = tid; e0 < tot; e0 += 4 * UP_THREADS) {
+    floatx4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = min(e0 + u * UP_THREADS, tot - 1);
+      v[u] = *(const floatx4*)(src + (long)(e / C4) * C + 4 * (e % C4));
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * UP_THREADS;
+      if (e < tot) *(floatx4*)(dst + (e / C4) * (C + 4) + 4 * (e % C4)) = v[u];
+    }
+  }
+}
+
+LBWN_DEV float dot4f(floatx4 a, floatx4 b, float c) {
+  c = fmaf(a[0], b[0], c);
+  c = fmaf(a[1], b[1], c);
+  c = fmaf(a[2], b[2], c);
+  return fmaf(a[3], b[3], c);
+}
+
+// Forward: LDS = W (the stage's filter, [s·Lo][I + 4]) | two row buffers [R][Lo + 4]
+__global__ __launch_bounds__(UP_THREADS) void lc_up_fwd_kernel(UpK a) {
+  __shared__ __attribute__((aligned(16))) float sm[UP_LDS];
+  const int f = blockIdx.x, tid = threadIdx.x, Lo = a.Lo, LP = Lo + 4;
+  int R = 1, I = a.Li;
+  int maxw = 0, last_in = 1;
+  for (int i = 0; i < a.nup; ++i) {
+    maxw = max(maxw, a.s[i] * Lo * ((i ? Lo : a.Li) + 4));
+    if (i + 1 < a.nup) last_in *= a.s[i];
+  }
+  float* W = sm;
+  float* buf[2] = {sm + maxw, sm + maxw + last_in * LP};
+  float* in = buf[0];
+  up_load_tile(in, a.mel + (long)f * a.Li, 1, a.Li, tid);   // stage 0 input: the mel frame (row stride Li + 4)
+  int IP = a.Li + 4;
+  for (int i = 0; i < a.nup; ++i) {
+    const int s = a.s[i], N = s * Lo;
+    up_load_rows(W, a.F[i], 0, N, I, tid);
+    __syncthreads();
+    float* out = buf[(i + 1) & 1];
+    const bool keep = i + 1 < a.nup;
+    float* g = a.act[i] + (long)f * R * s * Lo;
+    const int RT = (R + 3) / 4;
+    for (int w = tid; w < Lo * RT; w += UP_THREADS) {
+      const int o = w % Lo, rt = w / Lo;
+      float acc[4][UP_MAXS];
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int j = 0; j < UP_MAXS; ++j) acc[ii][j] = 0.f;
+      for (int k = 0; k < I; k += 4) {
+        floatx4 x[4];
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) x[ii] = *(const floatx4*)(in + min(4 * rt + ii, R - 1) * IP + k);
+#pragma unroll
+        for (int j = 0; j < UP_MAXS; ++j) {
+          if (j < s) {
+            const floatx4 wv = *(const floatx4*)(W + (j * Lo + o) * (I + 4) + k);
+#pragma unroll
+            for (int ii = 0; ii < 4; ++ii) acc[ii][j] = dot4f(x[ii], wv, acc[ii][j]);
+          }
+        }
+      }
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int t = 4 * rt + ii;
+        if (t >= R) break;
+#pragma unroll
+        for (int j = 0; j < UP_MAXS; ++j) {
+          if (j < s) {
+            g[(long)(s * t + j) * Lo + o] = acc[ii][j];
+            if (keep) out[(s * t + j) * LP + o] = acc[ii][j];
+          }
+        }
+      }
+    }
+    __syncthreads();   // W and `in` are free; `out` is the next stage's input
+    in = out;
+    IP = LP;
+    R *= s;
+    I = Lo;
+  }
+}
+
+// Backward, per frame, stages nup-1 .. 0 with D = d(stage output) rows [R·s][Lo] in LDS:
+//   dF_i partial [s·Lo][I] = Σ_t D[t][n]·IN[t][c]  (D viewed [R][s·Lo], IN = the stage input rows)
+//   din [R][I]             = Σ_n D[t][n]·F_i[n][c]  (the previous stage's D; skipped for stage 0)
+// LDS = D [hop][Lo + 4] | DN (din) [hop / s_last][Lo + 4] | IN [R][I + 4] | W (one phase j of
+// F_i: [Lo][I + 4]), D and DN swapping roles per stage.
+__global__ __launch_bounds__(UP_THREADS) void lc_up_bwd_kernel(UpK a) {
+  __shared__ __attribute__((aligned(16))) float sm[UP_LDS];
+  const int f = blockIdx.x, tid = threadIdx.x, Lo = a.Lo, LP = Lo + 4;
+  int hop = 1, offs[4], ptot = 0;
+  for (int i = 0; i < a.nup; ++i) {
+    hop *= a.s[i];
+    offs[i] = ptot;
+    ptot += a.s[i] * Lo * (i ? Lo : a.Li);
+  }
+  const int Imax = max(a.Li, Lo);
+  float* D = sm;
+  float* DN = D + hop * LP;
+  float* INB = DN + (hop / a.s[a.nup - 1]) * LP;
+  float* W = INB + (hop / a.s[a.nup - 1]) * (Imax + 4);
+  up_load_tile(D, a.dlc + (long)f * hop * Lo, hop, Lo, tid);
+  int R = hop;
+  for (int i = a.nup - 1; i >= 0; --i) {
+    const int s = a.s[i], I = i ? Lo : a.Li, IP = I + 4, N = s * Lo;
+    R /= s;   // stage input rows
+    const float* inp = i ? a.act[i - 1] + (long)f * R * Lo : a.mel + (long)f * a.Li;
+    up_load_tile(INB, inp, R, I, tid);
+    __syncthreads();
+    // dF_i partial: work item = (n4 group, c4 group), 4 x 4 outputs, K = R rows
+    float* dp = a.dpart + (long)f * ptot + offs[i];
+    const int C4 = I / 4;
+    for (int w = tid; w < (N / 4) * C4; w += UP_THREADS) {
+      const int c4 = w % C4, n4 = w / C4, j = (4 * n4) / Lo, o = (4 * n4) % Lo;
+      floatx4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      for (int t = 0; t < R; ++t) {
+        const floatx4 dv = *(const floatx4*)(D + (s * t + j) * LP + o);
+        const floatx4 xv = *(const floatx4*)(INB + t * IP + 4 * c4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] += dv[q] * xv;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) *(floatx4*)(dp + (long)(4 * n4 + q) * I + 4 * c4) = acc[q];
+    }
+    if (i == 0) break;   // no gradient into the mel input
+    // din: work item = (2-row group, c4 group), K = s·Lo in phases j (one phase of F_i in W)
+    const int RT2 = (R + 1) / 2, nwork = RT2 * C4;
+    floatx4 acc[2][2];   // up to 2 work items per thread (R·I/8 <= 2·512)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) acc[u][0] = acc[u][1] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < s; ++j) {
+      __syncthreads();   // W free (previous phase / the dF loop's readers done with INB are not W's)
+      up_load_rows(W, a.F[i], j * Lo, Lo, I, tid);
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int w = tid + u * UP_THREADS;
+        if (w >= nwork) break;
+        const int c4 = w % C4, r2 = w / C4, t0 = 2 * r2, t1 = min(2 * r2 + 1, R - 1);
+        for (int o = 0; o < Lo; o += 4) {
+          const floatx4 d0 = *(const floatx4*)(D + (s * t0 + j) * LP + o);
+          const floatx4 d1 = *(const floatx4*)(D + (s * t1 + j) * LP + o);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const floatx4 wv = *(const floatx4*)(W + (o + q) * IP + 4 * c4);
+            acc[u][0] += d0[q] * wv;
+            acc[u][1] += d1[q] * wv;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int w = tid + u * UP_THREADS;
+      if (w >= nwork) break;
+      const int c4 = w % C4, r2 = w / C4;
+      *(floatx4*)(DN + (2 * r2) * LP + 4 * c4) = acc[u][0];
+      if (2 * r2 + 1 < R) *(floatx4*)(DN + (2 * r2 + 1) * LP + 4 * c4) = acc[u][1];
+    }
+    __syncthreads();   // DN complete; D and INB free
+    float* tmp = D;
+    D = DN;
+    DN = tmp;
+  }
+}
+
+// filter gradients: dF[e] = Σ_f dpart[f][e], frames in order (deterministic)
+__global__ void lc_up_sum_kernel(const float* __restrict__ dpart, UpK a, float* g0, float* g1, float* g2, float* g3,
+                                 int ptot) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= ptot) return;
+  float s = 0.f;
+  for (int f = 0; f < a.frames; ++f) s += dpart[(long)f * ptot + e];
+  int off = 0;
+  float* g[4] = {g0, g1, g2, g3};
+  for (int i = 0; i < a.nup; ++i) {
+    const int n = a.s[i] * a.Lo * (i ? a.Lo : a.Li);
+    if (e < off + n) { g[i][e - off] = s; return; }
+    off += n;
+  }
+}
+
 }  // namespace
 
 int lbwn_gc_part_floats(int L, int Ge, int Cd) { return GC_CSPLIT * Ge * 2 * L * Cd; }
+
+// the fused upsample's envelope (else the per-stage GEMMs): <= 4 stages of stride <= 8, widths
+// multiples of 4, hop <= 256, and both kernels' LDS carve-outs within UP_LDS
+int lbwn_lc_up_fused_ok(int nup, const int* s, int Li, int Lo) {
+  if (nup < 1 || nup > 4 || Li % 4 || Lo % 4 || Li < 4 || Lo < 4 || Li > Lo) return 0;
+  int hop = 1, maxw = 0, last_in = 1;
+  for (int i = 0; i < nup; ++i) {
+    if (s[i] < 1 || s[i] > UP_MAXS) return 0;
+    hop *= s[i];
+    maxw = std::max(maxw, s[i] * Lo * ((i ? Lo : Li) + 4));
+    if (i + 1 < nup) last_in *= s[i];
+  }
+  if (hop > 256) return 0;
+  const int fwd = maxw + 2 * std::max(last_in, 1) * (Lo + 4) + (Li + 4);
+  const int Imax = std::max(Li, Lo), rin = hop / s[nup - 1];
+  const int bwd = hop * (Lo + 4) + rin * (Lo + 4) + rin * (Imax + 4) + Lo * (Imax + 4);
+  // din work items per thread <= 2
+  for (int i = 1; i < nup; ++i) {
+    int R = 1;
+    for (int j = 0; j < i; ++j) R *= s[j];
+    if ((R + 1) / 2 * (Lo / 4) > 2 * UP_THREADS) return 0;
+  }
+  return fwd <= UP_LDS && bwd <= UP_LDS;
+}
+int lbwn_lc_up_part_floats(int nup, const int* s, int Li, int Lo, int frames) {
+  long tot = 0;
+  for (int i = 0; i < nup; ++i) tot += (long)s[i] * Lo * (i ? Lo : Li);
+  return (int)(tot * frames);
+}
+
+static UpK up_args(int nup, const int* s, int Li, int Lo, int frames, const float* mel, const float* const* F,
+                   float* const* act) {
+  UpK k;
+  memset(&k, 0, sizeof(k));
+  k.mel = mel; k.nup = nup; k.Li = Li; k.Lo = Lo; k.frames = frames;
+  for (int i = 0; i < nup; ++i) { k.s[i] = s[i]; k.F[i] = F[i]; k.act[i] = act[i]; }
+  return k;
+}
+
+int lbwn_lc_up_fwd_launch(int nup, const int* s, int Li, int Lo, int frames, const float* mel, const float* const* F,
+                          float* const* act, hipStream_t st) {
+  LBWN_REQUIRE(lbwn_lc_up_fused_ok(nup, s, Li, Lo), "lc upsample: shape outside the fused kernel's envelope");
+  UpK k = up_args(nup, s, Li, Lo, frames, mel, F, act);
+  lc_up_fwd_kernel<<<frames, UP_THREADS, 0, st>>>(k);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_lc_up_bwd_launch(int nup, const int* s, int Li, int Lo, int frames, const float* mel, const float* const* F,
+                          float* const* act, const float* dlc, float* dpart, float* const* dF, hipStream_t st) {
+  LBWN_REQUIRE(lbwn_lc_up_fused_ok(nup, s, Li, Lo), "lc upsample: shape outside the fused kernel's envelope");
+  UpK k = up_args(nup, s, Li, Lo, frames, mel, F, act);
+  k.dlc = dlc; k.dpart = dpart;
+  lc_up_bwd_kernel<<<frames, UP_THREADS, 0, st>>>(k);
+  LBWN_CHECK_LAUNCH();
+  int ptot = 0;
+  for (int i = 0; i < nup; ++i) ptot += s[i] * Lo * (i ? Lo : Li);
+  lc_up_sum_kernel<<<(ptot + 255) / 256, 256, 0, st>>>(dpart, k, dF[0], nup > 1 ? dF[1] : nullptr,
+                                                       nup > 2 ? dF[2] : nullptr, nup > 3 ? dF[3] : nullptr, ptot);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
 
 int lbwn_gc_table_launch(const float* emb, const float* wsig, const float* wgate, float* out, int L, int ncat1,
                          int Ge, int Cd, hipStream_t st) {

@@ -41,6 +41,8 @@ struct lbwn_plan {
   bool cond_valid = false;
   int split_dlc, split_dlcx, split_up[8];
   size_t oSPLIT_AUX = 0;         // split-K workspace of the aux2 stream (LC / GC grads beside dSKIP)
+  bool up_fused = false;         // LC upsample as one fused launch per direction (cond.hip)
+  size_t oUPPART = 0;            // its per-frame filter-gradient partials
   size_t total;
   long x_layer_stride;  // floats
   int split_post2, split_post1, split_skip;
@@ -369,6 +371,8 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
       }
     }
     p->oCOND = p->Lo ? carve(cur, f * (size_t)M * ncond) : 0;
+    p->up_fused = p->Lo > 0 && lbwn_lc_up_fused_ok(p->nup, p->up, p->Li, p->Lo);
+    if (p->up_fused) p->oUPPART = carve(cur, f * (size_t)lbwn_lc_up_part_floats(p->nup, p->up, p->Li, p->Lo, (int)(M / hop)));
     p->oDVALL = p->Lo ? carve(cur, f * (size_t)M * ncond) : 0;
     p->oLCCAT = p->Lo ? carve(cur, f * (size_t)p->Lo * ncond) : 0;
     p->oDLCCAT = p->Lo ? carve(cur, f * (size_t)p->Lo * ncond) : 0;
@@ -522,7 +526,14 @@ int cond_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const float* mel,
     c.gc_tab = tab;
     c.gc_ld = 2L * L * Cd;
   }
-  if (p->Lo > 0) {
+  if (p->Lo > 0 && p->up_fused) {
+    float* act[8];
+    for (int i = 0; i < p->nup; ++i) act[i] = at<float>(ws, p->oLCACT[i]);
+    Probe(p, st, "lc_up_fwd");
+    if ((e = lbwn_lc_up_fwd_launch(p->nup, p->up, p->Li, p->Lo, (int)(p->M / p->hop), mel, P->lc_up, act, st)))
+      return e;
+    Probe::end(p, st, "lc_up_fwd");
+  } else if (p->Lo > 0) {
     const float* in = mel;
     long rows = (long)p->B * (p->T / p->hop);
     int I = p->Li;
@@ -591,6 +602,16 @@ int lc_upsample_bwd(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G, vo
                     hipStream_t st) {
   int e;
   const float* dout = at<float>(ws, p->oDLC[0]);
+  if (p->up_fused) {
+    const float* F[8];
+    float* act[8];
+    for (int i = 0; i < p->nup; ++i) { F[i] = P->lc_up[i]; act[i] = at<float>(ws, p->oLCACT[i]); }
+    Probe(p, st, "lc_up_bwd");
+    e = lbwn_lc_up_bwd_launch(p->nup, p->up, p->Li, p->Lo, (int)(p->M / p->hop), mel, F, act, dout,
+                              at<float>(ws, p->oUPPART), G->lc_up, st);
+    Probe::end(p, st, "lc_up_bwd");
+    return e;
+  }
   long rows = p->M;
   int buf = 0;
   Probe(p, st, "lc_up_bwd");

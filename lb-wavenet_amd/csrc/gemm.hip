@@ -452,6 +452,8 @@ __global__ __launch_bounds__(128 * WM, (WM == 2 && STAGES == 1) ? X3_OCC : 1) vo
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int tiles_n = (g.N + BN - 1) / BN, tiles_m = (g.M + BM - 1) / BM;
+  if (g.step_advance && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && tid == 0)   // no-return atomic
+    __hip_atomic_fetch_add(g.step_advance, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int t = gemm_tile();
   const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
   const int kz0 = gemm_split() * g.k_per_split;
@@ -697,7 +699,8 @@ int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int 
                      hipStream_t st) {
   if (lbwn_gemm_mode() == 1 && a.a_codes == nullptr && a.K >= 4 && a.M >= 4 && a.N >= 4)
     return gemm_launch_x3(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
-  LBWN_REQUIRE(a.colpart == nullptr, "gemm: column partials need the bf16-split form");
+  LBWN_REQUIRE(a.colpart == nullptr && a.step_advance == nullptr,
+               "gemm: column partials / the step counter need the bf16-split form");
   return gemm_launch_t<16, 128, 128>(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
 }
 

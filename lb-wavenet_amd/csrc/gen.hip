@@ -1047,6 +1047,10 @@ struct lbwn_gen_plan {
   long long max_steps;
   size_t oRING, oZCAT, oSKP, oHP, oLGP, oLOG, oSTEP, oCODE, oTEACH, oSAMP, oWAV, oGCP, oBSUM, oGIMG, oTRACE, total;
   size_t oGRAN;   // persistent form: granules [zg B·L·32 | sg B·Cs | lg P_NH·B·Q]
+  // GEMM form (B > P_MAXB): skip / post1 / post2 as bf16-split MFMA GEMMs over the B streams
+  // (split-K partial slabs in oGSPL) instead of the vector GEMVs
+  size_t oGSPL = 0;
+  int gsplit[3] = {1, 1, 1};
   long n_gran;
   bool trace, persist;
   int ksl_skip, ks_skip, ks_h, ks_lg;
@@ -1055,6 +1059,11 @@ struct lbwn_gen_plan {
   unsigned long long seed;
   int pre_bias;
 };
+
+// the per-step GEMM form: large B, shapes the split GEMM takes (N % 4, K % 4, row strides)
+static bool gemm_form_ok(const lbwn_gen_plan* p) {
+  return p->B > P_MAXB && p->Cs % 4 == 0 && p->Cp % 4 == 0 && p->Q % 4 == 0 && (p->L * p->Cd) % 4 == 0;
+}
 
 static size_t gcarve(size_t& cur, size_t bytes) {
   size_t o = cur;
@@ -1112,6 +1121,17 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
                p->Cp <= 16 * P_NH && have_dev && B + P_NH <= ncu;
   p->n_gran = (long)B * p->L * 32 + (long)B * p->Cs + (long)P_NH * B * p->Q;
   p->oGRAN = gcarve(cur, 8 * (size_t)p->n_gran);
+  if (gemm_form_ok(p)) {
+    // split K until ~256 blocks of 128 x 128 tiles (M = B streams is short), >= 4 k-steps of 32 each
+    const int Ns[3] = {p->Cs, p->Cp, p->Q}, Ks[3] = {p->L * p->Cd, p->Cs, p->Cp};
+    long most = 0;
+    for (int i = 0; i < 3; ++i) {
+      const int tiles = ((B + 127) / 128) * ((Ns[i] + 127) / 128);
+      p->gsplit[i] = std::max(1, std::min(256 / std::max(1, tiles), Ks[i] / 128));
+      most = std::max(most, (long)p->gsplit[i] * B * Ns[i]);
+    }
+    p->oGSPL = gcarve(cur, 4 * (size_t)most);
+  }
   p->total = cur;
   *out = p;
   return 0;
@@ -1175,6 +1195,52 @@ extern "C" int lbwn_gen_start(lbwn_gen_plan* p, const lbwn_params* P, void* ws, 
 
 extern "C" int lbwn_gen_is_persistent(const lbwn_gen_plan* p) { return p && p->persist ? 1 : 0; }
 
+static WaveK wave_args(lbwn_gen_plan* p, const lbwn_params* P, void* ws) {
+  WaveK c;
+  c.pre = P->pre; c.pre_b = P->pre_b; c.img = gat<float>(ws, p->oGIMG);
+  c.gc_proj = p->a.n_gc_embed > 0 ? gat<float>(ws, p->oGCP) : nullptr;
+  c.rings = gat<float>(ws, p->oRING); c.zcat = gat<float>(ws, p->oZCAT);
+  c.step = gat<long long>(ws, p->oSTEP); c.code = gat<int>(ws, p->oCODE);
+  c.trace = nullptr;
+  c.B = p->B; c.L = p->L; c.nbl = p->nbl; c.Cr = p->Cr; c.Cd = p->Cd; c.pre_bias = p->pre_bias;
+  return c;
+}
+
+// Per-step GEMM form (B > P_MAXB): the chain (gen_wave, one workgroup per stream) then the head as
+// three bf16-split MFMA GEMMs over all B streams (imodel.py:125-164: skip = Σ_l z_l·SKIP_l + Σb,
+// h = relu(relu(skip)·POST1 + b1), logits = h·POST2 + b2) and the sampler.  The K-split vector GEMVs
+// re-read every weight per 16-stream group with FMA (B = 256: 211 µs per step).
+static int gen_run_gemm(lbwn_gen_plan* p, const lbwn_params* P, void* ws, int n_steps, DrawK d, hipStream_t st) {
+  const WaveK c = wave_args(p, P, ws);
+  float* S = gat<float>(ws, p->oSKP);     // [B][Cs]   (the GEMV partial buffers are larger)
+  float* H = gat<float>(ws, p->oHP);      // [B][Cp]
+  float* LG = gat<float>(ws, p->oLGP);    // [B][Q] logits with b2
+  float* SPL = gat<float>(ws, p->oGSPL);
+  lbwn_gemm_args sk, p1, p2;
+  memset(&sk, 0, sizeof(sk));
+  sk.A = c.zcat; sk.lda = (long)p->L * p->Cd; sk.B = P->skip; sk.ldb = p->Cs; sk.C = S; sk.ldc = p->Cs;
+  sk.M = p->B; sk.N = p->Cs; sk.K = p->L * p->Cd; sk.bias = P->skip_b ? gat<float>(ws, p->oBSUM) : nullptr;
+  sk.step_advance = gat<long long>(ws, p->oSTEP);   // the sampler reads step - 1
+  p1 = sk;
+  p1.step_advance = nullptr;
+  p1.A = S; p1.lda = p->Cs; p1.relu_a = 1; p1.B = P->post1; p1.ldb = p->Cp; p1.C = H; p1.ldc = p->Cp;
+  p1.N = p->Cp; p1.K = p->Cs; p1.bias = P->post1_b; p1.relu_out = 1;
+  p2 = p1;
+  p2.A = H; p2.lda = p->Cp; p2.relu_a = 0; p2.B = P->post2; p2.ldb = p->Q; p2.C = LG; p2.ldc = p->Q;
+  p2.N = p->Q; p2.K = p->Cp; p2.bias = P->post2_b; p2.relu_out = 0;
+  d.part = LG; d.parts = 1; d.bias = nullptr;   // b2 added by the GEMM
+  for (int i = 0; i < n_steps; ++i) {
+    gen_wave_kernel<<<p->B, 512, 0, st>>>(c);
+    LBWN_CHECK_LAUNCH();
+    if (int e = lbwn_gemm_launch(sk, 1, 0, p->gsplit[0], SPL, st)) return e;
+    if (int e = lbwn_gemm_launch(p1, 1, 0, p->gsplit[1], SPL, st)) return e;
+    if (int e = lbwn_gemm_launch(p2, 1, 0, p->gsplit[2], SPL, st)) return e;
+    gen_sample_kernel<<<p->B, 64, 0, st>>>(d, c.step);
+    LBWN_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
 extern "C" int lbwn_gen_run(lbwn_gen_plan* p, const lbwn_params* P, void* ws, int n_steps, void* stream) {
   LBWN_REQUIRE(p && P && ws && n_steps >= 0, "gen_run: bad arguments");
   hipStream_t st = (hipStream_t)stream;
@@ -1204,6 +1270,7 @@ extern "C" int lbwn_gen_run(lbwn_gen_plan* p, const lbwn_params* P, void* ws, in
     LBWN_CHECK_LAUNCH();
     return 0;
   }
+  if (p->oGSPL && !p->trace && lbwn_gemm_mode() == 1) return gen_run_gemm(p, P, ws, n_steps, d, st);
   WaveK c;
   c.pre = P->pre; c.pre_b = P->pre_b; c.img = gat<float>(ws, p->oGIMG);
   c.gc_proj = p->a.n_gc_embed > 0 ? gat<float>(ws, p->oGCP) : nullptr;

@@ -18,6 +18,7 @@ struct lbwn_gemm_args {
   // (after bias/relu/mask), [ceil(M/256)][N] (one part per 256-row block tile), summed by
   // lbwn_colsum_final_launch: the bias gradient without a second pass over C
   float* colpart;
+  long long* step_advance;   // nullable, bf16-split form only: block 0 adds 1 (the per-step generator's counter)
   int k_per_split;     // set by the launcher
   long split_stride;   // set by the launcher
 };
@@ -193,3 +194,10 @@ int lbwn_gc_grad_launch(const float* emb, const float* wsig, const float* wgate,
                         float* demb, float* dsig, float* dgate, int L, int ncat1, int Ge, int Cd, hipStream_t st);
 int lbwn_gc_part_floats(int L, int Ge, int Cd);
 int lbwn_lc_pack_launch(float* cat, float* wsig, float* wgate, int L, int Clc, int Cd, int pack, hipStream_t st);
+// LC upsample (tmodel.py:68-83) fused over its stages, one block per mel frame (cond.hip)
+int lbwn_lc_up_fused_ok(int nup, const int* s, int Li, int Lo);
+int lbwn_lc_up_part_floats(int nup, const int* s, int Li, int Lo, int frames);
+int lbwn_lc_up_fwd_launch(int nup, const int* s, int Li, int Lo, int frames, const float* mel, const float* const* F,
+                          float* const* act, hipStream_t st);
+int lbwn_lc_up_bwd_launch(int nup, const int* s, int Li, int Lo, int frames, const float* mel, const float* const* F,
+                          float* const* act, const float* dlc, float* dpart, float* const* dF, hipStream_t st);

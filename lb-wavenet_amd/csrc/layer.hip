@@ -28,6 +28,14 @@ constexpr int RED_PARTS = 32;       // deferred reduction: parts prefetched per 
 #ifndef LBWN_ABL
 #define LBWN_ABL 0
 #endif
+// LDS bank-conflict attribution (tools/lds_conf.sh), counter-only builds: bit b sends one group of
+// chain_bwd_x3_kernel's LDS accesses to a conflict-free address (reads: a wave-uniform broadcast,
+// writes (2048): lane-contiguous 16-B slots); the outputs are wrong, SQ_LDS_BANK_CONFLICT's drop
+// per bit is that group's share.  0 in every real build.
+#ifndef LBWN_CONF
+#define LBWN_CONF 0
+#endif
+#define CONF(bit) ((LBWN_CONF & (bit)) != 0)
 
 // Compact kernel arguments (the full lbwn_layer_args by value spilled ~100 SGPRs).
 struct FwdK {
@@ -1524,7 +1532,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
           const int e = tid + 256 * i, row = e >> 3, c4 = (e & 7) * 4, sr = row + dn;
           const int ts = min(t0 + sr, a.T - 1);
           gl[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
-          go[i] = *(const floatx4*)(OC + swz(min(sr, LP - 1), c4));
+          go[i] = *(const floatx4*)(OC + (CONF(1) ? 0 : swz(min(sr, LP - 1), c4)));
         }
       }
       if (dn) {
@@ -1533,7 +1541,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
           const int e = tid + 256 * i, row = e >> 3, c4 = (e & 7) * 4, sr = row + dn, ts = t0 + sr;
           floatx4 v = sr < LP ? go[i] : gl[i];
           if (ts >= a.T) v = floatx4{0.f, 0.f, 0.f, 0.f};
-          *(floatx4*)(G + swz(row, c4)) = v;
+          *(floatx4*)(G + (CONF(2048) ? 4 * (tid & 255) : swz(row, c4))) = v;
         }
         // lands this wave's part of the weight image (LDS-DMA'd after the last layer's publish)
         // and the prefetched rows; the barrier then covers every wave's part
@@ -1560,10 +1568,10 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {   // own row: + out_a (the top layer writes it, g = 0)
         float* gp = G + swz(r, 8 * q + 4 * h);
-        floatx4 v = dn ? *(const floatx4*)gp : floatx4{0.f, 0.f, 0.f, 0.f};
+        floatx4 v = dn ? *(const floatx4*)(CONF(2) ? G : gp) : floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int j = 0; j < 4; ++j) { v[j] += oa[4 * q + j]; gv[4 * q + j] = v[j]; }
-        *(floatx4*)gp = v;
+        *(floatx4*)(CONF(2048) ? G + 4 * lane + 256 * q : gp) = v;
       }
       // 2. dz = dZ + RES·g  (f32 MFMA)
       floatx16 dz;
@@ -1571,7 +1579,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
         floatx4 rx[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          rx[q] = *(const floatx4*)(Rs + pi * XS + 8 * q + 4 * h);
+          rx[q] = *(const floatx4*)(Rs + (CONF(4) ? 8 * q : pi * XS + 8 * q + 4 * h));
           floatx4 v = dzr[q];
           if (!valid) v = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1599,8 +1607,8 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
         for (int q = 0; q < 4; ++q) {
           const floatx4 vs = floatx4{dvs[4 * q], dvs[4 * q + 1], dvs[4 * q + 2], dvs[4 * q + 3]};
           const floatx4 vg = floatx4{dvg[4 * q], dvg[4 * q + 1], dvg[4 * q + 2], dvg[4 * q + 3]};
-          *(floatx4*)(DVs + swz(r, 8 * q + 4 * h)) = vs;
-          *(floatx4*)(DVg + swz(r, 8 * q + 4 * h)) = vg;
+          *(floatx4*)(DVs + (CONF(2048) ? 4 * lane + 256 * q + 1024 * w : swz(r, 8 * q + 4 * h))) = vs;
+          *(floatx4*)(DVg + (CONF(2048) ? 4 * lane + 256 * q + 1024 * w : swz(r, 8 * q + 4 * h))) = vg;
           if (dvo) {
             *(floatx4*)(dvo + 8 * q + 4 * h) = vs;
             *(floatx4*)(dvo + 32 + 8 * q + 4 * h) = vg;
@@ -1618,8 +1626,8 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
         auto loadf = [&](int s2, int buf) {
 #pragma unroll
           for (int p = 0; p < 3; ++p) {
-            fa[buf][p] = *(const bf16x8*)(WD + (32 + pi) * XW_ROW + 64 * p + 16 * s2 + 8 * h);
-            fc[buf][p] = *(const bf16x8*)(WD + pi * XW_ROW + 64 * p + 16 * s2 + 8 * h);
+            fa[buf][p] = *(const bf16x8*)(WD + (CONF(8) ? 64 * p + 16 * s2 : (32 + pi) * XW_ROW + 64 * p + 16 * s2 + 8 * h));
+            fc[buf][p] = *(const bf16x8*)(WD + (CONF(8) ? 64 * p + 16 * s2 : pi * XW_ROW + 64 * p + 16 * s2 + 8 * h));
           }
         };
         loadf(0, 0);
@@ -1645,7 +1653,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const floatx4 v = floatx4{acc_c[4 * q], acc_c[4 * q + 1], acc_c[4 * q + 2], acc_c[4 * q + 3]};
-          *(floatx4*)(OC + swz(r, 8 * q + 4 * h)) = v;
+          *(floatx4*)(OC + (CONF(2048) ? 4 * lane + 256 * q + 1024 * w : swz(r, 8 * q + 4 * h))) = v;
           if (pub) __builtin_amdgcn_raw_buffer_store_b128(v, rw, (int)((m * 32 + 8 * q + 4 * h) * 4), 0, 16);
         }
       }
@@ -1685,10 +1693,10 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const int p = 32 * w + 16 * s2 + 2 * j + h;
-            xp[s2][j] = Xp[p * 32 + pi];
-            xc[s2][j] = Xc[p * 32 + pi];
-            ds[s2][j] = DVs[swz(p, pi)];
-            dg[s2][j] = DVg[swz(p, pi)];
+            xp[s2][j] = Xp[CONF(16) ? p * 32 : p * 32 + pi];
+            xc[s2][j] = Xc[CONF(16) ? p * 32 : p * 32 + pi];
+            ds[s2][j] = DVs[CONF(32) ? p * 32 : swz(p, pi)];
+            dg[s2][j] = DVg[CONF(32) ? p * 32 : swz(p, pi)];
           }
         XSTAMP(8);
         if (l > 0) {   // image pieces w, w+4, ... (30 of 1 KiB)
@@ -1727,8 +1735,8 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const int p = 32 * c8 + 4 * j + kg;
-            za[j] = ZT[p * 32 + cz];
-            ga[j] = G[swz(p, og)];
+            za[j] = ZT[CONF(64) ? p * 32 : p * 32 + cz];
+            ga[j] = G[CONF(128) ? p * 32 : swz(p, og)];
           }
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1743,13 +1751,13 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
         const float* pl = c4 < 32 ? DVs : DVg;
         floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int p = 0; p < 16; ++p) s4 += *(const floatx4*)(pl + swz(pc * 16 + p, c4 & 31));
+        for (int p = 0; p < 16; ++p) s4 += *(const floatx4*)(pl + (CONF(256) ? p * 32 : swz(pc * 16 + p, c4 & 31)));
         *(floatx4*)(part + pc * 96 + c4) = s4;
       } else if (tid < 192) {
         const int c4 = ((tid - 128) & 7) * 4, pc = (tid - 128) >> 3;
         floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int p = 0; p < 16; ++p) s4 += *(const floatx4*)(G + swz(pc * 16 + p, c4));
+        for (int p = 0; p < 16; ++p) s4 += *(const floatx4*)(G + (CONF(256) ? p * 32 : swz(pc * 16 + p, c4)));
         *(floatx4*)(part + pc * 96 + 64 + c4) = s4;
       }
       {
@@ -1784,7 +1792,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
         for (int g = 0; g < 4; ++g) {
           floatx4 v[4];
 #pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) v[s4] = *(const floatx4*)(SCR + (s4 * 4 + wu) * 1024 + (g * 64 + lane) * 4);
+          for (int s4 = 0; s4 < 4; ++s4) v[s4] = *(const floatx4*)(SCR + (CONF(512) ? (s4 * 4 + wu) * 1024 : (s4 * 4 + wu) * 1024 + (g * 64 + lane) * 4));
 #pragma unroll
           for (int e = 0; e < 4; ++e) accW[4 * g + e] = (v[0][e] + v[1][e]) + (v[2][e] + v[3][e]);
         }

@@ -271,6 +271,60 @@ class MaskedSliceWav:
         self._itr = None
 
 
+class DeviceBatches:
+    """Host -> device stage of the training input (the reference's tf.data prefetch feeding
+    the session, data.py:267-268): each numpy batch of the prefetch thread is copied into a
+    pinned host buffer and sent to the GPU with a non-blocking copy on the current stream, so
+    the host never waits for the GPU (a pageable ``torch.as_tensor(..., device=)`` copy
+    synchronised every step with the previous step's kernels).  ``depth`` slots rotate; a slot's
+    pinned buffers are refilled only after its previous copy completed (its event), and its
+    device buffers are reused in stream order after the step that read them.
+    Yields (file_read_count, wav int32 [B,T], mel f32 [B,T/hop,C] or None, ids int32 [B,T]),
+    the last three on ``device``."""
+
+    def __init__(self, itr, device, depth=3):
+        self.itr, self.device, self.depth = itr, device, depth
+        self.slots = [None] * depth
+        self.k = 0
+
+    def __iter__(self):
+        return self
+
+    def _slot(self, wav, mel, ids):
+        import torch
+        k = self.k
+        self.k = (self.k + 1) % self.depth
+        s = self.slots[k]
+        shapes = (wav.shape, None if mel is None else mel.shape)
+        if s is None or s['shapes'] != shapes:
+            def pair(shape, dt):
+                return (torch.empty(shape, dtype=dt, pin_memory=True), torch.empty(shape, dtype=dt, device=self.device))
+            s = {'shapes': shapes, 'wav': pair(wav.shape, torch.int32), 'ids': pair(ids.shape, torch.int32),
+                 'mel': None if mel is None else pair(mel.shape, torch.float32), 'ev': None}
+            self.slots[k] = s
+        elif s['ev'] is not None:
+            s['ev'].synchronize()          # this slot's previous copy (depth batches ago) has landed
+        return s
+
+    def __next__(self):
+        import torch
+        cnt, wav, mel, ids = next(self.itr)
+        s = self._slot(wav, mel, ids)
+        out = []
+        for key, a, dt in (('wav', wav, np.int32), ('mel', mel, np.float32), ('ids', ids, np.int32)):
+            if a is None:
+                out.append(None)
+                continue
+            host, dev = s[key]
+            host.numpy()[...] = np.asarray(a, dtype=dt)
+            dev.copy_(host, non_blocking=True)
+            out.append(dev)
+        ev = torch.cuda.Event()
+        ev.record()
+        s['ev'] = ev
+        return (cnt, out[0], out[1], out[2])
+
+
 def torch_tensor(a):
     import torch
     return torch.as_tensor(np.asarray(a))

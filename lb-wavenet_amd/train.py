@@ -109,7 +109,7 @@ def main(argv=None):
     import torch
     from lbwn import dist as lbdist
     from lbwn.arch import normalize_arch, mel_hop_sz as hop_of
-    from lbwn.data import MaskedSliceWav
+    from lbwn.data import DeviceBatches, MaskedSliceWav
     from lbwn.optim import AdamOptimizer
     from lbwn.tmodel import WaveNetTrain
 
@@ -150,7 +150,7 @@ def main(argv=None):
 
     print('Starting training...', file=stderr)
     step = args.resume_step or 1
-    itr = dset.get_itr()
+    itr = DeviceBatches(dset.get_itr(), net.device)   # pinned buffers, non-blocking H2D: no per-step sync
     while step < args.max_steps:
         try:
             file_read_count, wav_input, mel_input, id_mask = next(itr)

@@ -107,3 +107,54 @@ def test_generate_teacher_wav_end_to_end(tmp_path):
     tq = R.mu_encode_tf32(teacher, 256)
     _, w_ref = R.generate(arch, P, 2, n, seed=0, teacher_q=tq)
     np.testing.assert_allclose(wav, w_ref[:, :wav.shape[1]], rtol=1e-6, atol=1e-6)
+
+
+def _synthetic_catalog(tmp_path, n_files=24):
+    from lbwn.data import SyntheticSource
+    src = SyntheticSource(seed=7, hop=1, n_mel=0, n_voices=1)
+    lines = []
+    for i in range(n_files):
+        vid, wav, _ = next(src)
+        wp, mp = tmp_path / ('s%d.npy' % i), tmp_path / ('s%d.mel.npy' % i)
+        np.save(wp, wav.astype(np.int32))
+        np.save(mp, np.zeros((len(wav), 0), np.float32))
+        lines.append('%d\t%s\t%s' % (vid, wp, mp))
+    cat = tmp_path / 'cat.txt'
+    cat.write_text('\n'.join(lines) + '\n')
+    return str(cat)
+
+
+def test_train_py_runs_at_bench_speed(tmp_path):
+    """The drop-in train.py loop (dealer thread -> pinned buffers -> non-blocking H2D -> plan ->
+    DP hook -> TF1 Adam, progress line every 10 steps, train.py:216-252) at arch3 B=8 T=4096
+    runs within 10 % of bench.py's pre-dealt device ring at the same arch/B/T.  Steady-state
+    time per step = (wall(61 steps) - wall(21 steps)) / 40, so setup cancels."""
+    import time
+    import train
+    sys.path.insert(0, ROOT)
+    import bench
+    from lbwn import dist as lbdist
+    from lbwn.arch import load_arch
+    arch_file = os.path.join(ROOT, 'par', 'arch3.json')
+    par = json.load(open(os.path.join(ROOT, 'par', 'par1.json')))
+    par.update(batch_sz=8, slice_sz=4096)
+    pf = tmp_path / 'par.json'
+    pf.write_text(json.dumps(par))
+    cat = _synthetic_catalog(tmp_path)
+    walls = {}
+    for n in (21, 61):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        net = train.main(['--max-steps', str(n), '--seed', '3', str(tmp_path / ('ck%d' % n)), arch_file, str(pf),
+                          cat])
+        torch.cuda.synchronize()
+        walls[n] = time.perf_counter() - t0
+        assert int(net.counters[0]) == n - 1
+        del net
+        torch.cuda.empty_cache()
+    train_ms = (walls[61] - walls[21]) * 1000.0 / 40
+    tb = bench.TrainBench(load_arch(arch_file), 8, 4096, lbdist.DPContext())
+    bench_ms, _, _, _ = tb.run(40, 5)
+    tb.close()
+    print('train.py %.3f ms/step, bench %.3f ms/step' % (train_ms, bench_ms))
+    assert train_ms <= 1.10 * bench_ms, (train_ms, bench_ms)

@@ -18,8 +18,9 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(params=['persistent', 'per_step'])
 def form(request, monkeypatch):
-    """Both execution forms: the persistent one-launch kernel (default for B <= 16) and the
-    per-step launches (LBWN_GEN_PERSIST=0, the form every B > 32 runs)."""
+    """Both execution forms at B <= 16: the persistent one-launch kernel (the default there)
+    and the per-step launches with vector GEMVs (LBWN_GEN_PERSIST=0).  B > 16 runs the per-step
+    GEMM form (test_gen_arch3_gemm_form)."""
     if request.param == 'per_step':
         monkeypatch.setenv('LBWN_GEN_PERSIST', '0')
     else:
@@ -95,7 +96,7 @@ def test_gen_arch3_b10_graph_replay(form):
 
 def test_gen_rerun_and_large_batch():
     """A second run on the same plan restarts the tags with the step counter (stale granules
-    from the first run must not be taken), and B = 40 > 32 runs the per-step form."""
+    from the first run must not be taken), and B = 40 > 16 runs the per-step GEMM form."""
     arch = small(gc=5)
     B, n = 40, 24
     g, P = make_gen(arch, B, chunk=8)
@@ -114,3 +115,20 @@ def test_gen_rerun_and_large_batch():
     s2, _ = R.generate(arch, P2, 12, n, seed=7, gc_ids=gc[:12])
     np.testing.assert_array_equal(g2.samples().cpu().numpy()[:, :n], s2)
     assert int(g2.tensor('status', torch.int32).item()) == 0
+
+
+def test_gen_arch3_gemm_form():
+    """B = 64 (> 16): gen_wave per step, then skip / post1 / post2 as bf16-split MFMA GEMMs over
+    the 64 streams (split-K, bias + relu epilogues) and the sampler; draws equal the oracle's."""
+    arch = load_arch(os.path.join(ROOT, 'par', 'arch3.json'))
+    B, n = 64, 60
+    g, P = make_gen(arch, B, chunk=20)
+    g.run(n)
+    torch.cuda.synchronize()
+    assert not g.persistent
+    s_ref, _, lg_ref = R.generate(arch, P, B, n, seed=7, return_logits=True)
+    got = g.samples().cpu().numpy()[:, :n]
+    mism = int((got != s_ref).sum())
+    assert mism == 0, '%d / %d draws differ' % (mism, got.size)
+    np.testing.assert_allclose(g.logits().cpu().numpy(), lg_ref[:, -1], rtol=0, atol=1e-4 * np.abs(lg_ref).max())
+    assert int(g.tensor('step', torch.int64).item()) == n
