@@ -548,6 +548,8 @@ int cond_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const float* mel,
       rows *= s;
       I = p->Lo;
     }
+  }
+  if (p->Lo > 0) {
     p->cond_valid = false;
     if (!lc_in_chain(p)) {
       if ((e = cond_project(p, P, ws, st))) return e;

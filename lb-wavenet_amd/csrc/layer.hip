@@ -815,7 +815,10 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
         for (int q = 0; q < 4; ++q) {
           const floatx4 v = floatx4{acc_r[4 * q], acc_r[4 * q + 1], acc_r[4 * q + 2], acc_r[4 * q + 3]};
           *(floatx4*)(nrow + 8 * q + 4 * h) = v;
-          if (valid) __builtin_amdgcn_raw_buffer_store_b128(v, rn, ((a.H + t) * 32 + 8 * q + 4 * h) * 4, 0, 16);
+          // (LBWN_ABL 256 / 1024: timing-only ablations of the non-halo rows' stores / of sc1)
+          const bool abl_skip = (LBWN_ABL & 256) && r < LP - min(1 << ((l + 1) % a.nbl), LP);
+          if (valid && !abl_skip)
+            __builtin_amdgcn_raw_buffer_store_b128(v, rn, ((a.H + t) * 32 + 8 * q + 4 * h) * 4, 0, (LBWN_ABL & 1024) ? 0 : 16);
         }
         FSTAMP(8);
         // 7. the next layer's own tap from the row this wave just wrote (wave-local: no barrier)
@@ -831,7 +834,9 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
       FSTAMP(5);
       // 8. publish x_{l+1}: every wave drains its sc1 stores, barrier, one lane signals
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      FSTAMP(9);
       __syncthreads();
+      FSTAMP(10);
       if (tid == 0 && l + 1 < a.L) publish_flag(a.flags + tile, (unsigned)(l + 1));
       // 9. image of layer l+2 into IMG[l&1] (everyone is past this layer's reads of it; its loads
       //    landed with the drain), and the LC image of layer l+2 (LC_{l+1} was read in step 7,
@@ -848,8 +853,9 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
       FSTAMP(6);
       // 10. z (skip GEMM input) and σ rows, issued last: they drain in the shadow of the next
       //     layer (written before the image, the image writes' vmcnt waits waited them out)
-      if (valid) store_rows16(a.Z + m * a.ldz + (long)l * a.Cd, z, a.Cd, h);
-      if (X3 && a.SG && valid) {
+      if (valid && !(LBWN_ABL & 512)) store_rows16(a.Z + m * a.ldz + (long)l * a.Cd, z, a.Cd, h);
+      if (LBWN_ABL & 512) asm volatile("" ::"v"(z[0]), "v"(z[15]), "v"(sgv[0]), "v"(sgv[15]));
+      if (X3 && a.SG && valid && !(LBWN_ABL & 512)) {
         float* sgl = a.SG + (long)l * a.sgls;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -1411,8 +1417,13 @@ __global__ void pack_layers_fb_x3_kernel(const float* sig, const float* gate, co
   }
 }
 
-// element (p, c) of a 32-float-row tile with the 4-float groups XOR-permuted by row pair
-LBWN_DEV int swz(int p, int c) { return p * 32 + (c ^ (((p >> 1) & 7) << 2)); }
+// element (p, c) of a 32-float-row tile with the 4-float groups XOR-permuted: bit 4 of the column
+// by row parity, bits 2-3 by (p >> 1) & 3.  Eight consecutive rows (the 8 lanes of one
+// ds_write_b128 group writing the same column group of their own rows) land on 8 distinct groups:
+// conflict-free; rows p, p+1 read by the two lane halves of a b32 read fall in opposite 16-bank
+// halves (a row-pair permutation left those writes 2-way conflicted: 6.6M of the kernel's 15.6M
+// SQ_LDS_BANK_CONFLICT cycles, tools/lds_conf.sh)
+LBWN_DEV int swz(int p, int c) { return p * 32 + (c ^ (((p & 1) << 4) | (((p >> 1) & 3) << 2))); }
 
 // acc += A·B over one 32-deep k-step of v_mfma_f32_16x16x32_bf16 from split fragments
 LBWN_DEV floatx4 mfma16_x3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx4 acc) {
@@ -1559,6 +1570,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
       auto dma_rows3 = [&](int j) {
         const int row = 32 * w + 8 * j + (lane >> 3), c4 = (lane & 7) * 4;
         const int trow = min(t0 + row, a.T - 1);
+        if (CONF(1024)) return;
         dma16(xl + (long)(a.H + trow - d) * 32 + c4, Xp + (32 * w + 8 * j) * 32);
         dma16(xl + (long)(a.H + trow) * 32 + c4, Xc + (32 * w + 8 * j) * 32);
         dma16(a.Zf + (mb + trow) * a.lddz + (long)l * 32 + c4, ZT + (32 * w + 8 * j) * 32);
@@ -1703,7 +1715,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const int pc = w + 4 * i;
-            if (pc < BIMG_F / 256) dma16(isrc + pc * 256, IMG + pc * 256);
+            if (pc < BIMG_F / 256 && !CONF(1024)) dma16(isrc + pc * 256, IMG + pc * 256);
           }
           load_regs(l - 1);
         }
@@ -1746,19 +1758,15 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
       XSTAMP(11);
       // 8. bias partials (column sums of DV and G) and the slab
       float* slab = a.slab + ((long)l * ntiles + tile) * SLAB;
-      if (tid < 128) {
-        const int c4 = (tid & 15) * 4, pc = tid >> 4;
-        const float* pl = c4 < 32 ? DVs : DVg;
+      //    (wave 0: DVs, 1: DVg, 2: G; lane = (row class pc, 4-column group c4), rows pc + 8p:
+      //    each 16-lane b128 read group then covers both bank halves, conflict-free under swz)
+      if (tid < 192) {
+        const int c4 = (lane & 7) * 4, pc = lane >> 3;
+        const float* pl = w == 0 ? DVs : w == 1 ? DVg : G;
         floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int p = 0; p < 16; ++p) s4 += *(const floatx4*)(pl + (CONF(256) ? p * 32 : swz(pc * 16 + p, c4 & 31)));
-        *(floatx4*)(part + pc * 96 + c4) = s4;
-      } else if (tid < 192) {
-        const int c4 = ((tid - 128) & 7) * 4, pc = (tid - 128) >> 3;
-        floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int p = 0; p < 16; ++p) s4 += *(const floatx4*)(G + (CONF(256) ? p * 32 : swz(pc * 16 + p, c4)));
-        *(floatx4*)(part + pc * 96 + 64 + c4) = s4;
+        for (int p = 0; p < 16; ++p) s4 += *(const floatx4*)(pl + (CONF(256) ? p * 32 : swz(pc + 8 * p, c4)));
+        *(floatx4*)(part + pc * 96 + 32 * w + c4) = s4;
       }
       {
         const int i16 = lane & 15, kg = lane >> 4;

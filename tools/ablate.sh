@@ -6,5 +6,5 @@ cd "$(dirname "$0")/../lb-wavenet_amd/csrc"
 mkdir -p ../lbwn/abl build/abl
 for A in "$@"; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -DLBWN_ABL=$A -c layer.hip -o build/abl/layer_$A.o
-  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC build/gemm.o build/abl/layer_$A.o build/misc.o build/gen.o build/engine.o build/capi.o -o ../lbwn/abl/liblbwn_abl$A.so
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -fPIC build/gemm.o build/abl/layer_$A.o build/misc.o build/gen.o build/cond.o build/engine.o build/capi.o -o ../lbwn/abl/liblbwn_abl$A.so
 done

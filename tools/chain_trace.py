@@ -38,6 +38,8 @@ for n, m in zip(fnames, fmed):
     print('  %-26s %6d  (%4.1f %%)' % (n, m, 100.0 * m / ftot))
 print('  layer total                %6d  = %.2f us at 2.4 GHz' % (ftot, ftot / 2400.0))
 print('    of which residual + stores %6d, next own tap %6d' % (np.median(fw[1:-2, 8] - fw[1:-2, 4]), np.median(fw[1:-2, 5] - fw[1:-2, 8])))
+print('    drain (vmcnt 0) %6d, barrier %6d, publish + image %6d' % (np.median(fw[1:-2, 9] - fw[1:-2, 5]),
+      np.median(fw[1:-2, 10] - fw[1:-2, 9]), np.median(fw[1:-2, 6] - fw[1:-2, 10])))
 tr = allr[1]   # backward
 if net.lib.lbwn_gemm_get_mode() == 1:      # chain_bwd_x3_kernel: XSTAMP(0..6)
     names = ['G wait+build, DMA issue', 'dz,dv,DV', 'dx MFMA + OC', 'publish+img DMA+prefetch', 'dSIG MFMA',

@@ -5,7 +5,7 @@
 # Each variant sends one group of the kernel's LDS accesses to a conflict-free address
 # (layer.hip LBWN_CONF); SQ_LDS_BANK_CONFLICT of the kernel per variant, against the real build (0).
 set -o pipefail
-BITS="0 1 2 4 8 16 32 64 128 256 512 2048 4095"
+BITS="${CONF_BITS:-0 1024 2048 256 4095 5119}"
 if [ "$1" = build ]; then
   cd "$(dirname "$0")/../lb-wavenet_amd/csrc"
   mkdir -p ../lbwn/conf build/conf
