@@ -66,6 +66,20 @@ LBWN_DEV int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 // 1/(1+e^-x); tanh(x) = 2σ(2x) - 1 (absolute error ≈1e-7, inside the 1e-5 parity bar).
 LBWN_DEV float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 LBWN_DEV float tanhf_(float x) { return 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(-2.0f * x)) - 1.0f; }
+// The gate z = tanh(a)·σ(b) with ONE reciprocal (3 quarter-rate transcendentals instead of 4, on
+// the chains' critical path): with E1 = e^-2a, E2 = e^-b, R = 1/((1+E1)(1+E2)):
+// σ(b) = (1+E1)·R, z = (1-E1)·R.  a ≥ -20 and b ≥ -40 keep the product finite (tanh(-20) = -1 in
+// f32; σ(-40) = 4e-18 stands for anything smaller, with z consistent with it).
+LBWN_DEV float gate_zs(float a, float b, float& s) {
+  const float e1 = __expf(-2.0f * fmaxf(a, -20.0f)), e2 = __expf(-fmaxf(b, -40.0f));
+  const float p = 1.0f + e1, rr = __builtin_amdgcn_rcpf(p * (1.0f + e2));
+  s = p * rr;
+  return (1.0f - e1) * rr;
+}
+LBWN_DEV float gate_z(float a, float b) {
+  float s;
+  return gate_zs(a, b, s);
+}
 
 // Host-side error plumbing (defined in capi.cpp).
 void lbwn_set_error(const char* fmt, ...);

@@ -327,7 +327,7 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->oLOG = carve(cur, sizeof(float) * (size_t)M * p->Q);
   p->oDH = carve(cur, sizeof(float) * (size_t)M * p->Cp);
   p->oDS = carve(cur, sizeof(float) * (size_t)M * p->Cs);
-  p->oDZ = carve(cur, sizeof(float) * (size_t)M * ldz);
+  p->oDZ = carve(cur, sizeof(float) * (size_t)m32(M) * ldz);   // chain order (x3 chain): whole 32-row blocks
   for (int i = 0; i < 2; ++i) {
     p->oGA[i] = carve(cur, sizeof(float) * (size_t)M * p->Cr);
     p->oGC0[i] = carve(cur, sizeof(float) * (size_t)M * p->Cr);
@@ -829,10 +829,13 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   Probe(p, st, "ds");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
   Probe::end(p, st, "ds");
-  // dZ = dS·SKIPcatᵀ
+  // dZ = dS·SKIPcatᵀ; for the bf16-split chain in its row-load order (1-KiB runs per load
+  // instruction instead of one 16-B piece per row)
+  const bool dz_chain = p->chain && p->fwd_x3 && lbwn_gemm_mode() == 1;
   g = gemm0();
   g.A = DS; g.lda = Cs; g.B = P->skip; g.ldb = Cs; g.C = DZ; g.ldc = ldz; g.M = (int)M; g.N = (int)ldz; g.K = Cs;
   g.b3 = w3(p, ws, W3_SKIP_B);
+  if (dz_chain) g.c_chain_ls = m32(M) * 32;
   Probe(p, st, "dz");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
   Probe::end(p, st, "dz");
@@ -934,6 +937,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     c.X = X; c.xls = p->x_layer_stride; c.DZ = DZ; c.ldz = ldz; c.wpack = WPK; c.ids = ids;
     if (p->fwd_x3 && lbwn_gemm_mode() == 1) {   // bf16-split backward: no gate recompute (SG)
       c.Z = Z; c.SG = at<float>(ws, p->oSG); c.sgls = m32(M) * 32; c.bimg = at<float>(ws, p->oWPKB);
+      c.dzls = m32(M) * 32;   // dZ in chain order (the dZ GEMM above)
     }
     c.slab = SLABS; c.ocg = at<float>(ws, p->oOCG); c.ocls = M * 32;
     c.gc_tab = cd.gc_tab; c.gc_ld = cd.gc_ld; c.cond = cd.cond; c.ldcond = cd.ldcond;

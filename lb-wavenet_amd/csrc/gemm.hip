@@ -9,6 +9,7 @@
 // v_mfma_f32_32x32x2_f32.  In the latter the LDS image follows the global layout (no
 // transposing stage), and the MFMA k-order is permuted so a k-contiguous operand feeds four
 // MFMA steps from one ds_read_b128: at step j of an 8-deep group, lane half h uses k = 8g+4h+j.
+#include <type_traits>
 #include <stdlib.h>
 #include <string.h>
 
@@ -286,12 +287,12 @@ template <bool KC, bool KFULL, int ROWS, int NTHR>
 struct X3Stage {
   static constexpr int NQ = (2 * ROWS + NTHR - 1) / NTHR;          // MN: 4×4 blocks per thread
   static constexpr int NV = KC ? ROWS * 8 / NTHR : 4 * NQ;
-  floatx4 v[NV];
+  floatx4 v[2][NV];     // two payload sets (the 2-stage kernel keeps two k-steps in flight)
   const float* p[NV];   // KC: row pointers at the split's first k; MN: k-row pointers
   long step;            // floats per k-step
   int kq;               // 4·(tid%8): this thread's k offset in the step
   int kz;               // the split's first k
-  unsigned okm;         // !KFULL: bit i = k in range (zeroed at store time, not at load)
+  unsigned okm[2];      // !KFULL: bit i = k in range (zeroed at store time, not at load)
   LBWN_DEV static bool mine(int tid, int q) { return KC || tid + NTHR * q < 2 * ROWS; }
   LBWN_DEV void init(const float* __restrict__ P, long ld, int mn0, int MN, int kz0, int tid) {
     kq = 4 * (tid & 7);
@@ -309,34 +310,37 @@ struct X3Stage {
   }
   // k-step t of the split ending at kend (kend read only when !KFULL); a clamped index keeps
   // every load unconditional
+  template <int S = 0>
   LBWN_DEV void load(int t, int kend) {
-    okm = ~0u;
+    okm[S] = ~0u;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       if (KFULL) {
-        v[i] = *(const floatx4*)(p[i] + t * step);
+        v[S][i] = *(const floatx4*)(p[i] + t * step);
       } else {
         const int k = kz + t * X3_BK + kq + (KC ? 0 : (i & 3));       // this value's first k
         const int kc = KC ? min(k, kend - 4) : min(k, kend - 1);
         const long dk = kc - (kz + kq + (KC ? 0 : (i & 3)));           // k offset from p[i]
-        v[i] = *(const floatx4*)(p[i] + (KC ? dk : dk * (step / X3_BK)));
-        if (k >= kend) okm &= ~(1u << i);
+        v[S][i] = *(const floatx4*)(p[i] + (KC ? dk : dk * (step / X3_BK)));
+        if (k >= kend) okm[S] &= ~(1u << i);
       }
     }
   }
+  template <int S = 0>
   LBWN_DEV floatx4 val(int i) const {
-    return (KFULL || ((okm >> i) & 1)) ? v[i] : (floatx4){0.f, 0.f, 0.f, 0.f};
+    return (KFULL || ((okm[S] >> i) & 1)) ? v[S][i] : (floatx4){0.f, 0.f, 0.f, 0.f};
   }
+  template <int S = 0>
   LBWN_DEV void store(unsigned short* lds, int tid, bool relu) {
     if (KC) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) x3_store4(lds + ((tid >> 3) + (NTHR / 8) * i) * X3_ROW, kq, val(i), relu);
+      for (int i = 0; i < NV; ++i) x3_store4(lds + ((tid >> 3) + (NTHR / 8) * i) * X3_ROW, kq, val<S>(i), relu);
     } else {
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
         if (!mine(tid, q)) continue;
         const int b = tid + NTHR * q;
-        const floatx4 r0 = val(4 * q), r1 = val(4 * q + 1), r2 = val(4 * q + 2), r3 = val(4 * q + 3);
+        const floatx4 r0 = val<S>(4 * q), r1 = val<S>(4 * q + 1), r2 = val<S>(4 * q + 2), r3 = val<S>(4 * q + 3);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           floatx4 t = {r0[j], r1[j], r2[j], r3[j]};
@@ -351,7 +355,7 @@ struct X3Stage {
 template <int ROWS, int NTHR>
 struct X3Pre {
   static constexpr int NV = ROWS * 12 / NTHR;
-  uintx4 v[NV];
+  uintx4 v[2][NV];
   const unsigned short* p[NV];
   int ldst[NV];
   LBWN_DEV void init(const unsigned short* __restrict__ P3, int kchunks, int mn0, int MN, int kz0, int tid) {
@@ -362,13 +366,15 @@ struct X3Pre {
       ldst[i] = r * X3_ROW + 8 * part;
     }
   }
+  template <int S = 0>
   LBWN_DEV void load(int t) {
 #pragma unroll
-    for (int i = 0; i < NV; ++i) v[i] = *(const uintx4*)(p[i] + t * (3 * X3_BK));
+    for (int i = 0; i < NV; ++i) v[S][i] = *(const uintx4*)(p[i] + t * (3 * X3_BK));
   }
+  template <int S = 0>
   LBWN_DEV void store(unsigned short* lds) {
 #pragma unroll
-    for (int i = 0; i < NV; ++i) *(uintx4*)(lds + ldst[i]) = v[i];
+    for (int i = 0; i < NV; ++i) *(uintx4*)(lds + ldst[i]) = v[S][i];
   }
 };
 
@@ -410,7 +416,10 @@ LBWN_DEV void x3_epilogue_rows(const lbwn_gemm_args& g, floatx16 (&acc)[MI][2], 
           if (g.accumulate) v += cv[r];
         }
         if (row < g.M) {
-          C[(long)row * g.ldc + col] = v;
+          if (g.c_chain_ls)   // the chain's order: [col/32][row/32][(col/8)%4][row%32][(col/4)%2][4]
+            C[(col >> 5) * g.c_chain_ls + ((((long)(row >> 5) * 4 + ((col >> 3) & 3)) * 32 + (row & 31)) * 8 + (col & 7))] = v;
+          else
+            C[(long)row * g.ldc + col] = v;
           cs[ni] += v;
         }
       }
@@ -485,17 +494,19 @@ __global__ __launch_bounds__(128 * WM, (WM == 2 && STAGES == 1) ? X3_OCC : 1) vo
   const int fi = lane & 31, fh = lane >> 5;
   const int fa_off = (wm * 64 + fi) * X3_ROW + 8 * fh, fb_off = (wn * 64 + fi) * X3_ROW + 8 * fh;
 
-  // one 16-deep chunk c of the k-step held in slot `base`: 12 fragment reads, 24 MFMAs
-  auto chunk = [&](const unsigned short* base, int c) {
-    bf16x8 fa[MI][3], fb[NI][3];
+  // one 16-deep chunk c of the k-step held in slot `base`: 12 fragment reads, then 24 MFMAs
+  using Frags = bf16x8[MI + NI][3];
+  auto frags = [&](const unsigned short* base, int c, Frags& f) {
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi) fa[mi][p] = *(const bf16x8*)(base + fa_off + mi * 32 * X3_ROW + 32 * p + 16 * c);
+      for (int mi = 0; mi < MI; ++mi) f[mi][p] = *(const bf16x8*)(base + fa_off + mi * 32 * X3_ROW + 32 * p + 16 * c);
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni)
-        fb[ni][p] = *(const bf16x8*)(base + BM * X3_ROW + fb_off + ni * 32 * X3_ROW + 32 * p + 16 * c);
+        f[MI + ni][p] = *(const bf16x8*)(base + BM * X3_ROW + fb_off + ni * 32 * X3_ROW + 32 * p + 16 * c);
     }
+  };
+  auto mfmas = [&](const Frags& f) {
     // small terms first: a2b0, a1b1, a0b2, a1b0, a0b1, a0b0
 #pragma unroll
     for (int q = (X3_EXP == 2 ? 5 : 0); q < 6; ++q) {
@@ -504,8 +515,13 @@ __global__ __launch_bounds__(128 * WM, (WM == 2 && STAGES == 1) ? X3_OCC : 1) vo
       for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[mi][PA[q]], fb[ni][PB[q]], acc[mi][ni], 0, 0, 0);
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[mi][PA[q]], f[MI + ni][PB[q]], acc[mi][ni], 0, 0, 0);
     }
+  };
+  auto chunk = [&](const unsigned short* base, int c) {
+    Frags f;
+    frags(base, c, f);
+    mfmas(f);
   };
   auto stage_store = [&](unsigned short* base) {
     sa.store(base, tid, relu_a);
@@ -528,15 +544,42 @@ __global__ __launch_bounds__(128 * WM, (WM == 2 && STAGES == 1) ? X3_OCC : 1) vo
       __syncthreads();
     }
   } else {
-    // the prologue stored k-step 0 into slot 0; the registers now take k-step 1
-    if (ntiles > 1) stage_load(1);
-    for (int kt = 0; kt < ntiles; ++kt) {
+    // Two LDS slots and two register sets: k-step j's global loads land in set j & 1 two
+    // k-steps ahead of its LDS store (a lead of ~2 k-steps of MFMA time against the L2/HBM
+    // latency; one step of lead left the waves ~50 % parked on vmcnt): step 2.49 -> 2.41 ms
+    // (same box, tools/gemm_ab.sh).  Reading chunk 1's fragments at the step start as well
+    // (256 VGPRs) measured 2.53.  The prologue stored k-step 0 into slot 0 from set 0.
+    // Every load and store of the loop is unconditional (k-steps past the end re-load the last
+    // one, stores of them go to the idle slot): a guarded load made hipcc wait for all loads in
+    // flight (its counts cannot assume the guarded ones were issued).
+    const int last = max(ntiles - 1, 0);
+    auto step = [&](int kt, auto sset) {
+      constexpr int S = decltype(sset)::value;   // = (kt + 1) & 1
       const unsigned short* cur = smem + (kt & 1) * SLOT;
-      chunk(cur, 0);
-      if (kt + 1 < ntiles) stage_store(smem + ((kt + 1) & 1) * SLOT);
-      if (kt + 2 < ntiles) stage_load(kt + 2);
-      chunk(cur, 1);
+      Frags f0, f1;
+      frags(cur, 0, f0);
+      mfmas(f0);
+      unsigned short* nxt = smem + ((kt + 1) & 1) * SLOT;
+      sa.template store<S>(nxt, tid, relu_a);
+      if (BPRE) sp.template store<S>(nxt + BM * X3_ROW); else sb.template store<S>(nxt + BM * X3_ROW, tid, false);
+      const int kl = min(kt + 3, last);
+      sa.template load<S>(kl, kz1);
+      if (BPRE) sp.template load<S>(kl); else sb.template load<S>(kl, kz1);
+      frags(cur, 1, f1);
+      mfmas(f1);
       __syncthreads();
+    };
+    if (ntiles > 0) {
+      sa.template load<1>(min(1, last), kz1);
+      if (BPRE) sp.template load<1>(min(1, last)); else sb.template load<1>(min(1, last), kz1);
+      sa.template load<0>(min(2, last), kz1);
+      if (BPRE) sp.template load<0>(min(2, last)); else sb.template load<0>(min(2, last), kz1);
+      int kt = 0;
+      for (; kt + 1 < ntiles; kt += 2) {
+        step(kt, std::integral_constant<int, 1>());
+        step(kt + 1, std::integral_constant<int, 0>());
+      }
+      if (kt < ntiles) step(kt, std::integral_constant<int, 1>());
     }
   }
 
@@ -639,6 +682,9 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
                    hipStream_t st) {
   LBWN_REQUIRE(a.a_codes == nullptr, "gemm (bf16 split): one-hot A not supported");
   LBWN_REQUIRE(a.colpart == nullptr || split_k <= 1, "gemm (bf16 split): column partials need split_k = 1");
+  LBWN_REQUIRE(!a.c_chain_ls || (split_k <= 1 && !a.accumulate && !a.mask && a.N % 32 == 0 &&
+                                 a.c_chain_ls >= (a.M + 31L) / 32 * 32 * 32),
+               "gemm (bf16 split): chain-order C needs split_k = 1, no accumulate/mask, N %% 32 == 0");
   LBWN_REQUIRE(a.b3 == nullptr || (a.K % X3_BK == 0 && (((uintptr_t)a.b3) & 15) == 0),
                "gemm (bf16 split): pre-split B needs K %% 32 == 0 and 16-B alignment");
   // 256-row tiles (8 waves, 2-stage pipeline) for the tall k-contiguous products with N <= 2048
@@ -699,8 +745,8 @@ int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int 
                      hipStream_t st) {
   if (lbwn_gemm_mode() == 1 && a.a_codes == nullptr && a.K >= 4 && a.M >= 4 && a.N >= 4)
     return gemm_launch_x3(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
-  LBWN_REQUIRE(a.colpart == nullptr && a.step_advance == nullptr,
-               "gemm: column partials / the step counter need the bf16-split form");
+  LBWN_REQUIRE(a.colpart == nullptr && a.step_advance == nullptr && !a.c_chain_ls,
+               "gemm: column partials / the step counter / chain-order C need the bf16-split form");
   return gemm_launch_t<16, 128, 128>(a, a_kcontig, b_kcontig, split_k, slab_ws, st);
 }
 

@@ -215,7 +215,7 @@ __global__ __launch_bounds__(512) void gen_wave_kernel(WaveK a) {
     v += dpp<DPP_XOR2>(v);
     v += bco;                                      // conv output o (+ bias + GC term)
     const float vp = dpp<DPP_HALF_MIRROR>(v);      // the partner output (sig <-> gate, same channel)
-    const float z = tanhf_(sg ? vp : v) * sigmoidf_(sg ? v : vp);
+    const float z = gate_z(sg ? vp : v, sg ? v : vp);
     float* Zl = Z + (l & 1) * 32;
     if (lead) {
       Zl[ch] = z;
@@ -789,7 +789,7 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm) {
       v += dpp<DPP_XOR2>(v);
       v += bco;
       const float vp = dpp<DPP_HALF_MIRROR>(v);
-      const float z = tanhf_(sg ? vp : v) * sigmoidf_(sg ? v : vp);
+      const float z = gate_z(sg ? vp : v, sg ? v : vp);
       float* Zl = Z + (l & 1) * 32;
       if (lead) {
         Zl[ch] = z;

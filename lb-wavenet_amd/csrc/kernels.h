@@ -19,6 +19,10 @@ struct lbwn_gemm_args {
   // lbwn_colsum_final_launch: the bias gradient without a second pass over C
   float* colpart;
   long long* step_advance;   // nullable, bf16-split form only: block 0 adds 1 (the per-step generator's counter)
+  // bf16-split form, no split-K / accumulate / mask: > 0 stores C in the backward chain's row-load
+  // order instead of rows (ldc unused): 32-column block j at C + j·c_chain_ls, element (m, c) at
+  // sg_off(m, c / 8, (c / 4) & 1) + c % 4 (layer.hip), so the chain's own-row loads are 1-KiB runs
+  long c_chain_ls;
   int k_per_split;     // set by the launcher
   long split_stride;   // set by the launcher
 };
@@ -115,7 +119,8 @@ struct lbwn_chain_args {
   int B, T, H, L, nbl, Cr, Cd;
   int grid;                    // ≤ blocks resident at once (rounds of tiles)
   // backward only
-  const float* DZ;             // dZ (row stride ldz)
+  const float* DZ;             // dZ (row stride ldz), or in chain order (dzls > 0, bf16-split chain)
+  long dzls = 0;               // chain order: layer stride of DZ (lbwn_gemm_args::c_chain_ls)
   float* slab;                 // [L][ntiles][slab_stride]
   float* ocg; long ocls;       // out_c0 hand-off rows per layer [L][B·T][32]
   float* dx0_a; float* dx0_c;  // layer 0's dx parts [B·T][32]

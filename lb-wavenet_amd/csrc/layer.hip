@@ -705,6 +705,18 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
     }
     const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && tile == (int)blockIdx.x;
 #define FSTAMP(i) if (trc) a.trace[16 * l + (i)] = clock64()
+    // z (skip GEMM input) and σ rows of layer l-1, stored during layer l (LBWN_ABL 2048 variant)
+    constexpr bool DEFER_ZS = (LBWN_ABL & 2048) != 0;
+    floatx16 zk, sk;
+    auto store_zs = [&](int ll, const floatx16& zz, const floatx16& ss) {
+      if (valid) store_rows16(a.Z + m * a.ldz + (long)ll * a.Cd, zz, a.Cd, h);
+      if (X3 && a.SG && valid) {
+        float* sgl = a.SG + (long)ll * a.sgls;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *(floatx4*)(sgl + sg_off(m, q, h)) = floatx4{ss[4 * q], ss[4 * q + 1], ss[4 * q + 2], ss[4 * q + 3]};
+      }
+    };
     for (int l = 0; l < a.L; ++l) {
       FSTAMP(0);
       const int d = 1 << (l % a.nbl);
@@ -770,6 +782,7 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
 #pragma unroll
         for (int s2 = 0; s2 < 16; ++s2) ra[s2] = Rs[acc_row(s2, h) * XS + pi];
       }
+      if (DEFER_ZS && l > 0) store_zs(l - 1, zk, sk);
       __builtin_amdgcn_sched_barrier(0);
       // 5. dilated tap W0·x[t-d], gate
       const float* xp = (r >= d) ? cur + (r - d) * XS : HALO + r * XS;
@@ -778,8 +791,9 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
       floatx16 z, sgv;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        sgv[q] = sigmoidf_(acc_g[q]);
-        z[q] = tanhf_(acc_s[q]) * sgv[q];
+        float sq;
+        z[q] = gate_zs(acc_s[q], acc_g[q], sq);
+        sgv[q] = sq;
       }
       FSTAMP(4);
       if (l + 1 < a.L) {
@@ -811,14 +825,18 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
         const __amdgpu_buffer_rsrc_t rn =
             __builtin_amdgcn_make_buffer_rsrc(xn, (short)0, (int)((long)(a.H + a.T) * 32 * 4), BUF_DW3);
         float* nrow = nxt + r * XS;
+        // only the rows the next layer's consumer tile reads (the last min(d_{l+1}, LP)) cross
+        // CUs inside this launch: those are written through (sc1) and drained before the publish;
+        // the rest are plain stores, read after the launch (backward, SAVE).  Writing every row
+        // through cost ~3k cycles per layer (drain 2.4k + slower issue; tools/fwd_abl.sh)
+        const bool halo_row = r >= LP - min(1 << ((l + 1) % a.nbl), LP);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const floatx4 v = floatx4{acc_r[4 * q], acc_r[4 * q + 1], acc_r[4 * q + 2], acc_r[4 * q + 3]};
           *(floatx4*)(nrow + 8 * q + 4 * h) = v;
-          // (LBWN_ABL 256 / 1024: timing-only ablations of the non-halo rows' stores / of sc1)
-          const bool abl_skip = (LBWN_ABL & 256) && r < LP - min(1 << ((l + 1) % a.nbl), LP);
-          if (valid && !abl_skip)
-            __builtin_amdgcn_raw_buffer_store_b128(v, rn, ((a.H + t) * 32 + 8 * q + 4 * h) * 4, 0, (LBWN_ABL & 1024) ? 0 : 16);
+          const int off = ((a.H + t) * 32 + 8 * q + 4 * h) * 4;
+          if (valid && halo_row) __builtin_amdgcn_raw_buffer_store_b128(v, rn, off, 0, 16);
+          if (valid && !halo_row) __builtin_amdgcn_raw_buffer_store_b128(v, rn, off, 0, 0);
         }
         FSTAMP(8);
         // 7. the next layer's own tap from the row this wave just wrote (wave-local: no barrier)
@@ -853,16 +871,15 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
       FSTAMP(6);
       // 10. z (skip GEMM input) and σ rows, issued last: they drain in the shadow of the next
       //     layer (written before the image, the image writes' vmcnt waits waited them out)
-      if (valid && !(LBWN_ABL & 512)) store_rows16(a.Z + m * a.ldz + (long)l * a.Cd, z, a.Cd, h);
-      if (LBWN_ABL & 512) asm volatile("" ::"v"(z[0]), "v"(z[15]), "v"(sgv[0]), "v"(sgv[15]));
-      if (X3 && a.SG && valid && !(LBWN_ABL & 512)) {
-        float* sgl = a.SG + (long)l * a.sgls;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          *(floatx4*)(sgl + sg_off(m, q, h)) = floatx4{sgv[4 * q], sgv[4 * q + 1], sgv[4 * q + 2], sgv[4 * q + 3]};
+      if (DEFER_ZS) {
+        zk = z;
+        sk = sgv;
+      } else {
+        store_zs(l, z, sgv);
       }
       FSTAMP(7);
     }
+    if (DEFER_ZS) store_zs(a.L - 1, zk, sk);
 #undef FSTAMP
   }
 }
@@ -929,7 +946,7 @@ LBWN_DEV void slab_group_prefetch(const RedK& a, int grp, float (&pre)[RED_PARTS
 // Weight-gradient partials go to slab[l][tile] (summed by layer_reduce_all_kernel).
 struct ChainBK {
   const float* X; long xls;
-  const float* DZ; long lddz;
+  const float* DZ; long lddz; long dzls;   // dzls > 0: DZ in chain order (sg_off blocks per layer)
   const float* wpack;
   float* slab;                 // [L][ntiles][SLAB]
   float* ocg; long ocls;       // out_c0 hand-off rows: [L][B·T][32], layer stride ocls floats
@@ -1503,7 +1520,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
     auto load_regs = [&](int l) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        dzr[q] = *(const floatx4*)(a.DZ + mc * a.lddz + (long)l * 32 + 8 * q + 4 * h);
+        dzr[q] = *(const floatx4*)(a.DZ + l * a.dzls + sg_off(mc, q, h));   // chain order: 1-KiB runs
         zr[q] = *(const floatx4*)(a.Zf + mc * a.lddz + (long)l * 32 + 8 * q + 4 * h);
         sgr[q] = *(const floatx4*)(a.SG + (long)l * a.sgls + sg_off(mc, q, h));
       }
@@ -2251,7 +2268,7 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   LBWN_REQUIRE(c.grid >= 1 && c.flags && c.status && c.slab && c.ocg && c.dx0_a && c.dx0_c && c.DZ,
                "chain bwd: bad launch state");
   ChainBK k;
-  k.X = c.X; k.xls = c.xls; k.DZ = c.DZ; k.lddz = c.ldz; k.wpack = c.wpack; k.slab = c.slab;
+  k.X = c.X; k.xls = c.xls; k.DZ = c.DZ; k.lddz = c.ldz; k.dzls = c.dzls; k.wpack = c.wpack; k.slab = c.slab;
   k.ocg = c.ocg; k.ocls = c.ocls; k.dx0_a = c.dx0_a; k.dx0_c = c.dx0_c;
   k.gc_tab = c.gc_tab; k.gc_ld = c.gc_ld; k.ids = c.ids; k.cond = c.cond; k.ldcond = c.ldcond;
   k.dv_out = c.dv_out; k.lddv = c.lddv; k.gc_dtab = c.gc_dtab;
@@ -2265,6 +2282,7 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   const int tps = (c.T + LP - 1) / LP;
   // hand-off flags only: the status word is sticky for the whole step
   if (!c.flags_zeroed) LBWN_HIP(hipMemsetAsync(c.flags, 0, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st));
+  LBWN_REQUIRE(x3 == (c.dzls > 0), "chain bwd: the bf16-split chain reads dZ in chain order (dzls), the f32 chain in rows");
   if (x3) chain_bwd_x3_kernel<<<c.grid, 256, 0, st>>>(k);
   else chain_bwd_kernel<<<c.grid, 256, 0, st>>>(k);
   LBWN_CHECK_LAUNCH();

@@ -7,6 +7,5 @@ for A in "$@"; do
   export LBWN_LIB=lb-wavenet_amd/lbwn/abl/liblbwn_abl$A.so
   echo "== LBWN_ABL=$A"
   timeout -k 10 120 python tools/chain_trace.py 1 > gpurun_out/fabl_$A.txt 2>&1 || { echo "trace $A failed"; tail gpurun_out/fabl_$A.txt; exit 1; }
-  sed -n '/chain_fwd/,/drain/p' gpurun_out/fabl_$A.txt
-  timeout -k 10 120 python tools/kbench.py --iters 4 --probes layer_fwd@25 2>&1 | grep -v amdgpu.ids | tail -2 || { echo "kbench $A failed"; exit 1; }
+  grep -v amdgpu.ids gpurun_out/fabl_$A.txt | sed -n '1,12p'
 done
