@@ -691,6 +691,7 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
   // (skip fwd, post1/post2 fwd, dH1, dS: 3-8 % faster; dZ, N = 1600: step -0.5 % in a same-box
   // A/B since the epilogue and split changes); 128-row tiles at 2 blocks per CU for the rest
   // (the mn-contiguous weight gradients: 1.3-1.5x slower on 256-row tiles)
+  // (256-row tiles for dSKIP too, with the 2-deep staging: 341 -> 476 us)
   const int wm = (a.colpart || (a_kcontig && a.N <= 2048 && a.M >= 8192)) ? 4 : 2;
   lbwn_gemm_args g;
   dim3 grid;

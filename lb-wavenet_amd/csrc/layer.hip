@@ -705,9 +705,6 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
     }
     const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && tile == (int)blockIdx.x;
 #define FSTAMP(i) if (trc) a.trace[16 * l + (i)] = clock64()
-    // z (skip GEMM input) and σ rows of layer l-1, stored during layer l (LBWN_ABL 2048 variant)
-    constexpr bool DEFER_ZS = (LBWN_ABL & 2048) != 0;
-    floatx16 zk, sk;
     auto store_zs = [&](int ll, const floatx16& zz, const floatx16& ss) {
       if (valid) store_rows16(a.Z + m * a.ldz + (long)ll * a.Cd, zz, a.Cd, h);
       if (X3 && a.SG && valid) {
@@ -782,7 +779,6 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
 #pragma unroll
         for (int s2 = 0; s2 < 16; ++s2) ra[s2] = Rs[acc_row(s2, h) * XS + pi];
       }
-      if (DEFER_ZS && l > 0) store_zs(l - 1, zk, sk);
       __builtin_amdgcn_sched_barrier(0);
       // 5. dilated tap W0·x[t-d], gate
       const float* xp = (r >= d) ? cur + (r - d) * XS : HALO + r * XS;
@@ -871,15 +867,11 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
       FSTAMP(6);
       // 10. z (skip GEMM input) and σ rows, issued last: they drain in the shadow of the next
       //     layer (written before the image, the image writes' vmcnt waits waited them out)
-      if (DEFER_ZS) {
-        zk = z;
-        sk = sgv;
-      } else {
-        store_zs(l, z, sgv);
-      }
+      // (stored during the next layer instead, after its halo barrier, they lengthened that
+      // layer's publish drain: forward 276 -> 287 us, same box)
+      store_zs(l, z, sgv);
       FSTAMP(7);
     }
-    if (DEFER_ZS) store_zs(a.L - 1, zk, sk);
 #undef FSTAMP
   }
 }
