@@ -62,12 +62,13 @@ def chain_fwd_latency_floor(arch, B, T, clock_ghz=2.4, ncu=256):
         workgroup barriers (20 cyc each, taken) and the halo LDS write/read (2 x 50);
       * the dilated tap: 2 k-steps x 2 (sig, gate) x 6 split products = 24 v_mfma_f32_32x32x16_bf16
         at 32 cyc; the residual 12 of them; the gate 16 x (exp, rcp, exp, rcp) at 8 cyc issue
-        + 6 VALU at 4 = 16 x 56; splitting z into bf16 terms 16 x 22 cyc (5.5 VALU each).
+        + 6 VALU at 4 = 16 x 56 (one reciprocal since round 3: exp, exp, rcp + 6 VALU = 16 x 48);
+        splitting z into bf16 terms 16 x 22 cyc (5.5 VALU each).
     Rounds: tiles beyond one per CU run as further rounds of the whole chain."""
     from lbwn.arch import n_layers
     L = n_layers(arch)
     handoff = 332 + 0.3 * clock_ghz * 1e3 + 500 + 2 * 20 + 2 * 50
-    compute = 24 * 32 + 12 * 32 + 16 * 56 + 16 * 22
+    compute = 24 * 32 + 12 * 32 + 16 * 48 + 16 * 22
     layer = handoff + compute
     tiles = B * ((T + 127) // 128)
     rounds = (tiles + ncu - 1) // ncu
