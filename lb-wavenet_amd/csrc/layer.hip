@@ -977,8 +977,14 @@ LBWN_DEV void gc_scatter(float* gtab, long ld, const int* ids_b, const float* DV
     float s = 0.f;
     for (int p = 0; p < nv; ++p) s += dvw[p * DS + o];
     atomicAdd(gtab + (long)id0 * ld + col, s);
-  } else {
-    for (int p = 0; p < nv; ++p) atomicAdd(gtab + (long)idw[p] * ld + col, dvw[p * DS + o]);
+  } else {   // one atomic per run of equal ids (as gc_scatter_x3)
+    int p = 0;
+    while (p < nv) {
+      const int id = idw[p];
+      float s = 0.f;
+      for (; p < nv && idw[p] == id; ++p) s += dvw[p * DS + o];
+      atomicAdd(gtab + (long)id * ld + col, s);
+    }
   }
 }
 
@@ -1468,7 +1474,15 @@ LBWN_DEV void gc_scatter_x3(float* gtab, long ld, const int* ids_b, const float*
     for (int p = 0; p < nv; ++p) s += pl[swz(32 * w + p, oc)];
     atomicAdd(gtab + (long)id0 * ld + col, s);
   } else {
-    for (int p = 0; p < nv; ++p) atomicAdd(gtab + (long)idw[p] * ld + col, pl[swz(32 * w + p, oc)]);
+    // voice ids change only at file boundaries: one atomic per run of equal ids (a position-wise
+    // atomic loop made the arch5 chain 2x slower on batches with a boundary inside a tile)
+    int p = 0;
+    while (p < nv) {
+      const int id = idw[p];
+      float s = 0.f;
+      for (; p < nv && idw[p] == id; ++p) s += pl[swz(32 * w + p, oc)];
+      atomicAdd(gtab + (long)id * ld + col, s);
+    }
   }
 }
 
