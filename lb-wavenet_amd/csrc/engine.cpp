@@ -35,6 +35,7 @@ struct lbwn_plan {
   size_t oPADP = 0, oPADG = 0;
   int ctrace_blk = -1;            // LBWN_CHAIN_TRACE=<block>: chain cycle stamps (debug)
   size_t oGCTAB, oGCD, oGCPART, oLCACT[8], oCOND, oDVALL, oLCCAT, oDLCCAT, oDLC[2];
+  size_t oTGID = 0;              // GC + chain: per-tile uniform voice id (lbwn_gc_tile_sum_launch)
   // in-chain LC (bf16-split forward chain): L split LC images; COND is then computed only when a
   // backward path needs it (cond_valid: this step's COND is in the workspace)
   size_t oLCX = 0;
@@ -203,7 +204,7 @@ int head_pad_params(const lbwn_plan* p, const lbwn_params* P, void* ws, lbwn_par
   HeadPad h = head_pad_layout(p, reinterpret_cast<float*>(static_cast<char*>(ws) + p->oPADP));
   const size_t L = p->L, Cd = p->Cd, Cs = p->Cs, Cp = p->Cp, Q = p->Q, cs = p->Cs_ref, cp = p->Cp_ref;
   if (copy) {
-    LBWN_HIP(hipMemsetAsync(h.skip, 0, sizeof(float) * head_pad_floats(p), st));
+    if (int e = lbwn_zero_launch(h.skip, sizeof(float) * head_pad_floats(p), st)) return e;
     int e;
     if ((e = copy2d(h.skip, Cs, P->skip, cs, cs, L * Cd, st))) return e;
     if ((e = copy2d(h.skip_b, Cs, P->skip_b, cs, cs, L, st))) return e;
@@ -361,6 +362,7 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     const long ncond = 2L * L * p->Cd;
     p->oGCTAB = p->Ge ? carve(cur, f * (size_t)L * p->ncat1 * 2 * p->Cd) : 0;
     p->oGCD = p->Ge ? carve(cur, f * (size_t)L * p->ncat1 * 2 * p->Cd) : 0;
+    p->oTGID = p->Ge ? carve(cur, sizeof(int) * (size_t)B * ((T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS)) : 0;
     p->oGCPART = p->Ge ? carve(cur, f * (size_t)lbwn_gc_part_floats(L, p->Ge, p->Cd)) : 0;
     long rows = (long)B * (T / hop);
     for (int i = 0; i < 8; ++i) {
@@ -653,7 +655,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   P = &Ppad;
   // the sticky status word (chain spin timeouts OR their codes in) lives for one step:
   // zeroed here, read by the host after the step (lbwn_plan_tensor "status")
-  LBWN_HIP(hipMemsetAsync(at<char>(ws, p->oSTATUS), 0, 16 + 2 * p->nflag_bytes, st));
+  if ((e = lbwn_zero_launch(at<char>(ws, p->oSTATUS), 16 + 2 * p->nflag_bytes, st))) return e;
   p->bwd_flags_fresh = true;
   const int L = p->L, B = p->B, T = p->T, H = p->H, Cr = p->Cr, Cd = p->Cd;
   const long M = p->M, ldz = (long)L * Cd;
@@ -909,7 +911,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     cd.gc_tab = at<float>(ws, p->oGCTAB);
     cd.gc_ld = 2L * L * Cd;
     cd.gc_dtab = at<float>(ws, p->oGCD);
-    LBWN_HIP(hipMemsetAsync(cd.gc_dtab, 0, sizeof(float) * (size_t)L * p->ncat1 * 2 * Cd, st));
+    if ((e = lbwn_zero_launch(cd.gc_dtab, sizeof(float) * (size_t)L * p->ncat1 * 2 * Cd, st))) return e;
   }
   if (p->Lo > 0) {
     // the bf16-split backward chain reads no conditioning; the f32 chain and the per-layer
@@ -938,6 +940,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     if (p->fwd_x3 && lbwn_gemm_mode() == 1) {   // bf16-split backward: no gate recompute (SG)
       c.Z = Z; c.SG = at<float>(ws, p->oSG); c.sgls = m32(M) * 32; c.bimg = at<float>(ws, p->oWPKB);
       c.dzls = m32(M) * 32;   // dZ in chain order (the dZ GEMM above)
+      if (cd.gc_dtab) c.tile_gid = at<int>(ws, p->oTGID);
     }
     c.slab = SLABS; c.ocg = at<float>(ws, p->oOCG); c.ocls = M * 32;
     c.gc_tab = cd.gc_tab; c.gc_ld = cd.gc_ld; c.cond = cd.cond; c.ldcond = cd.ldcond;
@@ -976,6 +979,8 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     Probe(p, rst, "layer_reduce");
     if ((e = lbwn_layer_reduce_all_launch(r, L, (long)ntiles * sstr, rst))) return e;
     Probe::end(p, rst, "layer_reduce");
+    if (c.tile_gid && (e = lbwn_gc_tile_sum_launch(SLABS, L, ntiles, c.tile_gid, cd.gc_dtab, cd.gc_ld, p->ncat1, rst)))
+      return e;
     if ((e = gc_backward(p, P, G, ws, rst))) return e;
     if (p->Lo > 0) {
       if ((e = lc_dlc(p, P, ws, SPL, st))) return e;

@@ -130,6 +130,7 @@ struct lbwn_chain_args {
   // forward chain (layer stride sgls floats), and the backward images (lbwn_pack_layers_bx3)
   float* SG = nullptr; long sgls = 0;
   const float* bimg = nullptr;
+  int* tile_gid = nullptr;     // x3 backward + GC: [ntiles] uniform voice id per tile or -1
   // forward, bf16-split form: in-chain LC term (instead of cond): LC input [M][Lo], split images
   const float* lcact = nullptr; const unsigned short* lcimg = nullptr; int Lo = 0;
 };
@@ -191,6 +192,10 @@ int lbwn_head_nblocks(long M);
 int lbwn_mulaw_encode_launch(const float* x, int* q, long n, int n_quanta, int tf32, hipStream_t st);
 int lbwn_mulaw_decode_launch(const int* q, float* x, long n, int n_quanta, hipStream_t st);
 int lbwn_bcast_rows_launch(float* dst, int L, int N, hipStream_t st);
+int lbwn_zero_launch(void* p, size_t n_bytes, hipStream_t st);
+// GC table gradient of the uniform-id tiles from the backward chain's slab bias partials
+int lbwn_gc_tile_sum_launch(const float* slab, int L, int ntiles, const int* tile_gid, float* gtab, long ld,
+                            int ncat1, hipStream_t st);
 
 // Conditioning (cond.hip)
 int lbwn_gc_table_launch(const float* emb, const float* wsig, const float* wgate, float* out, int L, int ncat1,

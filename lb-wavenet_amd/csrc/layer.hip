@@ -951,6 +951,7 @@ struct ChainBK {
   long long* trace; int trace_blk;   // debug stamps (null in production)
   // bf16-split form (chain_bwd_x3_kernel): z rows (row stride lddz), σ rows [L][M][32], images
   const float* Zf; const float* SG; long sgls; const float* bimg;
+  int* tile_gid;               // GC: per tile its uniform voice id or -1 (x3 chain), or null
 };
 
 // dv rows of wave w's 32 positions (DV, position-major) scatter-added into the GC gradient
@@ -1451,38 +1452,27 @@ LBWN_DEV floatx4 mfma16_x3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx4 a
   return acc;
 }
 
-// gc_scatter over the swizzled dv planes
-LBWN_DEV void gc_scatter_x3(float* gtab, long ld, const int* ids_b, const float* DVs, const float* DVg, int t0, int T,
-                            int w, int lane, int Cd, int uni_id) {
-  const int tw0 = t0 + 32 * w;
-  const int nv = min(32, T - tw0);
-  if (nv <= 0) return;
-  const int* idw = ids_b + tw0;
-  int id0 = uni_id;
-  if (id0 < 0) {
-    id0 = idw[0];
-    bool uni = true;
-    for (int p = 1; p < nv; ++p) uni &= (idw[p] == id0);
-    if (!uni) id0 = -1;
-  }
+// GC rows of a wave whose 32 positions are not one voice: dv column sums per run of equal ids
+// (ids change only at file boundaries), one atomic per run and column.  The runs come from the
+// lanes' own ids (lane p of either half holds position 32w + p; -1 past the end): run starts =
+// ballot of id changes, computed once per tile by the caller (`starts`, bit p = a run starts at
+// position p; `pid` = the lane's id).  No global loads: the old per-position loop loaded each id
+// inside the loop and waited on every one (arch5 backward chain 550 -> 900 us on such batches).
+LBWN_DEV void gc_scatter_x3(float* gtab, long ld, const float* DVs, const float* DVg, int w, int lane, int Cd,
+                            unsigned starts, int pid) {
   const int o = lane, oc = o & 31;
   const float* pl = o < 32 ? DVs : DVg;
-  if (oc >= Cd) return;
   const int col = o < 32 ? oc : Cd + oc;
-  if (id0 >= 0) {
+  unsigned rest = starts;
+  while (rest) {   // wave-uniform
+    const int p0 = __ffs(rest) - 1;
+    rest &= rest - 1;
+    const int p1 = rest ? __ffs(rest) - 1 : 32;
+    const int id = __shfl(pid, p0);
+    if (id < 0) continue;   // positions past T
     float s = 0.f;
-    for (int p = 0; p < nv; ++p) s += pl[swz(32 * w + p, oc)];
-    atomicAdd(gtab + (long)id0 * ld + col, s);
-  } else {
-    // voice ids change only at file boundaries: one atomic per run of equal ids (a position-wise
-    // atomic loop made the arch5 chain 2x slower on batches with a boundary inside a tile)
-    int p = 0;
-    while (p < nv) {
-      const int id = idw[p];
-      float s = 0.f;
-      for (; p < nv && idw[p] == id; ++p) s += pl[swz(32 * w + p, oc)];
-      atomicAdd(gtab + (long)id * ld + col, s);
-    }
+    for (int p = p0; p < p1; ++p) s += pl[swz(32 * w + p, oc)];
+    if (oc < Cd) atomicAdd(gtab + (long)id * ld + col, s);
   }
 }
 
@@ -1517,10 +1507,17 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
     const int wave_id = __shfl(myid, 0);
     const bool wave_uni = __all(!valid || myid == wave_id);
     // GC grads: a tile whose valid positions share one voice id (the common case: ids change only
-    // at file boundaries) adds the tile's dv column sums -- the bias partial sums, computed anyway --
-    // to that id's row: 64 atomics per layer instead of a per-wave pass over DV
+    // at file boundaries) contributes its dv column sums -- the bias partials in its slab, computed
+    // anyway -- to that id's row; lbwn_gc_tile_sum_launch adds them after the chain in tile order
+    // (tile_gid[tile] = the id, or -1: this chain scatters the tile's rows itself).  64 atomics
+    // per tile and layer onto the few voice rows serialised at L2 and stretched the publish drains.
     const int tile_id = a.gc_tab ? a.ids[mb + t0] : 0;
     const bool tile_uni = __syncthreads_and(!valid || myid == tile_id);
+    if (a.tile_gid && tid == 0) a.tile_gid[tile] = tile_uni ? tile_id : -1;
+    // this wave's id runs (gc_scatter_x3): lane pi's position id, -1 past T; bit p = a run starts at p
+    const int gc_pid = valid ? myid : -1;
+    const int gc_prev = __shfl(gc_pid, max(pi - 1, 0));
+    const unsigned gc_starts = (unsigned)(__ballot(h == 0 && (pi == 0 || gc_pid != gc_prev)) & 0xffffffffull);
     // per-layer rows of this lane's position: dZ, z, σ (issued a layer ahead)
     floatx4 dzr[4], zr[4], sgr[4];
     auto load_regs = [&](int l) {
@@ -1704,9 +1701,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
       if (tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
       // the next layer's weight image and rows are issued between the dSIG MFMAs below (landed
       // by the next layer's G build: vmcnt(0) + barrier)
-      if (a.gc_dtab && !tile_uni)
-        gc_scatter_x3(a.gc_dtab + (long)l * 64, a.gc_ld, a.ids + mb, DVs, DVg, t0, a.T, w, lane, 32,
-                      wave_uni ? wave_id : -1);
+      if (a.gc_dtab && !tile_uni) gc_scatter_x3(a.gc_dtab + (long)l * 64, a.gc_ld, DVs, DVg, w, lane, 32, gc_starts, gc_pid);
       XSTAMP(4);
       // 6. dSIG / dGATE partials of ALL four tiles t (0 sig·prev, 1 sig·cur, 2 gate·prev, 3
       //    gate·cur) over this wave's own 32 positions: A[i=in][k=pos] = X[pos][in], B[k][j=o] =
@@ -1802,7 +1797,6 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 #pragma unroll
         for (int pc = 0; pc < 8; ++pc) s1 += part[pc * 96 + tid];
         slab[5120 + tid] = s1;
-        if (a.gc_dtab && tile_uni && tid < 64) atomicAdd(a.gc_dtab + (long)tile_id * a.gc_ld + (long)l * 64 + tid, s1);
       }
       XSTAMP(12);
       // dSIG / dGATE: partial of tile t to slot (wave, t) of Xp..DVs (64 KiB, dead until the next
@@ -2252,7 +2246,9 @@ int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
                  LC_KP);
   const int tps = (c.T + LP - 1) / LP;
   // hand-off flags only: the status word is sticky for the whole step
-  if (!c.flags_zeroed) LBWN_HIP(hipMemsetAsync(c.flags, 0, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st));
+  if (!c.flags_zeroed) {
+    if (int e = lbwn_zero_launch(c.flags, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st)) return e;
+  }
   const int cm = (!c.gc_tab && !c.cond) ? 0 : (c.gc_tab && !c.cond) ? 1 : 2;
   if (lc) {
     if (cm == 0) chain_fwd_kernel<true, true, 0><<<c.grid, 256, 0, st>>>(k);
@@ -2277,7 +2273,7 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   k.X = c.X; k.xls = c.xls; k.DZ = c.DZ; k.lddz = c.ldz; k.dzls = c.dzls; k.wpack = c.wpack; k.slab = c.slab;
   k.ocg = c.ocg; k.ocls = c.ocls; k.dx0_a = c.dx0_a; k.dx0_c = c.dx0_c;
   k.gc_tab = c.gc_tab; k.gc_ld = c.gc_ld; k.ids = c.ids; k.cond = c.cond; k.ldcond = c.ldcond;
-  k.dv_out = c.dv_out; k.lddv = c.lddv; k.gc_dtab = c.gc_dtab;
+  k.dv_out = c.dv_out; k.lddv = c.lddv; k.gc_dtab = c.gc_dtab; k.tile_gid = c.tile_gid;
   k.flags = c.flags; k.status = c.status;
   k.B = c.B; k.T = c.T; k.H = c.H; k.L = c.L; k.nbl = c.nbl; k.Cd = c.Cd;
   k.trace = c.trace ? c.trace + 16L * c.L : nullptr; k.trace_blk = c.trace_blk;
@@ -2287,7 +2283,9 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
                        "chain bwd x3: misaligned images / rows");
   const int tps = (c.T + LP - 1) / LP;
   // hand-off flags only: the status word is sticky for the whole step
-  if (!c.flags_zeroed) LBWN_HIP(hipMemsetAsync(c.flags, 0, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st));
+  if (!c.flags_zeroed) {
+    if (int e = lbwn_zero_launch(c.flags, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st)) return e;
+  }
   LBWN_REQUIRE(x3 == (c.dzls > 0), "chain bwd: the bf16-split chain reads dZ in chain order (dzls), the f32 chain in rows");
   if (x3) chain_bwd_x3_kernel<<<c.grid, 256, 0, st>>>(k);
   else chain_bwd_kernel<<<c.grid, 256, 0, st>>>(k);
@@ -2308,3 +2306,36 @@ int lbwn_layer_reduce_all_launch(const lbwn_layer_red_args& r, int L, long slab_
 }
 
 int lbwn_slab_floats() { return SLAB; }
+
+namespace {
+// gtab[id][l·64 + c] += Σ over tiles with tile_gid == id (in tile order) of the tile's dv column
+// sums slab[l][tile][5120 + c].  Block = (layer, id), thread = column: the block scans the tile ids
+// 64 at a time (one per lane, ballot), then adds its matching tiles' partials in tile order
+// (deterministic; blocks of ids with no uniform tile only scan).
+__global__ __launch_bounds__(64) void gc_tile_sum_kernel(const float* __restrict__ slab, long slab_layer, int ntiles,
+                                                         const int* __restrict__ tile_gid, float* gtab, long ld) {
+  const int l = blockIdx.x, id = blockIdx.y, c = threadIdx.x;
+  const float* sl = slab + l * slab_layer + 5120 + c;
+  float acc = 0.f;
+  bool any = false;
+  for (int t0 = 0; t0 < ntiles; t0 += 64) {
+    const int t = t0 + c;
+    unsigned long long mask = __ballot(t < ntiles && tile_gid[min(t, ntiles - 1)] == id);
+    any |= mask != 0;
+    while (mask) {
+      const int j = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      acc += sl[(long)(t0 + j) * SLAB];
+    }
+  }
+  if (any) gtab[(long)id * ld + (long)l * 64 + c] += acc;
+}
+}  // namespace
+
+int lbwn_gc_tile_sum_launch(const float* slab, int L, int ntiles, const int* tile_gid, float* gtab, long ld,
+                            int ncat1, hipStream_t st) {
+  LBWN_REQUIRE(ncat1 >= 1 && slab && tile_gid && gtab, "gc tile sums: bad arguments");
+  gc_tile_sum_kernel<<<dim3(L, ncat1), 64, 0, st>>>(slab, (long)ntiles * SLAB, ntiles, tile_gid, gtab, ld);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}

@@ -574,6 +574,24 @@ __global__ void bcast_rows_kernel(float* dst, int L, int N) {
 }
 }  // namespace
 
+namespace {
+__global__ void zero_words_kernel(unsigned* p, long n) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) p[e] = 0u;
+}
+}  // namespace
+
+// Zero n_bytes (a multiple of 4) on the stream: an ordinary kernel in the step's launch sequence.
+// hipMemsetAsync's fill kernel started 13-18 us after the kernel before it (runtime blit path;
+// profiles/r03_v2_step_timeline.txt: counters -> fill at the step start), a plain launch ~2 us.
+int lbwn_zero_launch(void* p, size_t n_bytes, hipStream_t st) {
+  LBWN_REQUIRE(n_bytes % 4 == 0, "zero: byte count must be a multiple of 4");
+  const long n = (long)(n_bytes / 4);
+  if (n == 0) return 0;
+  zero_words_kernel<<<grid_for(n, 256, 1024), 256, 0, st>>>((unsigned*)p, n);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
 int lbwn_bcast_rows_launch(float* dst, int L, int N, hipStream_t st) {
   if (L <= 1) return 0;
   bcast_rows_kernel<<<grid_for((long)(L - 1) * N), 256, 0, st>>>(dst, L, N);
