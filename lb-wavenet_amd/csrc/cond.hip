@@ -413,7 +413,8 @@ int lbwn_lc_up_fwd_launch(int nup, const int* s, int Li, int Lo, int frames, con
 }
 
 int lbwn_lc_up_bwd_launch(int nup, const int* s, int Li, int Lo, int frames, const float* mel, const float* const* F,
-                          float* const* act, const float* dlc, float* dpart, float* const* dF, hipStream_t st) {
+                          float* const* act, const float* dlc, float* dpart, float* const* dF, hipStream_t st,
+                          hipStream_t st_sum, hipEvent_t ev) {
   LBWN_REQUIRE(lbwn_lc_up_fused_ok(nup, s, Li, Lo), "lc upsample: shape outside the fused kernel's envelope");
   UpK k = up_args(nup, s, Li, Lo, frames, mel, F, act);
   k.dlc = dlc; k.dpart = dpart;
@@ -421,7 +422,13 @@ int lbwn_lc_up_bwd_launch(int nup, const int* s, int Li, int Lo, int frames, con
   LBWN_CHECK_LAUNCH();
   int ptot = 0;
   for (int i = 0; i < nup; ++i) ptot += s[i] * Lo * (i ? Lo : Li);
-  lc_up_sum_kernel<<<(ptot + 255) / 256, 256, 0, st>>>(dpart, k, dF[0], nup > 1 ? dF[1] : nullptr,
+  if (st_sum && st_sum != st && ev) {
+    LBWN_HIP(hipEventRecord(ev, st));
+    LBWN_HIP(hipStreamWaitEvent(st_sum, ev, 0));
+  } else {
+    st_sum = st;
+  }
+  lc_up_sum_kernel<<<(ptot + 255) / 256, 256, 0, st_sum>>>(dpart, k, dF[0], nup > 1 ? dF[1] : nullptr,
                                                        nup > 2 ? dF[2] : nullptr, nup > 3 ? dF[3] : nullptr, ptot);
   LBWN_CHECK_LAUNCH();
   return 0;

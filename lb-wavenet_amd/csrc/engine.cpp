@@ -57,7 +57,10 @@ struct lbwn_plan {
   // LDS, so nothing co-resides with the chains.
   bool overlap = false;
   hipStream_t aux2 = nullptr;
-  hipEvent_t ev_chain = nullptr, ev_join2 = nullptr, ev_dlc = nullptr;
+  hipEvent_t ev_chain = nullptr, ev_join2 = nullptr;
+  hipEvent_t ev_fwd_fork = nullptr, ev_fwd_up = nullptr;   // forward: LC upsample on aux2
+  hipEvent_t ev_upb = nullptr;   // backward: the upsample's per-frame pass done (main) -> its sum (aux2)
+  bool up_forked = false;        // this forward launched the fused upsample on aux2
   bool bwd_chain_event = false;  // the last backward recorded ev_chain (lbwn_plan_stream_wait)
   bool wpk_valid = false;        // the f32 layer images were packed this step
   // Weights pre-split into bf16 planes once per step for the bf16-split GEMMs (gemm.hip):
@@ -68,8 +71,10 @@ struct lbwn_plan {
   ~lbwn_plan() {
     if (aux2) (void)hipStreamDestroy(aux2);
     if (ev_chain) (void)hipEventDestroy(ev_chain);
+    if (ev_fwd_fork) (void)hipEventDestroy(ev_fwd_fork);
+    if (ev_fwd_up) (void)hipEventDestroy(ev_fwd_up);
+    if (ev_upb) (void)hipEventDestroy(ev_upb);
     if (ev_join2) (void)hipEventDestroy(ev_join2);
-    if (ev_dlc) (void)hipEventDestroy(ev_dlc);
   }
   // one-shot event probe
   char probe[32];
@@ -453,7 +458,9 @@ int ensure_device(lbwn_plan* p) {
     LBWN_HIP(hipStreamCreateWithPriority(&p->aux2, hipStreamNonBlocking, greatest));
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_chain, hipEventDisableTiming));
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_join2, hipEventDisableTiming));
-    LBWN_HIP(hipEventCreateWithFlags(&p->ev_dlc, hipEventDisableTiming));
+    LBWN_HIP(hipEventCreateWithFlags(&p->ev_fwd_fork, hipEventDisableTiming));
+    LBWN_HIP(hipEventCreateWithFlags(&p->ev_fwd_up, hipEventDisableTiming));
+    LBWN_HIP(hipEventCreateWithFlags(&p->ev_upb, hipEventDisableTiming));
   }
   return 0;
 }
@@ -529,12 +536,16 @@ int cond_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const float* mel,
     c.gc_ld = 2L * L * Cd;
   }
   if (p->Lo > 0 && p->up_fused) {
-    float* act[8];
-    for (int i = 0; i < p->nup; ++i) act[i] = at<float>(ws, p->oLCACT[i]);
-    Probe(p, st, "lc_up_fwd");
-    if ((e = lbwn_lc_up_fwd_launch(p->nup, p->up, p->Li, p->Lo, (int)(p->M / p->hop), mel, P->lc_up, act, st)))
-      return e;
-    Probe::end(p, st, "lc_up_fwd");
+    if (p->up_forked) {   // launched on aux2 at the forward's start; wait for it here
+      LBWN_HIP(hipStreamWaitEvent(st, p->ev_fwd_up, 0));
+    } else {
+      float* act[8];
+      for (int i = 0; i < p->nup; ++i) act[i] = at<float>(ws, p->oLCACT[i]);
+      Probe(p, st, "lc_up_fwd");
+      if ((e = lbwn_lc_up_fwd_launch(p->nup, p->up, p->Li, p->Lo, (int)(p->M / p->hop), mel, P->lc_up, act, st)))
+        return e;
+      Probe::end(p, st, "lc_up_fwd");
+    }
   } else if (p->Lo > 0) {
     const float* in = mel;
     long rows = (long)p->B * (p->T / p->hop);
@@ -603,7 +614,7 @@ int lc_dlc(lbwn_plan* p, const lbwn_params* P, void* ws, float* spl, hipStream_t
 }
 
 int lc_upsample_bwd(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G, void* ws, const float* mel, float* spl,
-                    hipStream_t st) {
+                    hipStream_t st, hipStream_t st_sum = nullptr) {
   int e;
   const float* dout = at<float>(ws, p->oDLC[0]);
   if (p->up_fused) {
@@ -612,7 +623,7 @@ int lc_upsample_bwd(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G, vo
     for (int i = 0; i < p->nup; ++i) { F[i] = P->lc_up[i]; act[i] = at<float>(ws, p->oLCACT[i]); }
     Probe(p, st, "lc_up_bwd");
     e = lbwn_lc_up_bwd_launch(p->nup, p->up, p->Li, p->Lo, (int)(p->M / p->hop), mel, F, act, dout,
-                              at<float>(ws, p->oUPPART), G->lc_up, st);
+                              at<float>(ws, p->oUPPART), G->lc_up, st, st_sum, p->ev_upb);
     Probe::end(p, st, "lc_up_bwd");
     return e;
   }
@@ -657,6 +668,19 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   // zeroed here, read by the host after the step (lbwn_plan_tensor "status")
   if ((e = lbwn_zero_launch(at<char>(ws, p->oSTATUS), 16 + 2 * p->nflag_bytes, st))) return e;
   p->bwd_flags_fresh = true;
+  // the fused LC upsample depends only on the mel input and the upsample filters: it runs on
+  // aux2 beside the weight packs, embedding, GC table and D-sep prepend, joined before the chain
+  p->up_forked = false;
+  if (p->Lo > 0 && p->up_fused && p->aux2) {
+    float* act[8];
+    for (int i = 0; i < p->nup; ++i) act[i] = at<float>(ws, p->oLCACT[i]);
+    LBWN_HIP(hipEventRecord(p->ev_fwd_fork, st));
+    LBWN_HIP(hipStreamWaitEvent(p->aux2, p->ev_fwd_fork, 0));
+    if ((e = lbwn_lc_up_fwd_launch(p->nup, p->up, p->Li, p->Lo, (int)(p->M / p->hop), mel, P->lc_up, act, p->aux2)))
+      return e;
+    LBWN_HIP(hipEventRecord(p->ev_fwd_up, p->aux2));
+    p->up_forked = true;
+  }
   const int L = p->L, B = p->B, T = p->T, H = p->H, Cr = p->Cr, Cd = p->Cd;
   const long M = p->M, ldz = (long)L * Cd;
   float* X = at<float>(ws, p->oX);
@@ -982,13 +1006,12 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     if (c.tile_gid && (e = lbwn_gc_tile_sum_launch(SLABS, L, ntiles, c.tile_gid, cd.gc_dtab, cd.gc_ld, p->ncat1, rst)))
       return e;
     if ((e = gc_backward(p, P, G, ws, rst))) return e;
+    // main stream: dlc, then the LC upsample backward (it needs dlc), then dSKIP below; the side
+    // stream keeps dLCcat, dPRE, the slab reduction and the GC grads (arch5 tail 916 -> ~800 us:
+    // behind dLCcat on the side stream the upsample backward was the last thing to finish)
     if (p->Lo > 0) {
       if ((e = lc_dlc(p, P, ws, SPL, st))) return e;
-      if (rst != st) {
-        LBWN_HIP(hipEventRecord(p->ev_dlc, st));
-        LBWN_HIP(hipStreamWaitEvent(rst, p->ev_dlc, 0));
-      }
-      if ((e = lc_upsample_bwd(p, P, G, ws, mel, SPLA, rst))) return e;
+      if ((e = lc_upsample_bwd(p, P, G, ws, mel, SPL, st, rst))) return e;   // its frame sum on the side
     }
     if (p->aux2) LBWN_HIP(hipEventRecord(p->ev_join2, rst));
   } else {

@@ -776,6 +776,9 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm) {
         xv[mm] = *(const floatx4*)(xin + 4 * mm);
       }
       const float bco = S[GI_WR + o] + S[GI_WR + 128 + o];
+      // sub-layer cycle stamps (trace only): layers 16..23 of the traced step, 6 per layer
+      long long* st6 = (tr && s == n - 1 && l >= 16 && l < 24 && L + 184 <= 2 * L + 136) ? tr + 8 + L + 128 + 6 * (l - 16) : nullptr;
+      if (st6) st6[0] = clock64();
       __builtin_amdgcn_sched_barrier(0);
       const int d = 1 << bl;
       if (rh == 0 && (rc >> 3) == w && rc < Cr) a.rings[roff + ((long)b * d + (t & (d - 1))) * Cr + rc] = x;
@@ -788,8 +791,10 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm) {
       v += dpp<DPP_XOR1>(v);
       v += dpp<DPP_XOR2>(v);
       v += bco;
+      if (st6) { asm volatile("" ::"v"(v)); st6[1] = clock64(); }
       const float vp = dpp<DPP_HALF_MIRROR>(v);
       const float z = gate_z(sg ? vp : v, sg ? v : vp);
+      if (st6) { asm volatile("" ::"v"(z)); st6[2] = clock64(); }
       float* Zl = Z + (l & 1) * 32;
       if (lead) {
         Zl[ch] = z;
@@ -798,6 +803,7 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm) {
       // the last layer's ring stores must land before the loaders DMA the next step's taps
       if (l == L - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lds_barrier();
+      if (st6) st6[3] = clock64();
       floatx4 zv[4], rw[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -811,8 +817,10 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm) {
       const float r = r0 + r1;
       const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(r), __float_as_uint(r), false, false);
       x += (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) + bro;
+      if (st6) { asm volatile("" ::"v"(x)); st6[4] = clock64(); }
       if (lane < 32) XW[rc] = x;
       wave_sync();
+      if (st6) st6[5] = clock64();
       if (tr && s == n - 1) tr[8 + l] = wall_clock64();
     }
     if (tr && s == n - 1) tr[1] = wall_clock64();

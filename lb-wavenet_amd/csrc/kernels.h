@@ -209,5 +209,7 @@ int lbwn_lc_up_fused_ok(int nup, const int* s, int Li, int Lo);
 int lbwn_lc_up_part_floats(int nup, const int* s, int Li, int Lo, int frames);
 int lbwn_lc_up_fwd_launch(int nup, const int* s, int Li, int Lo, int frames, const float* mel, const float* const* F,
                           float* const* act, hipStream_t st);
+// the per-frame pass on st; the frame-partial sum on st_sum (after ev, recorded on st, when they differ)
 int lbwn_lc_up_bwd_launch(int nup, const int* s, int Li, int Lo, int frames, const float* mel, const float* const* F,
-                          float* const* act, const float* dlc, float* dpart, float* const* dF, hipStream_t st);
+                          float* const* act, const float* dlc, float* dpart, float* const* dF, hipStream_t st,
+                          hipStream_t st_sum = nullptr, hipEvent_t ev = nullptr);

@@ -48,6 +48,12 @@ if g.persistent:
     print('  last head C: post1 partials %.2f, barrier %.2f, h %.2f' % tuple(us(tr[8 + L + 120:8 + L + 123])))
     print('  chain 0: logits gathered %.2f, draw done %.2f' % (us(tr[5]), us(tr[6])))
     print('  step period ~ %.2f us (draw done - start of the step it drew)' % us(tr[6]))
+    sub = tr[8 + L + 128:8 + L + 128 + 48].reshape(8, 6)
+    if np.all(sub > 0):
+        seg = np.diff(np.concatenate([sub, sub[1:, :1].tolist() + [[sub[-1, 5]]]], axis=1), axis=1)
+        med = np.median(seg[:7], axis=0)
+        print('  chain 0, layers 16-22, shader cycles: reads+conv dot+DPP %d, gate %d, z write+barrier %d, '
+              'residual %d, x write+sync %d, to next layer start %d' % tuple(med[:6]))
 else:
     rows = np.diff(np.concatenate([tr[:3], tr[4:4 + 2 * L]]))
     conv, res = rows[4::2], rows[3::2][:L]
