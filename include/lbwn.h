@@ -172,6 +172,17 @@ int lbwn_gemm_f32(const float* A, int64_t lda, int a_kcontig, const float* B, in
                   float* C, int64_t ldc, int M, int N, int K, const float* bias, int relu_a, int relu_out,
                   const float* mask, int64_t ldm, int accumulate, int split_k, float* slab_ws, void* stream);
 
+/* The same product with B given ALSO as pre-split bf16 planes b3 (lbwn_split_planes of B with
+ * rows = N: trans = 0 for B[n*ldb+k], 1 for B[k*ldb+n]), the form the training step uses for its
+ * weight operands; no split-K.  B stays required for the f32 mode (mode 0 ignores b3). */
+int lbwn_gemm_f32_presplit(const float* A, int64_t lda, int a_kcontig, const uint16_t* b3, int N, const float* B,
+                           int64_t ldb, int b_kcontig, float* C, int64_t ldc, int M, int K, const float* bias,
+                           int relu_a, int relu_out, const float* mask, int64_t ldm, int accumulate, void* stream);
+/* Exact three-term bf16 split of a weight, out[r][K/32][3][32] (K rounded up to 32, zero-filled):
+ * W[r*ldw+k] (trans = 0) or W[k*ldw+r] (trans = 1), r < rows. */
+int64_t lbwn_split_planes_elems_abi(int rows, int K);
+int lbwn_split_planes(const float* W, int64_t ldw, int rows, int K, int trans, uint16_t* out, void* stream);
+
 /* One residual layer forward (tmodel.py:117-184): x_in is the [B][H+T][n_res] halo
  * buffer whose rows [H-d, H) hold SAVE; writes z [M][*] (row stride ldz) and, if x_out,
  * x_out body rows (x + z·RES + b). gc_tab [n_cat+1][2·n_dil] / ids, cond [M][2·n_dil]

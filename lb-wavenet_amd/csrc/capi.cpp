@@ -58,6 +58,26 @@ int lbwn_gemm_f32(const float* A, int64_t lda, int a_kcontig, const float* B, in
   return lbwn_gemm_launch(g, a_kcontig, b_kcontig, split_k, slab_ws, (hipStream_t)stream);
 }
 
+int lbwn_gemm_f32_presplit(const float* A, int64_t lda, int a_kcontig, const uint16_t* b3, int N, const float* B,
+                           int64_t ldb, int b_kcontig, float* C, int64_t ldc, int M, int K, const float* bias,
+                           int relu_a, int relu_out, const float* mask, int64_t ldm, int accumulate, void* stream) {
+  LBWN_REQUIRE(b3 != nullptr, "gemm_f32_presplit: b3 is null");
+  lbwn_gemm_args g;
+  memset(&g, 0, sizeof(g));
+  g.A = A; g.lda = (long)lda; g.B = B; g.ldb = (long)ldb; g.C = C; g.ldc = (long)ldc;
+  g.M = M; g.N = N; g.K = K; g.bias = bias; g.relu_a = relu_a; g.relu_out = relu_out;
+  g.mask = mask; g.ldm = (long)ldm; g.accumulate = accumulate; g.b3 = (const unsigned short*)b3;
+  return lbwn_gemm_launch(g, a_kcontig, b_kcontig, 1, nullptr, (hipStream_t)stream);
+}
+
+int64_t lbwn_split_planes_elems_abi(int rows, int K) { return (int64_t)lbwn_split_planes_elems(rows, K); }
+
+int lbwn_split_planes(const float* W, int64_t ldw, int rows, int K, int trans, uint16_t* out, void* stream) {
+  const long l = (long)ldw;
+  unsigned short* o = (unsigned short*)out;
+  return lbwn_split_planes_launch(1, &W, &l, &rows, &K, &trans, &o, (hipStream_t)stream);
+}
+
 int lbwn_gemm_set_mode(int mode) { return lbwn_gemm_set_mode_impl(mode); }
 int lbwn_gemm_get_mode(void) { return lbwn_gemm_mode(); }
 

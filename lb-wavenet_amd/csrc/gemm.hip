@@ -263,10 +263,21 @@ constexpr int X3_NT = 256;
 #ifndef X3_OCC
 #define X3_OCC 2
 #endif
+#ifndef X3R
+#define X3R 1        // tall products with A k-contiguous and B pre-split: A in registers (gemm_x3r_kernel)
+#endif
+#ifndef X3_SCHED
+#define X3_SCHED 0   // 256-row k-step schedule: 0 = compiler's, 1/2 = interleave groups (see step())
+#endif
 
-// split 4 consecutive-k values into the three planes and store them
+// split 4 consecutive-k values into the three planes and store them.  relu without a branch
+// (a branch here split the k-step into basic blocks the scheduler cannot interleave with the
+// MFMAs): as integers, max(bits, 0) is relu on f32 (negative floats are negative ints) and
+// max(bits, INT_MIN) is the identity
 LBWN_DEV void x3_store4(unsigned short* row, int k, floatx4 x, bool relu) {
-  if (relu) { x[0] = fmaxf(x[0], 0.f); x[1] = fmaxf(x[1], 0.f); x[2] = fmaxf(x[2], 0.f); x[3] = fmaxf(x[3], 0.f); }
+  const int lo = relu ? 0 : (int)0x80000000;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) x[j] = __int_as_float(max(__float_as_int(x[j]), lo));
   unsigned h0, m0, l0, h1, m1, l1;
   split2((floatx2){x[0], x[1]}, h0, m0, l0);
   split2((floatx2){x[2], x[3]}, h1, m1, l1);
@@ -554,19 +565,39 @@ __global__ __launch_bounds__(128 * WM, (WM == 2 && STAGES == 1) ? X3_OCC : 1) vo
     // flight (its counts cannot assume the guarded ones were issued).
     const int last = max(ntiles - 1, 0);
     auto step = [&](int kt, auto sset) {
-      constexpr int S = decltype(sset)::value;   // = (kt + 1) & 1
-      const unsigned short* cur = smem + (kt & 1) * SLOT;
+      constexpr int S = decltype(sset)::value;   // = (kt + 1) & 1: the slot written, the register set
+      const unsigned short* cur = smem + (S ^ 1) * SLOT;   // compile-time slots: provably disjoint
+      unsigned short* nxt = smem + S * SLOT;
       Frags f0, f1;
       frags(cur, 0, f0);
       mfmas(f0);
-      unsigned short* nxt = smem + ((kt + 1) & 1) * SLOT;
+      if (X3_SCHED >= 2) frags(cur, 1, f1);
       sa.template store<S>(nxt, tid, relu_a);
       if (BPRE) sp.template store<S>(nxt + BM * X3_ROW); else sb.template store<S>(nxt + BM * X3_ROW, tid, false);
       const int kl = min(kt + 3, last);
       sa.template load<S>(kl, kz1);
       if (BPRE) sp.template load<S>(kl); else sb.template load<S>(kl, kz1);
-      frags(cur, 1, f1);   // (before the stage stores: 2.40 -> 2.50 ms, same box)
+      if (X3_SCHED < 2) frags(cur, 1, f1);   // (before the stage stores: 2.40 -> 2.50 ms, same box)
       mfmas(f1);
+      if (X3_SCHED == 1 || X3_SCHED == 2) {
+        // one k-step = 24 fragment reads, 48 MFMAs, the split VALU + LDS writes of the next
+        // k-step and the global loads of k-step kt + 3: the split work goes into the MFMA gaps of
+        // chunk 0 (≤ 4 VALU per gap hide beside a 32-cycle MFMA), chunk 1's fragment reads into
+        // its last gaps, the loads into chunk 1
+        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+        for (int i = 0; i < 24; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+          if (i & 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+          if (i >= 16) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+        for (int i = 0; i < 24; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          if (i < 8) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        }
+      }
       __syncthreads();
     };
     if (ntiles > 0) {
@@ -584,6 +615,175 @@ __global__ __launch_bounds__(128 * WM, (WM == 2 && STAGES == 1) ? X3_OCC : 1) vo
   }
 
   x3_epilogue(g, acc, m0, n0, wm, wn, lane, WM, WM == 4 ? (float*)smem : nullptr);
+}
+
+// ---------------------------------------------------------------------------------------------
+// 256 × 128 tiles with A in registers: A k-contiguous f32, B pre-split (lbwn_gemm_args::b3), the
+// form of every tall product of the step (skip / post1 / post2 forward, dH1, dS, dZ).  Wave w owns
+// rows m0 + 32w … +31 and all 128 columns (four 32 × 32 accumulators).  Lane (r, h) loads its own
+// A values of each 32-deep k-step straight from global memory (row r, k = 8h … 8h+7 and
+// 16+8h … 16+8h+7: two 32-B runs; a row's two lanes cover its 128-B line) and splits them in
+// registers into exactly the MFMA fragments it supplies, so A never passes through the LDS: the
+// LDS carries only B (26.6 KB per k-step instead of 80: no A image writes, no A fragment reads;
+// B's fragment reads are the A reads' former count).  A two k-steps ahead and B three (two
+// register sets each), one barrier per k-step.
+template <int X>
+__global__ __launch_bounds__(512, 1) void gemm_x3r_kernel(lbwn_gemm_args g) {
+  constexpr int NTHR = 512, BM = 256, BN = 128, NI = 4;
+  constexpr int SLOT = BN * X3_ROW;
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_n = (g.N + BN - 1) / BN;
+  if (g.step_advance && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && tid == 0)   // no-return atomic
+    __hip_atomic_fetch_add(g.step_advance, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int t = gemm_tile();
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  const int kz0 = gemm_split() * g.k_per_split;
+  const int kz1 = min(g.K, kz0 + g.k_per_split);
+  const int ntiles = (kz1 - kz0) / X3_BK;   // K % 32 == 0 (pre-split B)
+  const int last = max(ntiles - 1, 0);
+
+  floatx16 acc[NI];
+#pragma unroll
+  for (int b = 0; b < NI; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+
+  const int fr = lane & 31, fh = lane >> 5;
+  const float* pa = g.A + (long)min(m0 + 32 * wave + fr, g.M - 1) * g.lda + kz0 + 8 * fh;
+  const int alo = g.relu_a ? 0 : (int)0x80000000;   // relu as an integer max (x3_store4)
+  floatx4 av[2][4];
+  auto a_load = [&](auto sset, int kt) {
+    constexpr int S = decltype(sset)::value;
+    const float* p = pa + kt * X3_BK;
+    av[S][0] = *(const floatx4*)p;
+    av[S][1] = *(const floatx4*)(p + 4);
+    av[S][2] = *(const floatx4*)(p + 16);
+    av[S][3] = *(const floatx4*)(p + 20);
+  };
+  // the three bf16x8 fragments of chunk c (k = 16c + 8h + j) from register set S
+  auto a_split = [&](auto sset, int c, bf16x8 (&f)[3]) {
+    constexpr int S = decltype(sset)::value;
+    floatx4 x = av[S][2 * c], y = av[S][2 * c + 1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x[j] = __int_as_float(max(__float_as_int(x[j]), alo));
+      y[j] = __int_as_float(max(__float_as_int(y[j]), alo));
+    }
+    split8(x, y, f);
+  };
+
+  X3Pre<BN, NTHR> sp;
+  sp.init(g.b3, g.K / X3_BK, n0, g.N, kz0, tid);
+  if (ntiles > 0) {
+    sp.load(0);
+    sp.store(smem);
+    a_load(std::integral_constant<int, 0>(), 0);
+    a_load(std::integral_constant<int, 1>(), min(1, last));
+    sp.template load<1>(min(1, last));
+    sp.template load<0>(min(2, last));
+  }
+  __syncthreads();
+  const int fb_off = fr * X3_ROW + 8 * fh;
+
+  auto b_frags = [&](const unsigned short* base, int c, bf16x8 (&f)[NI][3]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) f[ni][p] = *(const bf16x8*)(base + fb_off + ni * 32 * X3_ROW + 32 * p + 16 * c);
+  };
+  auto mfmas = [&](const bf16x8 (&fa)[3], const bf16x8 (&fb)[NI][3]) {
+    // small terms first: a2b0, a1b1, a0b2, a1b0, a0b1, a0b0
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+        acc[ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[PA[q]], fb[ni][PB[q]], acc[ni], 0, 0, 0);
+    }
+  };
+  // k-step kt: A in register set kt & 1 (= S ^ 1), B in LDS slot kt & 1; B of k-step kt + 1 is
+  // stored from register set S into the other slot
+  auto step = [&](int kt, auto sset) {
+    constexpr int S = decltype(sset)::value;   // = (kt + 1) & 1
+    const unsigned short* cur = smem + (S ^ 1) * SLOT;
+    unsigned short* nxt = smem + S * SLOT;
+    bf16x8 fa0[3], fa1[3], fb[NI][3];
+    a_split(std::integral_constant<int, S ^ 1>(), 0, fa0);
+    a_split(std::integral_constant<int, S ^ 1>(), 1, fa1);
+    a_load(std::integral_constant<int, S ^ 1>(), min(kt + 2, last));
+    b_frags(cur, 0, fb);
+    mfmas(fa0, fb);
+    sp.template store<S>(nxt);
+    sp.template load<S>(min(kt + 3, last));
+    b_frags(cur, 1, fb);
+    mfmas(fa1, fb);
+    __syncthreads();
+  };
+  int kt = 0;
+  for (; kt + 1 < ntiles; kt += 2) {
+    step(kt, std::integral_constant<int, 1>());
+    step(kt + 1, std::integral_constant<int, 0>());
+  }
+  if (kt < ntiles) step(kt, std::integral_constant<int, 1>());
+
+  // epilogue (bias, relu, mask, accumulate, chain order, column partials): x3_epilogue_rows'
+  // element rules on this wave's 32-row band × 128 columns
+  const int h = fh, ci = fr;
+  float* C = g.C + (long)gemm_split() * g.split_stride;
+  const bool raw = g.split_stride != 0;
+  const int rbase = m0 + 32 * wave;
+  float cs[NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) {
+    cs[ni] = 0.f;
+    const int col = n0 + ni * 32 + ci, colc = min(col, g.N - 1);
+    float mv[16], cv[16];
+    if (!raw && g.mask) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mv[r] = g.mask[(long)min(rbase + acc_row(r, h), g.M - 1) * g.ldm + colc];
+    }
+    if (!raw && g.accumulate) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) cv[r] = C[(long)min(rbase + acc_row(r, h), g.M - 1) * g.ldc + colc];
+    }
+    const float bv = (!raw && g.bias) ? g.bias[colc] : 0.f;
+    if (col >= g.N) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = rbase + acc_row(r, h);
+      float v = acc[ni][r];
+      if (!raw) {
+        v += bv;
+        if (g.relu_out) v = fmaxf(v, 0.f);
+        if (g.mask && !(mv[r] > 0.f)) v = 0.f;
+        if (g.accumulate) v += cv[r];
+      }
+      if (row < g.M) {
+        if (g.c_chain_ls)
+          C[(col >> 5) * g.c_chain_ls + ((((long)(row >> 5) * 4 + ((col >> 3) & 3)) * 32 + (row & 31)) * 8 + (col & 7))] = v;
+        else
+          C[(long)row * g.ldc + col] = v;
+        cs[ni] += v;
+      }
+    }
+  }
+  if (g.colpart && !raw) {   // the block's 256-row column partials: lane halves, then waves in order
+    float* red = (float*)smem;   // free after the k-loop's last barrier
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      cs[ni] += __shfl_xor(cs[ni], 32);
+      if (h == 0) red[wave * 128 + ni * 32 + ci] = cs[ni];
+    }
+    __syncthreads();
+    const int col = n0 + tid;
+    if (tid < 128 && col < g.N) {
+      float s = 0.f;
+      for (int w = 0; w < 8; ++w) s += red[w * 128 + tid];
+      g.colpart[(long)(m0 >> 8) * g.N + col] = s;
+    }
+  }
 }
 
 // Pre-split planes of weights W (f32, row stride ldw): out[r][kc][plane][32] = split of
@@ -698,7 +898,10 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
   int e = gemm_setup(a, a_kcontig, b_kcontig, split_k, slab_ws, X3_BK, 64 * wm, 128, g, grid);
   if (e) return e;
   const bool kfull = a.K % X3_BK == 0, pre = a.b3 != nullptr;
-  if (wm == 4) {
+  if (wm == 4 && X3R && kfull && pre && a_kcontig) {
+    gemm_x3r_kernel<0><<<grid, 512, 0, st>>>(g);
+    LBWN_CHECK_LAUNCH();
+  } else if (wm == 4) {
     if (kfull && pre) e = gemm_launch_x3_t<true, true, 4>(g, grid, a_kcontig, b_kcontig, st);
     else if (kfull) e = gemm_launch_x3_t<true, false, 4>(g, grid, a_kcontig, b_kcontig, st);
     else e = gemm_launch_x3_t<false, false, 4>(g, grid, a_kcontig, b_kcontig, st);

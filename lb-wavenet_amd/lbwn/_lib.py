@@ -63,6 +63,10 @@ _SIGS = {
     'lbwn_mulaw_decode': (c_int, [c_fp, c_fp, c_int64, c_int, c_void_p]),
     'lbwn_gemm_f32': (c_int, [c_fp, c_int64, c_int, c_fp, c_int64, c_int, c_fp, c_int64, c_int, c_int, c_int,
                               c_fp, c_int, c_int, c_fp, c_int64, c_int, c_int, c_fp, c_void_p]),
+    'lbwn_gemm_f32_presplit': (c_int, [c_fp, c_int64, c_int, c_fp, c_int, c_fp, c_int64, c_int, c_fp, c_int64, c_int,
+                                       c_int, c_fp, c_int, c_int, c_fp, c_int64, c_int, c_void_p]),
+    'lbwn_split_planes_elems_abi': (c_int64, [c_int, c_int]),
+    'lbwn_split_planes': (c_int, [c_fp, c_int64, c_int, c_int, c_int, c_fp, c_void_p]),
     'lbwn_gemm_set_mode': (c_int, [c_int]),
     'lbwn_gemm_get_mode': (c_int, []),
     'lbwn_layer_image_floats_abi': (c_int, []),

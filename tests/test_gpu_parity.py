@@ -111,6 +111,38 @@ def test_gemm_large_skip_shape(lib, gemm_mode, mode):
     close(C.cpu().numpy(), (A @ Bm).numpy(), 1e-5, 'gemm_skip')
 
 
+@pytest.mark.parametrize('M,N,K,bkc,epi', [(8192, 512, 1600, 0, 0), (8200, 136, 96, 1, 1), (8192, 1600, 512, 1, 2),
+                                           (9000, 256, 512, 0, 1)])
+def test_gemm_presplit_tall(lib, gemm_mode, M, N, K, bkc, epi):
+    """The tall products of the training step (M >= 8192, A k-contiguous, B pre-split: the
+    A-in-registers kernel) against torch fp64: epi 0 plain, 1 bias + relu(A) + relu + mask +
+    accumulate, 2 bias only; ragged M / N tiles included."""
+    gemm_mode(1)
+    g = torch.Generator().manual_seed(11)
+    A = torch.randn(M, K, generator=g, dtype=torch.float64)
+    Bm = torch.randn(K, N, generator=g, dtype=torch.float64) * 0.05
+    bias = torch.randn(N, generator=g, dtype=torch.float64)
+    mask = (torch.rand(M, N, generator=g) > 0.3).double()
+    C0 = torch.randn(M, N, generator=g, dtype=torch.float64)
+    if epi == 1:
+        ref = torch.relu(torch.relu(A) @ Bm + bias) * mask + C0
+    elif epi == 2:
+        ref = A @ Bm + bias
+    else:
+        ref = A @ Bm
+    Ad = A.float().to(DEV).contiguous()
+    Bd = (Bm.t() if bkc else Bm).contiguous().float().to(DEV)
+    b3 = torch.empty(int(lib.lbwn_split_planes_elems_abi(N, K)), dtype=torch.int16, device=DEV)
+    _lib.check(lib.lbwn_split_planes(Bd.data_ptr(), K if bkc else N, N, K, 0 if bkc else 1, b3.data_ptr(), None))
+    Cd = C0.float().to(DEV).contiguous() if epi == 1 else torch.empty(M, N, device=DEV)
+    md, bd = mask.float().to(DEV), bias.float().to(DEV)
+    _lib.check(lib.lbwn_gemm_f32_presplit(Ad.data_ptr(), K, 1, b3.data_ptr(), N, Bd.data_ptr(), K if bkc else N, bkc,
+                                          Cd.data_ptr(), N, M, K, bd.data_ptr() if epi else None, int(epi == 1),
+                                          int(epi == 1), md.data_ptr() if epi == 1 else None, N, int(epi == 1), None))
+    torch.cuda.synchronize()
+    close(Cd.cpu().numpy(), ref.numpy(), 1e-5, 'gemm_presplit')
+
+
 def _gemm_err(lib, A, Bm, akc, bkc, split):
     M, K = A.shape
     N = Bm.shape[1]

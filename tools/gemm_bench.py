@@ -48,6 +48,14 @@ for name, m, n, k, akc, bkc, split in runs:
     def ours():
         _lib.check(lib.lbwn_gemm_f32(A.data_ptr(), A.shape[1], akc, B.data_ptr(), B.shape[1], bkc, C.data_ptr(), n,
                                      m, n, k, None, 0, 0, None, 0, 0, split, slab.data_ptr(), st))
+    b3 = None
+    if akc and split == 1 and k % 32 == 0:   # the step's form: B pre-split once per step
+        b3 = torch.empty(int(lib.lbwn_split_planes_elems_abi(n, k)), dtype=torch.int16, device='cuda')
+        _lib.check(lib.lbwn_split_planes(B.data_ptr(), B.shape[1], n, k, 0 if bkc else 1, b3.data_ptr(), st))
+
+    def ours_pre():
+        _lib.check(lib.lbwn_gemm_f32_presplit(A.data_ptr(), A.shape[1], akc, b3.data_ptr(), n, B.data_ptr(),
+                                              B.shape[1], bkc, C.data_ptr(), n, m, k, None, 0, 0, None, 0, 0, st))
     Am = A if akc else A.t()
     Bm = B.t() if bkc else B
 
@@ -59,6 +67,9 @@ for name, m, n, k, akc, bkc, split in runs:
         _lib.check(lib.lbwn_gemm_set_mode(mode))
         t = timeit(ours)
         res.append('%s %7.1f us %6.1f TF' % (('f32 ', 'x3  ')[mode], t * 1e6, fl / t / 1e12))
+    if b3 is not None:
+        t = timeit(ours_pre)
+        res.append('x3pre %7.1f us %6.1f TF' % (t * 1e6, fl / t / 1e12))
     t1 = timeit(ref)
     print('%-10s M%6d N%5d K%6d split %2d | %s | torch %7.1f us %6.1f TF' % (
         name, m, n, k, split, ' | '.join(res), t1 * 1e6, fl / t1 / 1e12), flush=True)
