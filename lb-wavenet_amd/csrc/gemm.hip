@@ -266,9 +266,6 @@ constexpr int X3_NT = 256;
 #ifndef X3R
 #define X3R 1        // tall products with A k-contiguous and B pre-split: A in registers (gemm_x3r_kernel)
 #endif
-#ifndef X3_SCHED
-#define X3_SCHED 0   // 256-row k-step schedule: 0 = compiler's, 1/2 = interleave groups (see step())
-#endif
 
 // split 4 consecutive-k values into the three planes and store them.  relu without a branch
 // (a branch here split the k-step into basic blocks the scheduler cannot interleave with the
@@ -571,33 +568,13 @@ __global__ __launch_bounds__(128 * WM, (WM == 2 && STAGES == 1) ? X3_OCC : 1) vo
       Frags f0, f1;
       frags(cur, 0, f0);
       mfmas(f0);
-      if (X3_SCHED >= 2) frags(cur, 1, f1);
       sa.template store<S>(nxt, tid, relu_a);
       if (BPRE) sp.template store<S>(nxt + BM * X3_ROW); else sb.template store<S>(nxt + BM * X3_ROW, tid, false);
       const int kl = min(kt + 3, last);
       sa.template load<S>(kl, kz1);
       if (BPRE) sp.template load<S>(kl); else sb.template load<S>(kl, kz1);
-      if (X3_SCHED < 2) frags(cur, 1, f1);   // (before the stage stores: 2.40 -> 2.50 ms, same box)
+      frags(cur, 1, f1);   // (before the stage stores: 2.40 -> 2.50 ms, same box)
       mfmas(f1);
-      if (X3_SCHED == 1 || X3_SCHED == 2) {
-        // one k-step = 24 fragment reads, 48 MFMAs, the split VALU + LDS writes of the next
-        // k-step and the global loads of k-step kt + 3: the split work goes into the MFMA gaps of
-        // chunk 0 (≤ 4 VALU per gap hide beside a 32-cycle MFMA), chunk 1's fragment reads into
-        // its last gaps, the loads into chunk 1
-        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-        for (int i = 0; i < 24; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-          if (i & 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-          if (i >= 16) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        }
-        for (int i = 0; i < 24; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          if (i < 8) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-        }
-      }
       __syncthreads();
     };
     if (ntiles > 0) {
@@ -626,8 +603,13 @@ __global__ __launch_bounds__(128 * WM, (WM == 2 && STAGES == 1) ? X3_OCC : 1) vo
 // registers into exactly the MFMA fragments it supplies, so A never passes through the LDS: the
 // LDS carries only B (26.6 KB per k-step instead of 80: no A image writes, no A fragment reads;
 // B's fragment reads are the A reads' former count).  A two k-steps ahead and B three (two
-// register sets each), one barrier per k-step.
-template <int X>
+// register sets each), one barrier per k-step.  The A fragments of k-step kt + 1 are split
+// during k-step kt's MFMAs, so the split VALU fills MFMA gaps.
+// Measured (skip fwd, M 32768 N 512 K 1600, same box, tools/gemm_exp.sh): 283-290 us against
+// 290 for the LDS-staged gemm_x3_kernel<..., 4, 2>; MFMA busy 54 % at a 1.97 GHz clock
+// (SQ_INSTS_MFMA·32 / SIMD vs GRBM_GUI_ACTIVE); timing-only ablations (wrong results): no
+// barrier 273, no A split 268, line-coalesced A loads 274, no A loads 241, no B fragment reads
+// 306 (the chip clocks down as the MFMAs pack closer: MI355X_MICROARCH.md 'DVFS give-back').
 __global__ __launch_bounds__(512, 1) void gemm_x3r_kernel(lbwn_gemm_args g) {
   constexpr int NTHR = 512, BM = 256, BN = 128, NI = 4;
   constexpr int SLOT = BN * X3_ROW;
@@ -703,24 +685,32 @@ __global__ __launch_bounds__(512, 1) void gemm_x3r_kernel(lbwn_gemm_args g) {
         acc[ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[PA[q]], fb[ni][PB[q]], acc[ni], 0, 0, 0);
     }
   };
-  // k-step kt: A in register set kt & 1 (= S ^ 1), B in LDS slot kt & 1; B of k-step kt + 1 is
-  // stored from register set S into the other slot
+  bf16x8 fa[2][3];
   auto step = [&](int kt, auto sset) {
     constexpr int S = decltype(sset)::value;   // = (kt + 1) & 1
     const unsigned short* cur = smem + (S ^ 1) * SLOT;
     unsigned short* nxt = smem + S * SLOT;
-    bf16x8 fa0[3], fa1[3], fb[NI][3];
-    a_split(std::integral_constant<int, S ^ 1>(), 0, fa0);
-    a_split(std::integral_constant<int, S ^ 1>(), 1, fa1);
-    a_load(std::integral_constant<int, S ^ 1>(), min(kt + 2, last));
+    bf16x8 fn[2][3], fb[NI][3];
     b_frags(cur, 0, fb);
-    mfmas(fa0, fb);
+    mfmas(fa[0], fb);
+    a_split(std::integral_constant<int, S>(), 0, fn[0]);
+    a_split(std::integral_constant<int, S>(), 1, fn[1]);
+    a_load(std::integral_constant<int, S>(), min(kt + 3, last));
     sp.template store<S>(nxt);
     sp.template load<S>(min(kt + 3, last));
     b_frags(cur, 1, fb);
-    mfmas(fa1, fb);
+    mfmas(fa[1], fb);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fa[c][p] = fn[c][p];
     __syncthreads();
   };
+  if (ntiles > 0) {
+    a_split(std::integral_constant<int, 0>(), 0, fa[0]);
+    a_split(std::integral_constant<int, 0>(), 1, fa[1]);
+    a_load(std::integral_constant<int, 0>(), min(2, last));
+  }
   int kt = 0;
   for (; kt + 1 < ntiles; kt += 2) {
     step(kt, std::integral_constant<int, 1>());
@@ -899,7 +889,7 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
   if (e) return e;
   const bool kfull = a.K % X3_BK == 0, pre = a.b3 != nullptr;
   if (wm == 4 && X3R && kfull && pre && a_kcontig) {
-    gemm_x3r_kernel<0><<<grid, 512, 0, st>>>(g);
+    gemm_x3r_kernel<<<grid, 512, 0, st>>>(g);
     LBWN_CHECK_LAUNCH();
   } else if (wm == 4) {
     if (kfull && pre) e = gemm_launch_x3_t<true, true, 4>(g, grid, a_kcontig, b_kcontig, st);
