@@ -35,6 +35,7 @@ struct lbwn_plan {
   size_t oPADP = 0, oPADG = 0;
   int ctrace_blk = -1;            // LBWN_CHAIN_TRACE=<block>: chain cycle stamps (debug)
   size_t oGCTAB, oGCD, oGCPART, oLCACT[8], oCOND, oDVALL, oLCCAT, oDLCCAT, oDLC[2];
+  size_t oLCCAT3 = 0;   // LCcat pre-split into bf16 planes (dlc's B; 0 = not used: K % 32 != 0)
   size_t oTGID = 0;              // GC + chain: per-tile uniform voice id (lbwn_gc_tile_sum_launch)
   // in-chain LC (bf16-split forward chain): L split LC images; COND is then computed only when a
   // backward path needs it (cond_valid: this step's COND is in the workspace)
@@ -382,6 +383,8 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     if (p->up_fused) p->oUPPART = carve(cur, f * (size_t)lbwn_lc_up_part_floats(p->nup, p->up, p->Li, p->Lo, (int)(M / hop)));
     p->oDVALL = p->Lo ? carve(cur, f * (size_t)M * ncond) : 0;
     p->oLCCAT = p->Lo ? carve(cur, f * (size_t)p->Lo * ncond) : 0;
+    if (p->Lo && ncond % 32 == 0)
+      p->oLCCAT3 = carve(cur, sizeof(unsigned short) * lbwn_split_planes_elems(p->Lo, (int)ncond));
     p->oDLCCAT = p->Lo ? carve(cur, f * (size_t)p->Lo * ncond) : 0;
     for (int i = 0; i < 2; ++i) p->oDLC[i] = p->Lo ? carve(cur, f * (size_t)M * std::max(p->Lo, p->Li)) : 0;
   }
@@ -607,6 +610,14 @@ int lc_dlc(lbwn_plan* p, const lbwn_params* P, void* ws, float* spl, hipStream_t
   g.A = at<float>(ws, p->oDVALL); g.lda = ncond; g.B = at<float>(ws, p->oLCCAT); g.ldb = ncond;
   g.C = at<float>(ws, p->oDLC[0]); g.ldc = p->Lo;
   g.M = (int)p->M; g.N = p->Lo; g.K = (int)ncond;
+  if (p->oLCCAT3 && lbwn_gemm_mode() == 1) {   // pre-split B: the A-in-registers GEMM (96-column tiles)
+    const float* w = g.B;
+    const long ld = ncond;
+    const int rows = p->Lo, K = (int)ncond, tr = 0;
+    unsigned short* o = at<unsigned short>(ws, p->oLCCAT3);
+    if ((e = lbwn_split_planes_launch(1, &w, &ld, &rows, &K, &tr, &o, st))) return e;
+    g.b3 = o;
+  }
   Probe(p, st, "lc_dlc");
   if ((e = lbwn_gemm_launch(g, 1, 1, p->split_dlcx, spl, st))) return e;
   Probe::end(p, st, "lc_dlc");

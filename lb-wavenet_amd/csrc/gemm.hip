@@ -362,7 +362,8 @@ struct X3Stage {
 // Pre-split operand [rows][K/32][3][32] bf16: ROWS rows × 12 granules of 16 B per k-step.
 template <int ROWS, int NTHR>
 struct X3Pre {
-  static constexpr int NV = ROWS * 12 / NTHR;
+  static constexpr int NV = (ROWS * 12 + NTHR - 1) / NTHR;   // the last may be partial (whole waves)
+  static_assert((ROWS * 12) % 64 == 0, "X3Pre: granules per wave");
   uintx4 v[2][NV];
   const unsigned short* p[NV];
   int ldst[NV];
@@ -382,7 +383,8 @@ struct X3Pre {
   template <int S = 0>
   LBWN_DEV void store(unsigned short* lds) {
 #pragma unroll
-    for (int i = 0; i < NV; ++i) *(uintx4*)(lds + ldst[i]) = v[S][i];
+    for (int i = 0; i < NV; ++i)
+      if ((ROWS * 12) % NTHR == 0 || (int)threadIdx.x + NTHR * i < ROWS * 12) *(uintx4*)(lds + ldst[i]) = v[S][i];
   }
 };
 
@@ -610,8 +612,9 @@ __global__ __launch_bounds__(128 * WM, (WM == 2 && STAGES == 1) ? X3_OCC : 1) vo
 // (SQ_INSTS_MFMA·32 / SIMD vs GRBM_GUI_ACTIVE); timing-only ablations (wrong results): no
 // barrier 273, no A split 268, line-coalesced A loads 274, no A loads 241, no B fragment reads
 // 306 (the chip clocks down as the MFMAs pack closer: MI355X_MICROARCH.md 'DVFS give-back').
+template <int NI>   // 4: 128 columns per tile; 3: 96 (N <= 96: arch5's dlc, N = 80)
 __global__ __launch_bounds__(512, 1) void gemm_x3r_kernel(lbwn_gemm_args g) {
-  constexpr int NTHR = 512, BM = 256, BN = 128, NI = 4;
+  constexpr int NTHR = 512, BM = 256, BN = 32 * NI;
   constexpr int SLOT = BN * X3_ROW;
   __shared__ __attribute__((aligned(16))) unsigned short smem[2 * SLOT];
 
@@ -764,13 +767,13 @@ __global__ __launch_bounds__(512, 1) void gemm_x3r_kernel(lbwn_gemm_args g) {
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
       cs[ni] += __shfl_xor(cs[ni], 32);
-      if (h == 0) red[wave * 128 + ni * 32 + ci] = cs[ni];
+      if (h == 0) red[wave * BN + ni * 32 + ci] = cs[ni];
     }
     __syncthreads();
     const int col = n0 + tid;
-    if (tid < 128 && col < g.N) {
+    if (tid < BN && col < g.N) {
       float s = 0.f;
-      for (int w = 0; w < 8; ++w) s += red[w * 128 + tid];
+      for (int w = 0; w < 8; ++w) s += red[w * BN + tid];
       g.colpart[(long)(m0 >> 8) * g.N + col] = s;
     }
   }
@@ -889,7 +892,12 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
   if (e) return e;
   const bool kfull = a.K % X3_BK == 0, pre = a.b3 != nullptr;
   if (wm == 4 && X3R && kfull && pre && a_kcontig) {
-    gemm_x3r_kernel<<<grid, 512, 0, st>>>(g);
+    if (a.N <= 96) {   // 96-column tiles: the grid is re-formed for them
+      grid.x = (unsigned)(((a.M + 255) / 256) * ((a.N + 95) / 96));
+      gemm_x3r_kernel<3><<<grid, 512, 0, st>>>(g);
+    } else {
+      gemm_x3r_kernel<4><<<grid, 512, 0, st>>>(g);
+    }
     LBWN_CHECK_LAUNCH();
   } else if (wm == 4) {
     if (kfull && pre) e = gemm_launch_x3_t<true, true, 4>(g, grid, a_kcontig, b_kcontig, st);

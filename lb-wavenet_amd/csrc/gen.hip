@@ -460,8 +460,29 @@ LBWN_DEV uint64_t splitmix(uint64_t seed, uint64_t stream, uint64_t step) {
 
 // v[j] = logit of code lane·per + j.  Returns the next input code of stream b after step t (the
 // teacher's or the draw); the writing wave stores logits, the sample, its µ-law decode, code[b].
+// µ-law decode of one code (ops.py:12-20)
+LBWN_DEV float mu_decode_q(int q, int Q) {
+  const float mu = (float)(Q - 1), inv = 1.f / mu;
+  const float aa = (2.f * (float)q - 1.f) * inv - 1.f;
+  const float sg = aa > 0.f ? 1.f : (aa < 0.f ? -1.f : 0.f);
+  return sg * (powf(1.f + mu, fabsf(aa)) - 1.f) * inv;
+}
+
+// the persistent form's wav: its draws store only the code (powf on lane 0 held the next step's
+// PRE row behind it); this decodes the run's samples [step - n, step) after the launch
+__global__ void gen_decode_kernel(const int* __restrict__ samples, float* __restrict__ wav, const long long* step,
+                                  int B, long long max_steps, int n, int Q) {
+  const long long t1 = min(*step, max_steps), t0 = max(*step - n, 0LL);
+  const long long span = t1 - t0;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)B * span;
+       e += (long long)gridDim.x * blockDim.x) {
+    const long long i = (e / span) * max_steps + t0 + e % span;
+    wav[i] = mu_decode_q(samples[i], Q);
+  }
+}
+
 template <int MP>
-LBWN_DEV int draw_core(float (&v)[MP], const DrawK& a, int b, long long t, bool write) {
+LBWN_DEV int draw_core(float (&v)[MP], const DrawK& a, int b, long long t, bool write, bool decode = true) {
   const int lane = threadIdx.x & 63, Q = a.Q;
   const int per = (Q + 63) >> 6, c0 = lane * per;
   float mx = -INFINITY;
@@ -502,10 +523,7 @@ LBWN_DEV int draw_core(float (&v)[MP], const DrawK& a, int b, long long t, bool 
   if (write && lane == 0) {
     if (t < a.max_steps) {
       a.samples[(long)b * a.max_steps + t] = found;
-      const float mu = (float)(Q - 1), inv = 1.f / mu;               // ops.py:12-20
-      const float aa = (2.f * (float)found - 1.f) * inv - 1.f;
-      const float sg = aa > 0.f ? 1.f : (aa < 0.f ? -1.f : 0.f);
-      a.wav[(long)b * a.max_steps + t] = sg * (powf(1.f + mu, fabsf(aa)) - 1.f) * inv;
+      if (decode) a.wav[(long)b * a.max_steps + t] = mu_decode_q(found, Q);
     }
     a.code[b] = next;
   }
@@ -551,6 +569,9 @@ __global__ __launch_bounds__(64) void gen_sample_kernel(DrawK a, const long long
   else draw_wave<4>(a, blockIdx.x, t, true);
 }
 
+#ifndef LBWN_GEN_SUBSTAMPS
+#define LBWN_GEN_SUBSTAMPS 0
+#endif
 constexpr long long G_SPIN_TIMEOUT = 400000000LL;   // wall_clock64 ticks (100 MHz) = 4 s
 
 // ---- persistent generation: one launch per run (B <= 16) --------------------------------
@@ -665,10 +686,15 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm) {
         bl = (blO + 1 == a.nbl) ? 0 : blO + 1;
       }
     };
-    auto issue = [&](long g) {   // weights of global layer g into slot g mod G_NS
-      const int l = (int)(g % L);
+    // the layer and ring slot of the next issue, advanced with wrap-around: g mod L and g mod G_NS
+    // of a 64-bit g were two long divisions per layer on the loaders' path to every barrier
+    int iss_l = 0, iss_slot = 0;
+    auto issue = [&](long /*g: layer iss_l, slot iss_slot*/) {   // weights of global layer g into slot g mod G_NS
+      const int l = iss_l;
       const float* src = a.img + (long)l * GIMG;
-      float* dst = RING + (g % G_NS) * G_SLOT;
+      float* dst = RING + iss_slot * G_SLOT;
+      iss_l = (iss_l + 1 == L) ? 0 : iss_l + 1;
+      iss_slot = (iss_slot + 1 == G_NS) ? 0 : iss_slot + 1;
 #pragma unroll
       for (int p = 0; p < G_PIECES; ++p) {
         const int pc = lw * G_PIECES + p;
@@ -728,7 +754,11 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm) {
   const int xin_off = kq < 2 ? 16 * kq : 16 * (kq - 2);
   const int Q = a.Q, per = (Q + 63) >> 6, c0 = lane * per;
   long long* tr = (a.trace && b == 0 && threadIdx.x == 0) ? a.trace : nullptr;
+  float bq[4];               // b2 of this lane's codes, loaded once (a global load in every draw before)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bq[j] = a.draw.bias ? a.draw.bias[min(c0 + j, Q - 1)] : 0.f;
   int code = a.code_in[b];   // step 0 of the run: the previous run's last draw (-1 at t = 0)
+  int slot = 0;              // ring slot of global layer G = s·L + l (G mod G_NS, advanced per layer)
   for (int s = 0; s <= n; ++s) {
     const long long t = t0 + s;
     if (s > 0) {
@@ -747,9 +777,9 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm) {
       for (int j = 0; j < 4; ++j) {
         const int cc = min(c0 + j, Q - 1);
         lv[j] = DL[cc] + DL[256 + cc];
-        if (a.draw.bias) lv[j] += a.draw.bias[cc];
+        if (a.draw.bias) lv[j] += bq[j];
       }
-      code = draw_core<4>(lv, a.draw, b, t - 1, w == 0);
+      code = draw_core<4>(lv, a.draw, b, t - 1, w == 0, false);
       if (s == n) {
         if (tr) tr[6] = wall_clock64();
         break;
@@ -766,8 +796,8 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm) {
     int bl = 0;
     lds_barrier();   // -1
     for (int l = 0; l < L; ++l) {
-      const long G = (long)s * L + l;
-      const float* S = RING + (G % G_NS) * G_SLOT;
+      const float* S = RING + slot * G_SLOT;
+      slot = (slot + 1 == G_NS) ? 0 : slot + 1;
       const float* xin = (kq < 2 ? XP + l * 32 : XW) + xin_off;
       floatx4 wv[4], xv[4];
 #pragma unroll
@@ -776,8 +806,13 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm) {
         xv[mm] = *(const floatx4*)(xin + 4 * mm);
       }
       const float bco = S[GI_WR + o] + S[GI_WR + 128 + o];
+      // (reading layer l+1's conv operands right after barrier l, and this layer's residual
+      // weights ahead of the conv, measured 38.0 -> 38.9 us per step: rejected)
       // sub-layer cycle stamps (trace only): layers 16..23 of the traced step, 6 per layer
-      long long* st6 = (tr && s == n - 1 && l >= 16 && l < 24 && L + 184 <= 2 * L + 136) ? tr + 8 + L + 128 + 6 * (l - 16) : nullptr;
+      // (compiled in only with -DLBWN_GEN_SUBSTAMPS=1: the lane-divergent stamp branches split the
+      // layer into basic blocks the scheduler cannot overlap, 38.5 -> 44 us per step at B = 10)
+      long long* st6 = (LBWN_GEN_SUBSTAMPS && tr && s == n - 1 && l >= 16 && l < 24 && L + 184 <= 2 * L + 136)
+                           ? tr + 8 + L + 128 + 6 * (l - 16) : nullptr;
       if (st6) st6[0] = clock64();
       __builtin_amdgcn_sched_barrier(0);
       const int d = 1 << bl;
@@ -1275,6 +1310,9 @@ extern "C" int lbwn_gen_run(lbwn_gen_plan* p, const lbwn_params* P, void* ws, in
     k.status = gat<int>(ws, p->oSTEP + 8);
     k.trace = p->trace ? gat<long long>(ws, p->oTRACE) : nullptr;
     gen_persist_kernel<<<p->B + P_NH, 512, 0, st>>>(k);
+    LBWN_CHECK_LAUNCH();
+    gen_decode_kernel<<<std::max(1, std::min(1024, (int)(((long long)p->B * n_steps + 255) / 256))), 256, 0, st>>>(
+        d.samples, d.wav, k.step, p->B, p->max_steps, n_steps, p->Q);
     LBWN_CHECK_LAUNCH();
     return 0;
   }
