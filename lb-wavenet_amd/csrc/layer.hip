@@ -627,7 +627,9 @@ static_assert(CF_LDS_X3LC * 4 + 16 <= 160 * 1024, "chain fwd x3 + LC LDS");
 // read with the own tap in step 7 of the previous layer (tile start for layer 0), and the image
 // two layers ahead is LDS-DMA'd in step 9, after the publish barrier (every wave is past its
 // reads), landing with the next layer's halo loads (in-order vmcnt) before its halo barrier.
-template <bool X3, bool LC, int CM>
+// TR: the traced build (in-kernel clock stamps, lbwn_plan's LBWN_CHAIN_TRACE): the stamps'
+// lane-divergent branches cost the untraced chains 0.5-3 % (same-box A/B, tools/ab_step.sh)
+template <bool X3, bool LC, int CM, bool TR>
 __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
   static_assert(X3 || !LC, "in-chain LC needs the split images");
   constexpr int IMGF = X3 ? XIMG_F : WIMG;              // floats per layer image
@@ -704,7 +706,7 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
       }
     }
     const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && tile == (int)blockIdx.x;
-#define FSTAMP(i) if (trc) a.trace[16 * l + (i)] = clock64()
+#define FSTAMP(i) if (TR && trc) a.trace[16 * l + (i)] = clock64()
     auto store_zs = [&](int ll, const floatx16& zz, const floatx16& ss) {
       if (valid) store_rows16(a.Z + m * a.ldz + (long)ll * a.Cd, zz, a.Cd, h);
       if (X3 && a.SG && valid) {
@@ -1476,6 +1478,7 @@ LBWN_DEV void gc_scatter_x3(float* gtab, long ld, const float* DVs, const float*
   }
 }
 
+template <bool TR>
 __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
   __shared__ __attribute__((aligned(16))) float sm[CBX_LDS];
   __shared__ int s_fail;
@@ -1541,7 +1544,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) oa[q] = 0.f;
     const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && it == (int)blockIdx.x;
-#define XSTAMP(i) if (trc) a.trace[16 * l + (i)] = clock64()
+#define XSTAMP(i) if (TR && trc) a.trace[16 * l + (i)] = clock64()
     for (int l = a.L - 1; l >= 0; --l) {
       XSTAMP(0);
       const int d = 1 << (l % a.nbl);
@@ -2224,6 +2227,13 @@ int lbwn_layer_reduce_launch(const lbwn_layer_red_args& r, hipStream_t st) {
 
 int lbwn_chain_fwd_lds_bytes() { return CF_LDS * 4; }
 
+// the untraced or the traced instantiation of one forward chain
+static void fwd_launch(bool traced, void (*plain)(ChainFK), void (*traced_k)(ChainFK), int grid, const ChainFK& k,
+                       hipStream_t st) {
+  if (traced) hipLaunchKernelGGL(traced_k, dim3(grid), dim3(256), 0, st, k);
+  else hipLaunchKernelGGL(plain, dim3(grid), dim3(256), 0, st, k);
+}
+
 int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   LBWN_REQUIRE(c.Cr == 32 && c.Cd == 32, "chain fwd: n_res = n_dil = 32 only");
   LBWN_REQUIRE(c.grid >= 1 && c.flags && c.status, "chain fwd: bad launch state");
@@ -2251,15 +2261,15 @@ int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   }
   const int cm = (!c.gc_tab && !c.cond) ? 0 : (c.gc_tab && !c.cond) ? 1 : 2;
   if (lc) {
-    if (cm == 0) chain_fwd_kernel<true, true, 0><<<c.grid, 256, 0, st>>>(k);
-    else chain_fwd_kernel<true, true, 1><<<c.grid, 256, 0, st>>>(k);   // lc: cond is null
+    if (cm == 0) fwd_launch(c.trace != nullptr, chain_fwd_kernel<true, true, 0, false>, chain_fwd_kernel<true, true, 0, true>, c.grid, k, st);
+    else fwd_launch(c.trace != nullptr, chain_fwd_kernel<true, true, 1, false>, chain_fwd_kernel<true, true, 1, true>, c.grid, k, st);   // lc: cond is null
   } else if (c.wpack_x3) {
-    if (cm == 0) chain_fwd_kernel<true, false, 0><<<c.grid, 256, 0, st>>>(k);
-    else if (cm == 1) chain_fwd_kernel<true, false, 1><<<c.grid, 256, 0, st>>>(k);
-    else chain_fwd_kernel<true, false, 2><<<c.grid, 256, 0, st>>>(k);
+    if (cm == 0) fwd_launch(c.trace != nullptr, chain_fwd_kernel<true, false, 0, false>, chain_fwd_kernel<true, false, 0, true>, c.grid, k, st);
+    else if (cm == 1) fwd_launch(c.trace != nullptr, chain_fwd_kernel<true, false, 1, false>, chain_fwd_kernel<true, false, 1, true>, c.grid, k, st);
+    else fwd_launch(c.trace != nullptr, chain_fwd_kernel<true, false, 2, false>, chain_fwd_kernel<true, false, 2, true>, c.grid, k, st);
   } else {
-    if (cm == 0) chain_fwd_kernel<false, false, 0><<<c.grid, 256, 0, st>>>(k);
-    else chain_fwd_kernel<false, false, 2><<<c.grid, 256, 0, st>>>(k);
+    if (cm == 0) fwd_launch(c.trace != nullptr, chain_fwd_kernel<false, false, 0, false>, chain_fwd_kernel<false, false, 0, true>, c.grid, k, st);
+    else fwd_launch(c.trace != nullptr, chain_fwd_kernel<false, false, 2, false>, chain_fwd_kernel<false, false, 2, true>, c.grid, k, st);
   }
   LBWN_CHECK_LAUNCH();
   return 0;
@@ -2287,7 +2297,8 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
     if (int e = lbwn_zero_launch(c.flags, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st)) return e;
   }
   LBWN_REQUIRE(x3 == (c.dzls > 0), "chain bwd: the bf16-split chain reads dZ in chain order (dzls), the f32 chain in rows");
-  if (x3) chain_bwd_x3_kernel<<<c.grid, 256, 0, st>>>(k);
+  if (x3 && k.trace) chain_bwd_x3_kernel<true><<<c.grid, 256, 0, st>>>(k);
+  else if (x3) chain_bwd_x3_kernel<false><<<c.grid, 256, 0, st>>>(k);
   else chain_bwd_kernel<<<c.grid, 256, 0, st>>>(k);
   LBWN_CHECK_LAUNCH();
   return 0;
