@@ -312,9 +312,10 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     p->split_dlc = pick_split(p->Lo, 2 * L * p->Cd, M);
     p->split_floats = std::max(p->split_floats, (long)p->split_dlc * p->Lo * 2 * L * p->Cd);
     // dlc = DV·LCcatᵀ (M × n_lc_out, K = L·2Cd): 256-row tiles, one N tile; split K until the
-    // grid has ~512 blocks (it ran on 128 blocks of 256 CUs at B = 8)
+    // grid has ~one block per CU (it ran on 128 blocks of 256 CUs at B = 8; it runs beside dLCcat,
+    // so 512 blocks measured slower: C5 per GPU 3.11 -> 3.06 ms at 256 blocks, same box)
     const long dtiles = (M + 255) / 256 * ((p->Lo + 127) / 128);
-    p->split_dlcx = (int)std::max<long>(1, std::min<long>(512 / std::max<long>(1, dtiles), (2L * L * p->Cd) / 256));
+    p->split_dlcx = (int)std::max<long>(1, std::min<long>(256 / std::max<long>(1, dtiles), (2L * L * p->Cd) / 256));
     p->split_floats = std::max(p->split_floats, (long)p->split_dlcx * M * p->Lo);
     long rows = (long)B * (T / hop);
     for (int i = 0; i < p->nup; ++i) {
