@@ -260,6 +260,9 @@ constexpr int X3_NT = 256;
 #ifndef X3_EXP
 #define X3_EXP 0   // timing experiments only: 2 = one product per block, 4 = no in-loop global loads
 #endif
+#ifndef X3Q
+#define X3Q 1        // the tall 128-column products on v_mfma_f32_16x16x32_bf16 (gemm_x3q_kernel)
+#endif
 #ifndef X3_OCC
 #define X3_OCC 2
 #endif
@@ -779,6 +782,178 @@ __global__ __launch_bounds__(512, 1) void gemm_x3r_kernel(lbwn_gemm_args g) {
   }
 }
 
+// The same tile and data flow on v_mfma_f32_16x16x32_bf16 (equal cycles per FLOP; the chip holds a
+// higher clock on it under load, MI355X_MICROARCH.md 'DVFS give-back' item 7): each wave's
+// 32 × 128 band is 2 × 8 accumulators of 16 × 16, one MFMA takes the whole 32-deep k-step.  Lane
+// l = (r = l & 15, q = l >> 4) supplies A[16mi + r][8q + j] (one 32-B run of a row per mi: a row's
+// four lanes cover its 128-B line) and B[8q + j][16ni + r]; the k-step runs as two halves of 4
+// column blocks.
+template <int NB>   // 16-column blocks: 8 (128 columns) or 6 (96: N <= 96, arch5's dlc)
+__global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
+  constexpr int NTHR = 512, BM = 256, BN = 16 * NB, NH = NB / 2;
+  constexpr int SLOT = BN * X3_ROW;
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_n = (g.N + BN - 1) / BN;
+  if (g.step_advance && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && tid == 0)   // no-return atomic
+    __hip_atomic_fetch_add(g.step_advance, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int t = gemm_tile();
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  const int kz0 = gemm_split() * g.k_per_split;
+  const int kz1 = min(g.K, kz0 + g.k_per_split);
+  const int ntiles = (kz1 - kz0) / X3_BK;   // K % 32 == 0 (pre-split B)
+  const int last = max(ntiles - 1, 0);
+
+  floatx4 acc[2][NB];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[a][b] = (floatx4){0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const float* pa0 = g.A + (long)min(m0 + 32 * wave + fr, g.M - 1) * g.lda + kz0 + 8 * fq;
+  const float* pa1 = g.A + (long)min(m0 + 32 * wave + 16 + fr, g.M - 1) * g.lda + kz0 + 8 * fq;
+  const int alo = g.relu_a ? 0 : (int)0x80000000;   // relu as an integer max (x3_store4)
+  floatx4 av[2][4];
+  auto a_load = [&](auto sset, int kt) {
+    constexpr int S = decltype(sset)::value;
+    av[S][0] = *(const floatx4*)(pa0 + kt * X3_BK);
+    av[S][1] = *(const floatx4*)(pa0 + kt * X3_BK + 4);
+    av[S][2] = *(const floatx4*)(pa1 + kt * X3_BK);
+    av[S][3] = *(const floatx4*)(pa1 + kt * X3_BK + 4);
+  };
+  auto a_split = [&](auto sset, int mi, bf16x8 (&f)[3]) {
+    constexpr int S = decltype(sset)::value;
+    floatx4 x = av[S][2 * mi], y = av[S][2 * mi + 1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x[j] = __int_as_float(max(__float_as_int(x[j]), alo));
+      y[j] = __int_as_float(max(__float_as_int(y[j]), alo));
+    }
+    split8(x, y, f);
+  };
+
+  X3Pre<BN, NTHR> sp;
+  sp.init(g.b3, g.K / X3_BK, n0, g.N, kz0, tid);
+  if (ntiles > 0) {
+    sp.load(0);
+    sp.store(smem);
+    a_load(std::integral_constant<int, 0>(), 0);
+    a_load(std::integral_constant<int, 1>(), min(1, last));
+    sp.template load<1>(min(1, last));
+    sp.template load<0>(min(2, last));
+  }
+  __syncthreads();
+  const int fb_off = fr * X3_ROW + 8 * fq;
+
+  auto b_frags = [&](const unsigned short* base, int half, bf16x8 (&f)[NH][3]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int nb = 0; nb < NH; ++nb) f[nb][p] = *(const bf16x8*)(base + fb_off + (NH * half + nb) * 16 * X3_ROW + 32 * p);
+  };
+  auto mfmas = [&](const bf16x8 (&fa)[2][3], const bf16x8 (&fb)[NH][3], int half) {
+    // small terms first: a2b0, a1b1, a0b2, a1b0, a0b1, a0b0
+#pragma unroll
+    for (int qq = 0; qq < 6; ++qq) {
+      constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int nb = 0; nb < NH; ++nb)
+          acc[mi][NH * half + nb] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mi][PA[qq]], fb[nb][PB[qq]], acc[mi][NH * half + nb], 0, 0, 0);
+    }
+  };
+  bf16x8 fa[2][3];
+  auto step = [&](int kt, auto sset) {
+    constexpr int S = decltype(sset)::value;   // = (kt + 1) & 1
+    const unsigned short* cur = smem + (S ^ 1) * SLOT;
+    unsigned short* nxt = smem + S * SLOT;
+    bf16x8 fn[2][3], fb[NH][3];
+    b_frags(cur, 0, fb);
+    mfmas(fa, fb, 0);
+    a_split(std::integral_constant<int, S>(), 0, fn[0]);
+    a_split(std::integral_constant<int, S>(), 1, fn[1]);
+    a_load(std::integral_constant<int, S>(), min(kt + 3, last));
+    sp.template store<S>(nxt);
+    sp.template load<S>(min(kt + 3, last));
+    b_frags(cur, 1, fb);
+    mfmas(fa, fb, 1);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fa[c][p] = fn[c][p];
+    __syncthreads();
+  };
+  if (ntiles > 0) {
+    a_split(std::integral_constant<int, 0>(), 0, fa[0]);
+    a_split(std::integral_constant<int, 0>(), 1, fa[1]);
+    a_load(std::integral_constant<int, 0>(), min(2, last));
+  }
+  int kt = 0;
+  for (; kt + 1 < ntiles; kt += 2) {
+    step(kt, std::integral_constant<int, 1>());
+    step(kt + 1, std::integral_constant<int, 0>());
+  }
+  if (kt < ntiles) step(kt, std::integral_constant<int, 1>());
+
+  // epilogue: element (mi, nb, i) is row rbase + 16mi + 4q + i, column n0 + 16nb + r
+  float* C = g.C + (long)gemm_split() * g.split_stride;
+  const bool raw = g.split_stride != 0;
+  const int rbase = m0 + 32 * wave;
+  float cs[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    cs[nb] = 0.f;
+    const int col = n0 + nb * 16 + fr, colc = min(col, g.N - 1);
+    float mv[8], cv[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int rowc = min(rbase + 16 * (e >> 2) + 4 * fq + (e & 3), g.M - 1);
+      if (!raw && g.mask) mv[e] = g.mask[(long)rowc * g.ldm + colc];
+      if (!raw && g.accumulate) cv[e] = C[(long)rowc * g.ldc + colc];
+    }
+    const float bv = (!raw && g.bias) ? g.bias[colc] : 0.f;
+    if (col >= g.N) continue;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int row = rbase + 16 * (e >> 2) + 4 * fq + (e & 3);
+      float v = acc[e >> 2][nb][e & 3];
+      if (!raw) {
+        v += bv;
+        if (g.relu_out) v = fmaxf(v, 0.f);
+        if (g.mask && !(mv[e] > 0.f)) v = 0.f;
+        if (g.accumulate) v += cv[e];
+      }
+      if (row < g.M) {
+        if (g.c_chain_ls)
+          C[(col >> 5) * g.c_chain_ls + ((((long)(row >> 5) * 4 + ((col >> 3) & 3)) * 32 + (row & 31)) * 8 + (col & 7))] = v;
+        else
+          C[(long)row * g.ldc + col] = v;
+        cs[nb] += v;
+      }
+    }
+  }
+  if (g.colpart && !raw) {   // the block's 256-row column partials: lane quarters, then waves in order
+    float* red = (float*)smem;   // free after the k-loop's last barrier
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      cs[nb] += __shfl_xor(cs[nb], 16);
+      cs[nb] += __shfl_xor(cs[nb], 32);
+      if (fq == 0) red[wave * BN + nb * 16 + fr] = cs[nb];
+    }
+    __syncthreads();
+    const int col = n0 + tid;
+    if (tid < BN && col < g.N) {
+      float s = 0.f;
+      for (int w = 0; w < 8; ++w) s += red[w * BN + tid];
+      g.colpart[(long)(m0 >> 8) * g.N + col] = s;
+    }
+  }
+}
+
 // Pre-split planes of weights W (f32, row stride ldw): out[r][kc][plane][32] = split of
 // W[r][32·kc + j] (k-contiguous, trans = 0) or W[32·kc + j][r] (trans = 1); k ≥ K is zero.
 // Up to 6 weights per launch (blockIdx.y = job).
@@ -894,7 +1069,10 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
   if (wm == 4 && X3R && kfull && pre && a_kcontig) {
     if (a.N <= 96) {   // 96-column tiles: the grid is re-formed for them
       grid.x = (unsigned)(((a.M + 255) / 256) * ((a.N + 95) / 96));
-      gemm_x3r_kernel<3><<<grid, 512, 0, st>>>(g);
+      if (X3Q) gemm_x3q_kernel<6><<<grid, 512, 0, st>>>(g);
+      else gemm_x3r_kernel<3><<<grid, 512, 0, st>>>(g);
+    } else if (X3Q) {
+      gemm_x3q_kernel<8><<<grid, 512, 0, st>>>(g);
     } else {
       gemm_x3r_kernel<4><<<grid, 512, 0, st>>>(g);
     }
