@@ -7,7 +7,9 @@ so the same variables are written as ONE safetensors file ``<ckpt_path>-<step>.s
 with identical keys; the optimizer's TF1 Adam slots may ride along under TF's slot names
 (``<var>/Adam``, ``<var>/Adam_1``) so a resume is exact.  ``max_to_keep`` rotation follows
 tf.train.Saver (oldest files deleted beyond n_keep_checkpoints).  Loading never unpickles:
-safetensors only.
+safetensors only.  A reference-written TF V2 bundle (``<pfx>-<step>.index`` +
+``.data-00000-of-00001``) at the same prefix is read when no safetensors file is there
+(lbwn/tfckpt.py), and ``export_tf_bundle`` writes one the reference's Saver can restore.
 """
 import os
 import sys
@@ -15,6 +17,8 @@ import sys
 import numpy as np
 import torch
 from safetensors.torch import load_file, save_file
+
+from . import tfckpt
 
 SUFFIX = '.safetensors'
 
@@ -41,8 +45,11 @@ def save_tensors(path, tensors):
 
 
 def load_tensors(path):
-    """{name: cpu tensor} from '<pfx>-<step>' prefixes or a .safetensors path."""
+    """{name: cpu tensor} from '<pfx>-<step>' prefixes or a .safetensors path; a TF V2 bundle
+    at the prefix when there is no safetensors file (the reference's own checkpoints)."""
     f = ckpt_file(path)
+    if not os.access(f, os.R_OK) and not path.endswith(SUFFIX) and tfckpt.exists(path):
+        return {k: torch.from_numpy(np.array(v)) for k, v in tfckpt.read_bundle(path).items()}
     if not os.access(f, os.R_OK):
         print("Couldn't find checkpoint file {}".format(f), file=sys.stderr)   # ckpt.py:71-75
         sys.exit(1)
@@ -95,9 +102,27 @@ class Checkpoint:
         with torch.no_grad():
             for k, dst in self.saveable_objects.items():
                 src = loaded[k]
+                if src.dim() == 0 and dst.numel() == 1:   # TF's scalar GLOBAL_STEP / VALID_SAMPLES
+                    src = src.reshape(dst.shape)
                 if tuple(src.shape) != tuple(dst.shape):
                     print('Checkpoint {}: {} has shape {}, model expects {}'.format(
                         f, k, tuple(src.shape), tuple(dst.shape)), file=sys.stderr)
                     sys.exit(1)
                 dst.copy_(src.to(dst.dtype))
         return loaded
+
+
+# the reference's scalar int32 counters (tmodel.py:223-226, arch.py:101-102); the rest keep dtype/shape
+_TF_SCALARS = ('GLOBAL_STEP', 'VALID_SAMPLES')
+
+
+def export_tf_bundle(tensors, prefix):
+    """Write {name: tensor} as a TF V2 bundle at ``prefix`` in the reference's variable forms
+    (GLOBAL_STEP / VALID_SAMPLES as int32 scalars); returns the prefix."""
+    out = {}
+    for k, v in tensors.items():
+        a = (v.detach().to('cpu') if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))).numpy()
+        if k in _TF_SCALARS:
+            a = np.asarray(a.reshape(()), dtype=np.int32)
+        out[k] = a
+    return tfckpt.write_bundle(prefix, out)
