@@ -335,22 +335,52 @@ __global__ void fill_kernel(float* p, float v, long n) {
 // counters[2] (int64) is Adam's apply count t-1; lr_t = lr·√(1-β2^t)/(1-β1^t).
 // status (nullable): the step's chain status word; nonzero = a hand-off timed out and the
 // gradients are garbage, so the update is skipped (params, m, v untouched).
-__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ gr, float* __restrict__ m,
-                            float* __restrict__ v, long nw, long n, float lr, float b1, float b2, float eps,
-                            float l2, const float* stats, const long long* counters, const unsigned* status) {
+// one element of TF1 Adam (training_ops.cc ApplyAdam restated: m, v, then θ -= lr_t·m/(√v + ε))
+LBWN_DEV float adam_elem(float th, float g, float& m, float& v, float lr_t, float b1, float b2, float eps) {
+  const float mm = b1 * m + (1.f - b1) * g;
+  const float vv = b2 * v + (1.f - b2) * g * g;
+  m = mm;
+  v = vv;
+  return th - lr_t * mm / (sqrtf(vv) + eps);
+}
+
+// Four elements per thread as dwordx4 loads and stores (the flat buffers are 16-B aligned, checked
+// by the launcher); the n % 4 tail elements one per thread.  HBM-bound: 28 B per parameter.
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ gr,
+                                                   float* __restrict__ m, float* __restrict__ v, long nw, long n,
+                                                   float lr, float b1, float b2, float eps, float l2,
+                                                   const float* stats, const long long* counters,
+                                                   const unsigned* status) {
   if (status && *status) return;
   const double t = (double)(counters[2] + 1);
   const float lr_t = (float)((double)lr * sqrt(1.0 - pow((double)b2, t)) / (1.0 - pow((double)b1, t)));
   const float inv = stats ? (stats[1] > 0.f ? 1.f / stats[1] : 0.f) : 1.f;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
-    const float th = p[e];
+  const long n4 = n >> 2;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const floatx4 th = ((const floatx4*)p)[i];
+    floatx4 g = ((const floatx4*)gr)[i];
+    floatx4 mm = ((const floatx4*)m)[i], vv = ((const floatx4*)v)[i], out;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gj = g[j] * inv;
+      if (4 * i + j < nw) gj += l2 * th[j];
+      float mj = mm[j], vj = vv[j];
+      out[j] = adam_elem(th[j], gj, mj, vj, lr_t, b1, b2, eps);
+      mm[j] = mj;
+      vv[j] = vj;
+    }
+    ((floatx4*)m)[i] = mm;
+    ((floatx4*)v)[i] = vv;
+    ((floatx4*)p)[i] = out;
+  }
+  const long e = 4 * n4 + blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (e < n) {
     float g = gr[e] * inv;
-    if (e < nw) g += l2 * th;
-    const float mm = b1 * m[e] + (1.f - b1) * g;
-    const float vv = b2 * v[e] + (1.f - b2) * g * g;
-    m[e] = mm;
-    v[e] = vv;
-    p[e] = th - lr_t * mm / (sqrtf(vv) + eps);
+    if (e < nw) g += l2 * p[e];
+    float mj = m[e], vj = v[e];
+    p[e] = adam_elem(p[e], g, mj, vj, lr_t, b1, b2, eps);
+    m[e] = mj;
+    v[e] = vj;
   }
 }
 
@@ -540,8 +570,10 @@ int lbwn_fill_launch(float* p, float v, long n, hipStream_t st) {
 int lbwn_adam_launch2(float* params, const float* grads, float* m, float* v, long nw, long n, float lr, float b1,
                       float b2, float eps, float l2, const float* stats, const long long* counters, const unsigned* status,
                       hipStream_t st) {
-  adam_kernel<<<grid_for(n, 256, 4096), 256, 0, st>>>(params, grads, m, v, nw, n, lr, b1, b2, eps, l2, stats,
-                                                      counters, status);
+  LBWN_REQUIRE(!(((uintptr_t)params | (uintptr_t)grads | (uintptr_t)m | (uintptr_t)v) & 15),
+               "adam: parameter, gradient and slot buffers must be 16-byte aligned");
+  adam_kernel<<<grid_for(std::max(n / 4, 1L), 256, 4096), 256, 0, st>>>(params, grads, m, v, nw, n, lr, b1, b2, eps,
+                                                                        l2, stats, counters, status);
   LBWN_CHECK_LAUNCH();
   return 0;
 }

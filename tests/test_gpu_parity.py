@@ -465,3 +465,30 @@ def test_adam_step_matches_oracle():
         assert d.max() <= 2 * 3 * 1e-3 + 1e-6, name
         assert np.mean(d) <= 2e-6, (name, np.mean(d))
     assert net.counters[0].item() == 3 and net.counters[1].item() == 3 * st['n_valid']
+
+
+@pytest.mark.parametrize('n,nw', [(1003, 501), (4096, 4096), (7, 3), (1, 0)])
+def test_adam_kernel_ragged(lib, n, nw):
+    """lbwn_adam_tf1 on lengths that are not multiples of its 4-wide vector step and a weight /
+    bias boundary inside a vector: TF1 Adam (training_ops.cc ApplyAdam; oracle AdamTF1) with the
+    l2 term on the first nw elements and the gradient scaled by 1 / n_valid, at step t = 5."""
+    rng = np.random.default_rng(n)
+    p0, g0, m0 = (rng.standard_normal(n).astype(np.float32) for _ in range(3))
+    v0 = rng.random(n).astype(np.float32)
+    dev = 'cuda'
+    p, g, m, v = (torch.tensor(a, device=dev) for a in (p0, g0, m0, v0))
+    stats = torch.tensor([0.0, 7.0, 0.0, 0.0], device=dev)
+    counters = torch.tensor([4, 0, 4, 0], dtype=torch.int64, device=dev)
+    lr, b1, b2, eps, l2 = 1e-3, 0.9, 0.999, 1e-8, 1e-3
+    _lib.check(lib.lbwn_adam_tf1(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), nw, n, lr, b1, b2, eps, l2,
+                                 stats.data_ptr(), counters.data_ptr(), None, None))
+    torch.cuda.synchronize()
+    gd = g0.astype(np.float64) / 7.0
+    gd[:nw] += l2 * p0[:nw]
+    md = b1 * m0 + (1 - b1) * gd
+    vd = b2 * v0 + (1 - b2) * gd * gd
+    lr_t = lr * np.sqrt(1 - b2 ** 5) / (1 - b1 ** 5)
+    pd = p0 - lr_t * md / (np.sqrt(vd) + eps)
+    np.testing.assert_allclose(m.cpu().numpy(), md, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(v.cpu().numpy(), vd, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(p.cpu().numpy(), pd, rtol=1e-6, atol=1e-7)

@@ -42,7 +42,7 @@ def per_name(rows, skip_steps=8):
             for k, n in NAMED.items():
                 if k in name:
                     key = n
-            if 'gemm_f32_kernel' in name or 'gemm_x3_kernel' in name:
+            if any(g in name for g in ('gemm_f32_kernel', 'gemm_x3_kernel', 'gemm_x3r_kernel', 'gemm_x3q_kernel')):
                 key = GEMM_ORDER[gi] if gi < len(GEMM_ORDER) else 'gemm%d' % gi
                 gi += 1
             if key:
