@@ -138,7 +138,8 @@ def _gen(net, arch, B, chunk, max_steps, env=None):
 
 def _gen_form(g, B):
     if g.persistent:
-        return 'persistent (one launch per chunk)'
+        groups = (B + 15) // 16
+        return 'persistent (one launch per chunk%s)' % (', %d stream groups' % groups if groups > 1 else '')
     return 'per-step, head as MFMA GEMMs' if B > 16 else 'per-step, head as vector GEMVs'
 
 

@@ -147,7 +147,8 @@ int lbwn_gen_start(lbwn_gen_plan* plan, const lbwn_params* params, void* workspa
  * plans (lbwn_gen_is_persistent) run the whole call as ONE launch whose blocks must all be
  * resident: nothing else may occupy the device's CUs meanwhile. */
 int lbwn_gen_run(lbwn_gen_plan* plan, const lbwn_params* params, void* workspace, int n_steps, void* stream);
-/* 1 when the plan runs the persistent one-launch form (B <= 16 and the layer/head sizes fit;
+/* 1 when the plan runs the persistent one-launch form (groups of <= 16 streams, each with its
+ * own 32 head blocks, while every block fits on the device: B <= 80 on 256 CUs; layer/head sizes fit;
  * LBWN_GEN_PERSIST=0 at plan creation selects the per-step launches), else 0. */
 int lbwn_gen_is_persistent(const lbwn_gen_plan* plan);
 

@@ -5,7 +5,8 @@
 // cache: layer l keeps its last d inputs, slot t mod d, replacing imodel's shift-by-chunk
 // buffers imodel.py:88-98, :190-207), the next input code, the teacher vector and a
 // counter-based RNG.  Two execution forms, chosen at plan creation:
-//   persistent (B <= 16, the default there): ONE launch per run, gen_persist_kernel — chain
+//   persistent (the default while its blocks fit: groups of <= 16 streams, each group with its
+//     own head blocks, B <= 80 on 256 CUs): ONE launch per run, gen_persist_kernel — chain
 //     blocks (one per stream) and 32 head blocks hand z, the skip vector and the partial logits
 //     to each other as tagged granules; weights of the head stay in registers for the run
 //   per step (any B): gen_wave (one workgroup per stream: PRE row (+bias), 50 × [dilated conv,
@@ -574,8 +575,10 @@ __global__ __launch_bounds__(64) void gen_sample_kernel(DrawK a, const long long
 #endif
 constexpr long long G_SPIN_TIMEOUT = 400000000LL;   // wall_clock64 ticks (100 MHz) = 4 s
 
-// ---- persistent generation: one launch per run (B <= 16) --------------------------------
-// Roles (one 512-thread workgroup per CU, all resident: B + P_NH <= CUs):
+// ---- persistent generation: one launch per run (stream groups of <= 16) ----------------
+// Roles (one 512-thread workgroup per CU, all resident): streams split into groups of Bg <= 16, each
+// group's Bg chain blocks and P_NH head blocks hand off among themselves only (groups x (Bg + P_NH)
+// <= CUs; B = 64: four groups, 192 blocks); within a group:
 //   chain block b < B   per step: draw the previous step (gather the P_NH partial-logit
 //                       granules of stream b, Σ + b2, wave-level draw), PRE row, 50 layers as in
 //                       gen_wave (LDS-DMA ring continuous across steps; the next step's taps are
@@ -594,7 +597,7 @@ constexpr long long G_SPIN_TIMEOUT = 400000000LL;   // wall_clock64 ticks (100 M
 // (status 5).  Three hops per step (z tail, skip all-gather, logit partials) replace the
 // per-step path's four launch boundaries and its weight re-fetches.
 constexpr int P_NH = 32;     // head blocks
-constexpr int P_MAXB = 16;   // streams (beyond 16 the per-step form is faster: measured 90 vs 87 us at B 32 / 64)
+constexpr int P_MAXB = 16;   // streams per group (phase A maps 16 columns x 16 streams onto 512 threads)
 constexpr int P_MAXL = 236;  // layers (the draw's two half-sums use tap-table rows 240..255)
 constexpr int P_DLROW = 240;
 constexpr int P_LA = 8;      // layers per head round (phase A)
@@ -611,6 +614,9 @@ struct PersistK {
   DrawK draw;               // outputs; draw.bias = b2
   int* status;
   long long* trace;         // wall stamps of the run's last step (tools/gen_trace.py), or null
+  int Bg;                   // streams per group: block g·(Bg + P_NH) + r is group g's chain block r < Bg
+                            // (stream g·Bg + r) or head block r - Bg; groups hand off only inside
+  long long* gstep;         // step counters of groups 1.. (group 0's is *step, the plan's "step")
 };
 
 // poll granules base[off + i·stride], i < nv (N at most; the rest re-read granule nv-1), until
@@ -655,12 +661,12 @@ LBWN_DEV void dma4_sc1(const float* src, float* lds_dst) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 4, 0, 16);
 }
 
-LBWN_DEV void persist_chain(const PersistK& a, float* sm) {
+LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* stepc, long long* trace) {
   float* RING = sm;                  // [G_NS][G_SLOT]
   float* XP = sm + G_NS * G_SLOT;    // [L][32] dilated taps of this step
   float* DL = XP + P_DLROW * 32;     // [2][256] half-sums of the partial logits of the step being drawn
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, b = blockIdx.x, L = a.L, n = a.n_steps;
-  const long long t0 = *a.step;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, L = a.L, n = a.n_steps;
+  const long long t0 = *stepc;
   const long GT = (long)n * L;       // layers of the run, in order: global index g = s·L + l
 
   if (wid >= 4) {   // ---- loader waves
@@ -753,7 +759,7 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm) {
   float* Z = XP + (G_MAXL + 2) * 32 + 128;
   const int xin_off = kq < 2 ? 16 * kq : 16 * (kq - 2);
   const int Q = a.Q, per = (Q + 63) >> 6, c0 = lane * per;
-  long long* tr = (a.trace && b == 0 && threadIdx.x == 0) ? a.trace : nullptr;
+  long long* tr = (trace && b == 0 && threadIdx.x == 0) ? trace : nullptr;
   float bq[4];               // b2 of this lane's codes, loaded once (a global load in every draw before)
 #pragma unroll
   for (int j = 0; j < 4; ++j) bq[j] = a.draw.bias ? a.draw.bias[min(c0 + j, Q - 1)] : 0.f;
@@ -860,13 +866,14 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm) {
     }
     if (tr && s == n - 1) tr[1] = wall_clock64();
   }
-  if (b == 0 && threadIdx.x == 0) *a.step = t0 + n;   // every block read it at its start (see header)
+  if (b % a.Bg == 0 && threadIdx.x == 0) *stepc = t0 + n;   // the group's blocks read it at their start
 }
 
-LBWN_DEV void persist_head(const PersistK& a, int m, float* sm) {
+LBWN_DEV void persist_head(const PersistK& a, int m, float* sm, int b0, int B, long long* stepc, long long* trace) {
+  // B: this group's streams b0 .. b0+B-1 (granule and logit layouts are over all a.B streams)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int B = a.B, L = a.L, Cd = a.Cd, Cs = a.Cs, Cp = a.Cp, Q = a.Q, n = a.n_steps;
-  const long long t0 = *a.step;
+  const int L = a.L, Cd = a.Cd, Cs = a.Cs, Cp = a.Cp, Q = a.Q, n = a.n_steps;
+  const long long t0 = *stepc;
   float* ZS = sm;                  // [2][P_LA layers][16 b][32 k] z of a round (double-buffered)
   float* RS = ZS + 2 * P_LA * 512; // [16 b][512 k] relu(skip + Σb), zero-padded
   float* HP = RS + P_MAXB * 512;   // [32 kg][16 b][16 c] per-thread partials (skip, then post1)
@@ -892,7 +899,7 @@ LBWN_DEV void persist_head(const PersistK& a, int m, float* sm) {
   // z granules polled by this thread: (stream zb0, channel zk) of every layer of a round
   const int zb0 = tid >> 5, zk = tid & 31;
   const bool zn0 = zb0 < B && zk < Cd;
-  long long* tr = (a.trace && m == P_NH - 1 && tid == 0) ? a.trace : nullptr;
+  long long* tr = (trace && m == P_NH - 1 && tid == 0) ? trace : nullptr;
   for (int s = 0; s < n; ++s) {
     const unsigned tag = (unsigned)(t0 + s + 1);
     // A. skip columns, P_LA layers per round: the round's z granules and this lane's 8 weights
@@ -911,7 +918,7 @@ LBWN_DEV void persist_head(const PersistK& a, int m, float* sm) {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         wv8[j] = wsrc[((long)min(li, L - 1) * Cd + min(j, Cd - 1 - 8 * kql)) * Cs];
-      sweep<P_LA>(a.zg, (unsigned)(((zn0 ? zb0 : 0) * L + l0) * 32 + (zn0 ? zk : 0)), 32u, nl, tag, zv, a.status);
+      sweep<P_LA>(a.zg, (unsigned)((b0 + (zn0 ? zb0 : 0)) * L + l0) * 32 + (zn0 ? zk : 0), 32u, nl, tag, zv, a.status);
       if (tr && s == n - 1) tr[8 + L + 40 + r] = wall_clock64();
 #pragma unroll
       for (int j = 0; j < 8; ++j)
@@ -955,14 +962,14 @@ LBWN_DEV void persist_head(const PersistK& a, int m, float* sm) {
         for (int g = 0; g < 32; ++g) v[g] = HP[(g * 16 + sb) * 16 + c];
 #pragma unroll
         for (int g = 0; g < 32; ++g) x += v[g];
-        put_granule(a.sg + (long)sb * Cs + scol, tag, x);   // B. publish this block's skip columns
+        put_granule(a.sg + (long)(b0 + sb) * Cs + scol, tag, x);   // B. publish this block's skip columns
       }
     }
     if (tr && s == n - 1) tr[2] = wall_clock64();
     // B. gather the whole skip vector: thread k = tid polls column k of every stream
     if (tid < Cs) {
       float v[P_MAXB];
-      sweep<P_MAXB>(a.sg, (unsigned)tid, (unsigned)Cs, B, tag, v, a.status);
+      sweep<P_MAXB>(a.sg, (unsigned)(b0 * Cs + tid), (unsigned)Cs, B, tag, v, a.status);
       const float bs = a.bsum ? a.bsum[tid] : 0.f;
 #pragma unroll
       for (int bb = 0; bb < P_MAXB; ++bb)
@@ -1033,7 +1040,7 @@ LBWN_DEV void persist_head(const PersistK& a, int m, float* sm) {
             lp = fmaf(hv[j][q][2], p2[4 * q + 2], lp);
             lp = fmaf(hv[j][q][3], p2[4 * q + 3], lp);
           }
-          if (g0 + j < B) put_granule(a.lg + ((long)m * B + g0 + j) * Q + tid, tag, lp);
+          if (g0 + j < B) put_granule(a.lg + ((long)m * a.B + b0 + g0 + j) * Q + tid, tag, lp);
         }
       }
     }
@@ -1043,8 +1050,13 @@ LBWN_DEV void persist_head(const PersistK& a, int m, float* sm) {
 
 __global__ __launch_bounds__(512) void gen_persist_kernel(PersistK a) {
   __shared__ __attribute__((aligned(16))) float sm[G_LDS];
-  if ((int)blockIdx.x < a.B) persist_chain(a, sm);
-  else persist_head(a, blockIdx.x - a.B, sm);
+  const int per = a.Bg + P_NH, g = blockIdx.x / per, r = blockIdx.x % per;
+  const int b0 = g * a.Bg, Bg = min(a.Bg, a.B - b0);
+  long long* stepc = g ? a.gstep + (g - 1) : a.step;
+  long long* trace = g ? nullptr : a.trace;
+  if (r < Bg) persist_chain(a, sm, b0 + r, stepc, trace);
+  else if (r >= a.Bg) persist_head(a, r - a.Bg, sm, b0, Bg, stepc, trace);
+  // (a ragged last group leaves chain slots r in [Bg, a.Bg) idle)
 }
 
 // gc_proj[l][b][o] = GC_EMBED[gc_id[b]] · [GC_SIGNAL_l | GC_GATE_l]  (imodel.py:53-56, :113-118)
@@ -1096,6 +1108,8 @@ struct lbwn_gen_plan {
   int gsplit[3] = {1, 1, 1};
   long n_gran;
   bool trace, persist;
+  int pgroups = 1, pbg = 0;   // persistent form: stream groups of pbg <= P_MAXB, each with its own P_NH heads
+  long n_gran_core = 0;       // granules before the groups' step counters
   int ksl_skip, ks_skip, ks_h, ks_lg;
   long n_ring;
   long long n_teacher, max_teacher;
@@ -1105,7 +1119,7 @@ struct lbwn_gen_plan {
 
 // the per-step GEMM form: large B, shapes the split GEMM takes (N % 4, K % 4, row strides)
 static bool gemm_form_ok(const lbwn_gen_plan* p) {
-  return p->B > P_MAXB && p->Cs % 4 == 0 && p->Cp % 4 == 0 && p->Q % 4 == 0 && (p->L * p->Cd) % 4 == 0;
+  return !p->persist && p->B > P_MAXB && p->Cs % 4 == 0 && p->Cp % 4 == 0 && p->Q % 4 == 0 && (p->L * p->Cd) % 4 == 0;
 }
 
 static size_t gcarve(size_t& cur, size_t bytes) {
@@ -1160,9 +1174,14 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
   const bool have_dev = hipGetDevice(&dev) == hipSuccess &&
                         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess;
   const char* pe = getenv("LBWN_GEN_PERSIST");
-  p->persist = (!pe || strcmp(pe, "0") != 0) && B <= P_MAXB && p->L <= P_MAXL && p->Q <= 256 && p->Cs <= 16 * P_NH &&
-               p->Cp <= 16 * P_NH && have_dev && B + P_NH <= ncu;
-  p->n_gran = (long)B * p->L * 32 + (long)B * p->Cs + (long)P_NH * B * p->Q;
+  // B > P_MAXB: ceil(B / P_MAXB) independent groups in the same launch while every block fits
+  // (4 x (16 + 32) = 192 blocks for B = 64 on 256 CUs; beyond that the per-step GEMM form)
+  p->pgroups = (B + P_MAXB - 1) / P_MAXB;
+  p->pbg = (B + p->pgroups - 1) / p->pgroups;
+  p->persist = (!pe || strcmp(pe, "0") != 0) && p->L <= P_MAXL && p->Q <= 256 && p->Cs <= 16 * P_NH &&
+               p->Cp <= 16 * P_NH && have_dev && p->pgroups * (p->pbg + P_NH) <= ncu;
+  p->n_gran_core = (long)B * p->L * 32 + (long)B * p->Cs + (long)P_NH * B * p->Q;
+  p->n_gran = p->n_gran_core + p->pgroups;   // + the groups' step counters (zeroed with the granules)
   p->oGRAN = gcarve(cur, 8 * (size_t)p->n_gran);
   if (gemm_form_ok(p)) {
     // split K until ~256 blocks of 128 x 128 tiles (M = B streams is short), >= 4 k-steps of 32 each
@@ -1309,7 +1328,9 @@ extern "C" int lbwn_gen_run(lbwn_gen_plan* p, const lbwn_params* P, void* ws, in
     k.draw = d;
     k.status = gat<int>(ws, p->oSTEP + 8);
     k.trace = p->trace ? gat<long long>(ws, p->oTRACE) : nullptr;
-    gen_persist_kernel<<<p->B + P_NH, 512, 0, st>>>(k);
+    k.Bg = p->pbg;
+    k.gstep = reinterpret_cast<long long*>(g + p->n_gran_core);
+    gen_persist_kernel<<<p->pgroups * (p->pbg + P_NH), 512, 0, st>>>(k);
     LBWN_CHECK_LAUNCH();
     gen_decode_kernel<<<std::max(1, std::min(1024, (int)(((long long)p->B * n_steps + 255) / 256))), 256, 0, st>>>(
         d.samples, d.wav, k.step, p->B, p->max_steps, n_steps, p->Q);

@@ -93,7 +93,8 @@ class WaveNetGen:
 
     @property
     def persistent(self):
-        """True when the plan runs each gen_run as one persistent launch (B <= 16)."""
+        """True when the plan runs each gen_run as one persistent launch (stream groups of <= 16,
+        B <= 80 on 256 CUs)."""
         return bool(self._plan is not None and self.lib.lbwn_gen_is_persistent(self._plan))
 
     def tensor(self, name, dtype=torch.float32):

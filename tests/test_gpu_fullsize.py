@@ -86,6 +86,10 @@ def torch_sum_xent(logits, q, ids):
     return (xent * mask).sum(), int(mask.sum())
 
 
+def _grad(p):
+    return p.grad.cpu().numpy() if p.grad is not None else np.zeros(tuple(p.shape))
+
+
 def _tensors(net, q, ids, mel, dev, grad):
     P0, S0 = oracle_params(net)
     P = {k: torch.tensor(v, device=dev, requires_grad=grad) for k, v in P0.items()}
@@ -110,12 +114,12 @@ def test_restatement_matches_oracle():
     tl, zs, Ss, ns, _ = torch_forward(arch, P, qt, it, S, mt)
     np.testing.assert_allclose(tl.detach().cpu().numpy(), lg, rtol=0, atol=1e-10)
     for k, v in new_save.items():
-        np.testing.assert_array_equal(ns[k].cpu().numpy(), v)
+        np.testing.assert_allclose(ns[k].cpu().numpy(), v, rtol=1e-12, atol=1e-12)
     sx, nv = torch_sum_xent(tl, qt, it)
     assert nv == st['n_valid']
     (sx / nv).backward()
-    for k, g in G.items():
-        close(P[k].grad.cpu().numpy(), g, 1e-10, k)
+    for k, g in G.items():   # (the last layer's RESIDUAL feeds nothing: no autograd edge, zero gradient)
+        close(_grad(P[k]), g, 1e-10, k)
 
 
 @pytest.mark.parametrize('arch_name,B', [('arch5', 32), ('arch3', 8)])
@@ -186,4 +190,4 @@ def test_full_size_forward_backward(arch_name, B):
     assert int(net.plan_tensor(T, 'status').view(torch.int32)[0]) == 0, 'chain hand-off timed out'
     scale = 1.0 / nv
     for name in net.layout.names():
-        close(net.grads[name].double().cpu().numpy() * scale, P[name].grad.cpu().numpy() * scale, 2e-4, name)
+        close(net.grads[name].double().cpu().numpy() * scale, _grad(P[name]) * scale, 2e-4, name)

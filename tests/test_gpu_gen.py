@@ -18,9 +18,9 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(params=['persistent', 'per_step'])
 def form(request, monkeypatch):
-    """Both execution forms at B <= 16: the persistent one-launch kernel (the default there)
-    and the per-step launches with vector GEMVs (LBWN_GEN_PERSIST=0).  B > 16 runs the per-step
-    GEMM form (test_gen_arch3_gemm_form)."""
+    """Both execution forms: the persistent one-launch kernel (the default while its blocks fit:
+    groups of <= 16 streams, B <= 80 on 256 CUs) and the per-step launches (LBWN_GEN_PERSIST=0:
+    vector GEMVs at B <= 16, the head as MFMA GEMMs beyond)."""
     if request.param == 'per_step':
         monkeypatch.setenv('LBWN_GEN_PERSIST', '0')
     else:
@@ -94,9 +94,11 @@ def test_gen_arch3_b10_graph_replay(form):
     assert int(g.tensor('status', torch.int32).item()) == 0
 
 
-def test_gen_rerun_and_large_batch():
+def test_gen_rerun_and_large_batch(form):
     """A second run on the same plan restarts the tags with the step counter (stale granules
-    from the first run must not be taken), and B = 40 > 16 runs the per-step GEMM form."""
+    from the first run must not be taken); B = 40 > 16 runs as three stream groups (14, 14, 12:
+    a ragged last group) of the persistent launch, or with LBWN_GEN_PERSIST=0 the per-step
+    GEMM form."""
     arch = small(gc=5)
     B, n = 40, 24
     g, P = make_gen(arch, B, chunk=8)
@@ -104,28 +106,32 @@ def test_gen_rerun_and_large_batch():
     g.run(n, gc_ids=gc)
     g.run(n, gc_ids=gc)
     torch.cuda.synchronize()
-    assert not g.persistent
+    assert g.persistent == (form == 'persistent')
+    assert int(g.tensor('status', torch.int32).item()) == 0
+    assert int(g.tensor('step', torch.int64).item()) == n
     s_ref, _ = R.generate(arch, P, B, n, seed=7, gc_ids=gc)
     np.testing.assert_array_equal(g.samples().cpu().numpy()[:, :n], s_ref)
     g2, P2 = make_gen(arch, 12, chunk=8)
     g2.run(n, gc_ids=gc[:12])
     g2.run(n, gc_ids=gc[:12])
     torch.cuda.synchronize()
-    assert g2.persistent
+    assert g2.persistent == (form == 'persistent')
     s2, _ = R.generate(arch, P2, 12, n, seed=7, gc_ids=gc[:12])
     np.testing.assert_array_equal(g2.samples().cpu().numpy()[:, :n], s2)
     assert int(g2.tensor('status', torch.int32).item()) == 0
 
 
-def test_gen_arch3_gemm_form():
-    """B = 64 (> 16): gen_wave per step, then skip / post1 / post2 as bf16-split MFMA GEMMs over
+def test_gen_arch3_gemm_form(form):
+    """B = 64 (> 16): four stream groups of 16 in one persistent launch (192 blocks), or with
+    LBWN_GEN_PERSIST=0 gen_wave per step, then skip / post1 / post2 as bf16-split MFMA GEMMs over
     the 64 streams (split-K, bias + relu epilogues) and the sampler; draws equal the oracle's."""
     arch = load_arch(os.path.join(ROOT, 'par', 'arch3.json'))
     B, n = 64, 60
     g, P = make_gen(arch, B, chunk=20)
     g.run(n)
     torch.cuda.synchronize()
-    assert not g.persistent
+    assert g.persistent == (form == 'persistent')
+    assert int(g.tensor('status', torch.int32).item()) == 0
     s_ref, _, lg_ref = R.generate(arch, P, B, n, seed=7, return_logits=True)
     got = g.samples().cpu().numpy()[:, :n]
     mism = int((got != s_ref).sum())

@@ -1,5 +1,5 @@
 """Wall-clock trace of one cached-generation step (LBWN_GEN_TRACE=1, set here), arch3, B
-streams.  Persistent form (default for B <= 16): the run's last step as seen by chain block 0
+streams.  Persistent form (default for B <= 80, groups of <= 16): the run's last step as seen by chain block 0
 and the last head block; per-step form (LBWN_GEN_PERSIST=0): per-layer cycles of stream 0's
 gen_wave and the GEMV stamps.  Usage: python tools/gen_trace.py [B]"""
 import os
