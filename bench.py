@@ -200,7 +200,7 @@ def gen_latency_floor(arch, clock_ghz=2.4):
             'handoffs': 3, 'handoff_us': 0.8, 'step_us': step_us, 'clock_ghz': clock_ghz}
 
 
-def bench_gen(net, arch, B=10, seconds=3.0, sr=16000, chunk=1000, sweep=(16, 64, 256)):
+def bench_gen(net, arch, B=10, seconds=3.0, sr=16000, chunk=1000, sweep=(16, 64, 80, 256)):
     """imodel.py cached generation, arch3, B=10, 3 s @ 16 kHz (BASELINE configs[2]), graph
     replay of chunk-sized step sequences; weights = the benchmark net's.  Also a B sweep and
     the step time against the latency floor of its dependent chain."""
