@@ -661,6 +661,10 @@ LBWN_DEV void dma4_sc1(const float* src, float* lds_dst) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 4, 0, 16);
 }
 
+#ifndef LBWN_GEN_RW_EARLY
+#define LBWN_GEN_RW_EARLY 0
+#endif
+
 LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* stepc, long long* trace) {
   float* RING = sm;                  // [G_NS][G_SLOT]
   float* XP = sm + G_NS * G_SLOT;    // [L][32] dilated taps of this step
@@ -837,6 +841,14 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* step
       const float z = gate_z(sg ? vp : v, sg ? v : vp);
       if (st6) { asm volatile("" ::"v"(z)); st6[2] = clock64(); }
       float* Zl = Z + (l & 1) * 32;
+#if LBWN_GEN_RW_EARLY
+      // residual weights (slot resident since the last barrier) issued before the z write: the
+      // barrier's lgkmcnt(0) retires them together with it, so only z is read after the barrier
+      floatx4 rw[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rw[q] = *(const floatx4*)(S + GI_W + ((rh * 4 + q) * 32 + rc) * 4);
+      const float bro = S[GI_WR + 64 + rc];
+#endif
       if (lead) {
         Zl[ch] = z;
         if (ch < Cd) put_granule(a.zg + ((long)b * L + l) * 32 + ch, (unsigned)(t + 1), z);
@@ -845,6 +857,11 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* step
       if (l == L - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lds_barrier();
       if (st6) st6[3] = clock64();
+#if LBWN_GEN_RW_EARLY
+      floatx4 zv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) zv[q] = *(const floatx4*)(Zl + 16 * rh + 4 * q);
+#else
       floatx4 zv[4], rw[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -852,6 +869,7 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* step
         rw[q] = *(const floatx4*)(S + GI_W + ((rh * 4 + q) * 32 + rc) * 4);
       }
       const float bro = S[GI_WR + 64 + rc];
+#endif
       float r0 = dot4(rw[0], zv[0], 0.f), r1 = dot4(rw[1], zv[1], 0.f);
       r0 = dot4(rw[2], zv[2], r0);
       r1 = dot4(rw[3], zv[3], r1);

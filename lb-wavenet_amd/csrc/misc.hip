@@ -234,6 +234,79 @@ __global__ __launch_bounds__(256) void head_kernel(lbwn_head_args a) {
   }
 }
 
+// The same head with the row held in registers (Q <= 64·QV): one coalesced load pass, exp once,
+// the gradient written from registers (the generic kernel above re-reads the row three times and
+// evaluates exp twice).  Lane c-order (c = lane + 64·j) and the first-max tie-break are kept, so
+// argmax (avg_diff) is identical; Σe is summed per lane, then across the wave.
+template <int QV>
+__global__ __launch_bounds__(256) void head_reg_kernel(lbwn_head_args a) {
+  __shared__ float part[4][3];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long M = (long)a.B * a.T;
+  const int Q = a.Q;
+  float s_xent = 0.f, s_valid = 0.f, s_diff = 0.f;
+  for (long m = (long)blockIdx.x * 4 + w; m < M; m += (long)gridDim.x * 4) {
+    float* row = a.logits + m * Q;
+    const int t = (int)(m % a.T);
+    if (t == a.T - 1) {  // logits_out[:, :-1] (tmodel.py:231): the last position has no target
+      if (a.write_grad)
+#pragma unroll
+        for (int j = 0; j < QV; ++j)
+          if (lane + 64 * j < Q) row[lane + 64 * j] = 0.f;
+      continue;
+    }
+    const int tgt = a.q[m + 1];
+    const bool valid = a.ids[m + 1] != 0;   // tmodel.py:232
+    float v[QV];
+#pragma unroll
+    for (int j = 0; j < QV; ++j) v[j] = (lane + 64 * j < Q) ? row[lane + 64 * j] : -INFINITY;
+    float mx = -INFINITY;
+    int am = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < QV; ++j)
+      if (v[j] > mx) { mx = v[j]; am = lane + 64 * j; }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float om = __shfl_xor(mx, o);
+      const int oa = __shfl_xor(am, o);
+      if (om > mx || (om == mx && oa < am)) { mx = om; am = oa; }
+    }
+    float e[QV], se = 0.f, pick = 0.f;
+#pragma unroll
+    for (int j = 0; j < QV; ++j) {
+      e[j] = (lane + 64 * j < Q) ? expf(v[j] - mx) : 0.f;
+      se += e[j];
+      if (lane + 64 * j == tgt) pick = v[j];
+    }
+    se = wave_sum(se);
+    pick = wave_sum(pick);   // the one lane holding the target's logit; the rest add 0
+    const float xent = (mx + logf(se)) - pick;
+    if (a.write_grad) {
+      const float inv = 1.f / se;
+#pragma unroll
+      for (int j = 0; j < QV; ++j) {
+        const int c = lane + 64 * j;
+        if (c < Q) row[c] = valid ? e[j] * inv - (c == tgt ? 1.f : 0.f) : 0.f;
+      }
+    }
+    if (lane == 0 && valid) {
+      s_xent += xent;
+      s_valid += 1.f;
+      s_diff += fabsf((float)(tgt - am));
+    }
+  }
+  if (lane == 0) {
+    part[w][0] = s_xent;
+    part[w][1] = s_valid;
+    part[w][2] = s_diff;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int k = threadIdx.x;
+    a.partial[blockIdx.x * 3 + k] = ((part[0][k] + part[1][k]) + part[2][k]) + part[3][k];
+  }
+}
+
 // stats[0] = Σxent, [1] = n_valid, [2] = Σ|diff|, [3] = 1/n_valid (0 if none)
 __global__ void stats_reduce_kernel(const float* partial, int nparts, float* stats) {
   __shared__ double sh[3][256];
@@ -484,7 +557,9 @@ int lbwn_shift_add_launch(float* out, const float* a, const float* c0, int gd, i
 int lbwn_head_launch(const lbwn_head_args& a, int* nblocks_out, hipStream_t st) {
   const long M = (long)a.B * a.T;
   const int nb = (int)std::min<long>((M + 3) / 4, 2048);
-  head_kernel<<<nb, 256, 0, st>>>(a);
+  if (a.Q <= 256) head_reg_kernel<4><<<nb, 256, 0, st>>>(a);
+  else if (a.Q <= 512) head_reg_kernel<8><<<nb, 256, 0, st>>>(a);
+  else head_kernel<<<nb, 256, 0, st>>>(a);
   LBWN_CHECK_LAUNCH();
   if (nblocks_out) *nblocks_out = nb;
   return 0;

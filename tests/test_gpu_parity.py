@@ -208,8 +208,11 @@ def test_layer_forward(lib, d, T, C):
 
 # ---- head --------------------------------------------------------------------------------
 
-def test_head_xent(lib):
-    B, T, Q = 3, 257, 256
+@pytest.mark.parametrize('Q', [256, 100, 512, 520])
+def test_head_xent(lib, Q):
+    """Softmax xent head: the register-resident kernel (Q <= 256, <= 512, ragged lanes) and the
+    generic one (Q > 512)."""
+    B, T = 3, 257
     rng = np.random.default_rng(5)
     lg = rng.normal(size=(B, T, Q)) * 3
     q, ids = rand_batch(dict(n_quant=Q), B, T, invalid=20)
@@ -226,6 +229,7 @@ def test_head_xent(lib):
     assert int(s[1]) == st['n_valid']
     np.testing.assert_allclose(s[0], st['sum_xent'], rtol=1e-5)
     assert int(s[2]) // (B * (T - 1)) == st['avg_diff']
+    assert int(s[2]) == st['sum_absdiff']
     np.testing.assert_allclose(lgd.cpu().numpy() / st['n_valid'], dlog, rtol=0, atol=1e-6)
 
 

@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-v2}
-TESTS=0 bash tools/gpu_cycle.sh $TAG || exit 1
+TESTS=${TESTS:-0} bash tools/gpu_cycle.sh $TAG || exit 1
 timeout -k 10 500 python bench.py > gpurun_out/bench_full_$TAG.json 2> gpurun_out/bench_full_$TAG.err || { tail -20 gpurun_out/bench_full_$TAG.err; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_gen_$TAG -o run -- python tools/gen_bench.py --batch 10 --steps 4000 > gpurun_out/prof_gen_$TAG.log 2>&1 || exit 1
 S=$(find gpurun_out/prof_gen_$TAG -name '*kernel_stats.csv' | head -1)
