@@ -55,6 +55,13 @@ LBWN_DEV void wave_sync() {
 // Two raw s_barriers per layer: B1 (x of layer l written; before it each loader retires layer
 // l's pieces, and the compute waves' reads of slot l-1 retired, so the loaders refill it after
 // B1) and B2 (z of layer l written).  No global loads on the compute chain.
+// LBWN_GEN_SPLITK (A/B switch): conv lane (c, sg, kq) takes inputs 8kq..8kq+7 of BOTH taps (pieces
+// m = 0, 1: x[t-d]; m = 2, 3: x[t]) instead of 16 of one tap, so the dilated half of the next
+// layer's conv runs beside the residual and only 8 current-tap FMAs (two chains of 4) remain
+// between the x write and the gate
+#ifndef LBWN_GEN_SPLITK
+#define LBWN_GEN_SPLITK 0
+#endif
 constexpr int GI_W = 16 * 256;              // conv: [w 4][m 4][lane 64][4]  W[16kq+4m+j][32sg+8w+c]
 constexpr int GI_R = 4 * 256;               // residual: [h 2][q 4][c 32][4] RES[16h+4q+j][c]
 constexpr int GI_WR = GI_W + GI_R;          // 20 pieces of 1 KiB
@@ -199,7 +206,11 @@ __global__ __launch_bounds__(512) void gen_wave_kernel(WaveK a) {
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       wv[m] = *(const floatx4*)(S + (w * 4 + m) * 256 + lane * 4);
+#if LBWN_GEN_SPLITK
+      xv[m] = *(const floatx4*)((m < 2 ? XP + l * 32 : XW) + 8 * kq + 4 * (m & 1));
+#else
       xv[m] = *(const floatx4*)(xin + 4 * m);
+#endif
     }
     const float bco = S[GI_WR + o] + S[GI_WR + 128 + o];
     __builtin_amdgcn_sched_barrier(0);
@@ -255,7 +266,12 @@ __global__ void gen_pack_kernel(const float* sig, const float* gate, const float
     if (e < GI_W) {
       const int w = e / 1024, m = (e / 256) % 4, ln = (e % 256) / 4, j = e % 4;
       const int c = ln >> 3, sg = (ln >> 2) & 1, kq = ln & 3;
-      const int k = 16 * kq + 4 * m + j, tap = k >> 5, in = k & 31, oc = 8 * w + c;
+#if LBWN_GEN_SPLITK
+      const int k = (m < 2 ? 0 : 32) + 8 * kq + 4 * (m & 1) + j;
+#else
+      const int k = 16 * kq + 4 * m + j;
+#endif
+      const int tap = k >> 5, in = k & 31, oc = 8 * w + c;
       if (in < Cr && oc < Cd) v = (sg ? gate : sig)[(long)l * 2 * Cr * Cd + (tap * Cr + in) * Cd + oc];
     } else if (e < GI_WR) {
       const int f = e - GI_W, j = f & 3, oc = (f >> 2) & 31, q = (f >> 7) & 3, h = f >> 9;
@@ -768,6 +784,13 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* step
 #pragma unroll
   for (int j = 0; j < 4; ++j) bq[j] = a.draw.bias ? a.draw.bias[min(c0 + j, Q - 1)] : 0.f;
   int code = a.code_in[b];   // step 0 of the run: the previous run's last draw (-1 at t = 0)
+  float accd = 0.f;          // LBWN_GEN_SPLITK: the dilated-tap partial of the next layer's conv
+  auto dilated = [&](const float* Sl, int l) {
+    const floatx4 w0 = *(const floatx4*)(Sl + (w * 4) * 256 + lane * 4);
+    const floatx4 w1 = *(const floatx4*)(Sl + (w * 4 + 1) * 256 + lane * 4);
+    const floatx4 x0 = *(const floatx4*)(XP + l * 32 + 8 * kq), x1 = *(const floatx4*)(XP + l * 32 + 8 * kq + 4);
+    return dot4(w1, x1, dot4(w0, x0, 0.f));
+  };
   int slot = 0;              // ring slot of global layer G = s·L + l (G mod G_NS, advanced per layer)
   for (int s = 0; s <= n; ++s) {
     const long long t = t0 + s;
@@ -805,9 +828,20 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* step
     long roff = 0;
     int bl = 0;
     lds_barrier();   // -1
+#if LBWN_GEN_SPLITK
+    accd = dilated(RING + slot * G_SLOT, 0);   // this step's taps and layer 0's slot landed by -1
+#endif
     for (int l = 0; l < L; ++l) {
       const float* S = RING + slot * G_SLOT;
       slot = (slot + 1 == G_NS) ? 0 : slot + 1;
+#if LBWN_GEN_SPLITK
+      floatx4 wv[2], xv[2];   // the current tap's pieces; the dilated half is in accd
+#pragma unroll
+      for (int mm = 0; mm < 2; ++mm) {
+        wv[mm] = *(const floatx4*)(S + (w * 4 + 2 + mm) * 256 + lane * 4);
+        xv[mm] = *(const floatx4*)(XW + 8 * kq + 4 * mm);
+      }
+#else
       const float* xin = (kq < 2 ? XP + l * 32 : XW) + xin_off;
       floatx4 wv[4], xv[4];
 #pragma unroll
@@ -815,6 +849,7 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* step
         wv[mm] = *(const floatx4*)(S + (w * 4 + mm) * 256 + lane * 4);
         xv[mm] = *(const floatx4*)(xin + 4 * mm);
       }
+#endif
       const float bco = S[GI_WR + o] + S[GI_WR + 128 + o];
       // (reading layer l+1's conv operands right after barrier l, and this layer's residual
       // weights ahead of the conv, measured 38.0 -> 38.9 us per step: rejected)
@@ -829,9 +864,13 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* step
       if (rh == 0 && (rc >> 3) == w && rc < Cr) a.rings[roff + ((long)b * d + (t & (d - 1))) * Cr + rc] = x;
       roff += (long)d * a.B * Cr;
       bl = (bl + 1 == a.nbl) ? 0 : bl + 1;
+#if LBWN_GEN_SPLITK
+      const float acc0 = dot4(wv[0], xv[0], accd), acc1 = dot4(wv[1], xv[1], 0.f);
+#else
       float acc0 = dot4(wv[0], xv[0], 0.f), acc1 = dot4(wv[1], xv[1], 0.f);
       acc0 = dot4(wv[2], xv[2], acc0);
       acc1 = dot4(wv[3], xv[3], acc1);
+#endif
       float v = acc0 + acc1;
       v += dpp<DPP_XOR1>(v);
       v += dpp<DPP_XOR2>(v);
@@ -857,6 +896,9 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* step
       if (l == L - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lds_barrier();
       if (st6) st6[3] = clock64();
+#if LBWN_GEN_SPLITK
+      accd = dilated(RING + slot * G_SLOT, min(l + 1, L - 1));   // layer l+1's slot landed by this barrier
+#endif
 #if LBWN_GEN_RW_EARLY
       floatx4 zv[4];
 #pragma unroll
