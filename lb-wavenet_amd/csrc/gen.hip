@@ -39,8 +39,8 @@ LBWN_DEV void wave_sync() {
 // ---- per-stream layer chain --------------------------------------------------------------
 // One workgroup of 8 waves per stream: waves 0-3 compute (one per SIMD), waves 4-7 move data.
 //   compute wave w owns channels 8w..8w+7 (lane group c = lane>>3 <-> channel 8w+c):
-//     conv      lane = (c, sg = sig|gate, kq = k-quarter): 16 FMAs over its quarter of
-//               [x[t-d] | x[t]] (4 weight + 4 broadcast input ds_read_b128), the quarters summed
+//     conv      lane = (c, sg = sig|gate, kq): 16 FMAs over inputs 8kq..8kq+7 of x[t-d] and of
+//               x[t] (4 weight + 4 broadcast input ds_read_b128), the four lanes' sums summed
 //               by two DPP quad permutes, the sig/gate partner fetched by row_half_mirror,
 //               z = tanh(sig)·σ(gate) on all 8 lanes of the group
 //     residual  lane = (c, kp = k-eighth): 4 FMAs over z[4kp..4kp+3], DPP-reduced over kp
@@ -55,14 +55,12 @@ LBWN_DEV void wave_sync() {
 // Two raw s_barriers per layer: B1 (x of layer l written; before it each loader retires layer
 // l's pieces, and the compute waves' reads of slot l-1 retired, so the loaders refill it after
 // B1) and B2 (z of layer l written).  No global loads on the compute chain.
-// LBWN_GEN_SPLITK (A/B switch): conv lane (c, sg, kq) takes inputs 8kq..8kq+7 of BOTH taps (pieces
-// m = 0, 1: x[t-d]; m = 2, 3: x[t]) instead of 16 of one tap, so the dilated half of the next
-// layer's conv runs beside the residual and only 8 current-tap FMAs (two chains of 4) remain
-// between the x write and the gate
-#ifndef LBWN_GEN_SPLITK
-#define LBWN_GEN_SPLITK 0
-#endif
-constexpr int GI_W = 16 * 256;              // conv: [w 4][m 4][lane 64][4]  W[16kq+4m+j][32sg+8w+c]
+// Conv lane (c, sg, kq) takes inputs 8kq..8kq+7 of BOTH taps (pieces m = 0, 1: x[t-d]; m = 2, 3:
+// x[t]), so the persistent chain computes the dilated half of the next layer's conv beside the
+// residual and only 8 current-tap FMAs (two chains of 4) remain between the x write and the gate
+// (with the residual weights read before the z write: 36.3 -> 35.0 us per step at B = 10, same box;
+// either change alone: 36.2 / 36.5)
+constexpr int GI_W = 16 * 256;              // conv: [w 4][m 4][lane 64][4]  W[32(m>>1)+8kq+4(m&1)+j][32sg+8w+c]
 constexpr int GI_R = 4 * 256;               // residual: [h 2][q 4][c 32][4] RES[16h+4q+j][c]
 constexpr int GI_WR = GI_W + GI_R;          // 20 pieces of 1 KiB
 constexpr int GIMG = GI_WR + 192;           // global image: + conv bias [64] + residual bias [64] + zeros [64]
@@ -194,23 +192,17 @@ __global__ __launch_bounds__(512) void gen_wave_kernel(WaveK a) {
   }
   if (lane < 32) XW[rc] = x;
   if (tr) a.trace[1] = clock64();
-  const int xin_off = kq < 2 ? 16 * kq : 16 * (kq - 2);
   long roff = 0;   // ring offset of layer l
   int bl = 0;      // l % nbl
   lds_barrier();   // barrier -1: taps and slot 0 landed, every wave's XW written
   if (tr) a.trace[2] = clock64();
   for (int l = 0; l < L; ++l) {
     const float* S = RING + (l % G_NS) * G_SLOT;
-    const float* xin = (kq < 2 ? XP + l * 32 : XW) + xin_off;
     floatx4 wv[4], xv[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       wv[m] = *(const floatx4*)(S + (w * 4 + m) * 256 + lane * 4);
-#if LBWN_GEN_SPLITK
       xv[m] = *(const floatx4*)((m < 2 ? XP + l * 32 : XW) + 8 * kq + 4 * (m & 1));
-#else
-      xv[m] = *(const floatx4*)(xin + 4 * m);
-#endif
     }
     const float bco = S[GI_WR + o] + S[GI_WR + 128 + o];
     __builtin_amdgcn_sched_barrier(0);
@@ -266,11 +258,7 @@ __global__ void gen_pack_kernel(const float* sig, const float* gate, const float
     if (e < GI_W) {
       const int w = e / 1024, m = (e / 256) % 4, ln = (e % 256) / 4, j = e % 4;
       const int c = ln >> 3, sg = (ln >> 2) & 1, kq = ln & 3;
-#if LBWN_GEN_SPLITK
       const int k = (m < 2 ? 0 : 32) + 8 * kq + 4 * (m & 1) + j;
-#else
-      const int k = 16 * kq + 4 * m + j;
-#endif
       const int tap = k >> 5, in = k & 31, oc = 8 * w + c;
       if (in < Cr && oc < Cd) v = (sg ? gate : sig)[(long)l * 2 * Cr * Cd + (tap * Cr + in) * Cd + oc];
     } else if (e < GI_WR) {
@@ -677,9 +665,6 @@ LBWN_DEV void dma4_sc1(const float* src, float* lds_dst) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 4, 0, 16);
 }
 
-#ifndef LBWN_GEN_RW_EARLY
-#define LBWN_GEN_RW_EARLY 0
-#endif
 
 LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* stepc, long long* trace) {
   float* RING = sm;                  // [G_NS][G_SLOT]
@@ -777,14 +762,13 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* step
   const int rc = lane & 31, rh = lane >> 5;
   float* XW = XP + (G_MAXL + 2) * 32 + 32 * w;
   float* Z = XP + (G_MAXL + 2) * 32 + 128;
-  const int xin_off = kq < 2 ? 16 * kq : 16 * (kq - 2);
   const int Q = a.Q, per = (Q + 63) >> 6, c0 = lane * per;
   long long* tr = (trace && b == 0 && threadIdx.x == 0) ? trace : nullptr;
   float bq[4];               // b2 of this lane's codes, loaded once (a global load in every draw before)
 #pragma unroll
   for (int j = 0; j < 4; ++j) bq[j] = a.draw.bias ? a.draw.bias[min(c0 + j, Q - 1)] : 0.f;
   int code = a.code_in[b];   // step 0 of the run: the previous run's last draw (-1 at t = 0)
-  float accd = 0.f;          // LBWN_GEN_SPLITK: the dilated-tap partial of the next layer's conv
+  float accd = 0.f;          // the dilated-tap partial of the next layer's conv
   auto dilated = [&](const float* Sl, int l) {
     const floatx4 w0 = *(const floatx4*)(Sl + (w * 4) * 256 + lane * 4);
     const floatx4 w1 = *(const floatx4*)(Sl + (w * 4 + 1) * 256 + lane * 4);
@@ -828,28 +812,16 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* step
     long roff = 0;
     int bl = 0;
     lds_barrier();   // -1
-#if LBWN_GEN_SPLITK
     accd = dilated(RING + slot * G_SLOT, 0);   // this step's taps and layer 0's slot landed by -1
-#endif
     for (int l = 0; l < L; ++l) {
       const float* S = RING + slot * G_SLOT;
       slot = (slot + 1 == G_NS) ? 0 : slot + 1;
-#if LBWN_GEN_SPLITK
       floatx4 wv[2], xv[2];   // the current tap's pieces; the dilated half is in accd
 #pragma unroll
       for (int mm = 0; mm < 2; ++mm) {
         wv[mm] = *(const floatx4*)(S + (w * 4 + 2 + mm) * 256 + lane * 4);
         xv[mm] = *(const floatx4*)(XW + 8 * kq + 4 * mm);
       }
-#else
-      const float* xin = (kq < 2 ? XP + l * 32 : XW) + xin_off;
-      floatx4 wv[4], xv[4];
-#pragma unroll
-      for (int mm = 0; mm < 4; ++mm) {
-        wv[mm] = *(const floatx4*)(S + (w * 4 + mm) * 256 + lane * 4);
-        xv[mm] = *(const floatx4*)(xin + 4 * mm);
-      }
-#endif
       const float bco = S[GI_WR + o] + S[GI_WR + 128 + o];
       // (reading layer l+1's conv operands right after barrier l, and this layer's residual
       // weights ahead of the conv, measured 38.0 -> 38.9 us per step: rejected)
@@ -864,13 +836,7 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* step
       if (rh == 0 && (rc >> 3) == w && rc < Cr) a.rings[roff + ((long)b * d + (t & (d - 1))) * Cr + rc] = x;
       roff += (long)d * a.B * Cr;
       bl = (bl + 1 == a.nbl) ? 0 : bl + 1;
-#if LBWN_GEN_SPLITK
       const float acc0 = dot4(wv[0], xv[0], accd), acc1 = dot4(wv[1], xv[1], 0.f);
-#else
-      float acc0 = dot4(wv[0], xv[0], 0.f), acc1 = dot4(wv[1], xv[1], 0.f);
-      acc0 = dot4(wv[2], xv[2], acc0);
-      acc1 = dot4(wv[3], xv[3], acc1);
-#endif
       float v = acc0 + acc1;
       v += dpp<DPP_XOR1>(v);
       v += dpp<DPP_XOR2>(v);
@@ -880,14 +846,12 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* step
       const float z = gate_z(sg ? vp : v, sg ? v : vp);
       if (st6) { asm volatile("" ::"v"(z)); st6[2] = clock64(); }
       float* Zl = Z + (l & 1) * 32;
-#if LBWN_GEN_RW_EARLY
       // residual weights (slot resident since the last barrier) issued before the z write: the
       // barrier's lgkmcnt(0) retires them together with it, so only z is read after the barrier
       floatx4 rw[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) rw[q] = *(const floatx4*)(S + GI_W + ((rh * 4 + q) * 32 + rc) * 4);
       const float bro = S[GI_WR + 64 + rc];
-#endif
       if (lead) {
         Zl[ch] = z;
         if (ch < Cd) put_granule(a.zg + ((long)b * L + l) * 32 + ch, (unsigned)(t + 1), z);
@@ -896,22 +860,10 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* step
       if (l == L - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lds_barrier();
       if (st6) st6[3] = clock64();
-#if LBWN_GEN_SPLITK
       accd = dilated(RING + slot * G_SLOT, min(l + 1, L - 1));   // layer l+1's slot landed by this barrier
-#endif
-#if LBWN_GEN_RW_EARLY
       floatx4 zv[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) zv[q] = *(const floatx4*)(Zl + 16 * rh + 4 * q);
-#else
-      floatx4 zv[4], rw[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        zv[q] = *(const floatx4*)(Zl + 16 * rh + 4 * q);
-        rw[q] = *(const floatx4*)(S + GI_W + ((rh * 4 + q) * 32 + rc) * 4);
-      }
-      const float bro = S[GI_WR + 64 + rc];
-#endif
       float r0 = dot4(rw[0], zv[0], 0.f), r1 = dot4(rw[1], zv[1], 0.f);
       r0 = dot4(rw[2], zv[2], r0);
       r1 = dot4(rw[3], zv[3], r1);
