@@ -823,8 +823,9 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* step
         xv[mm] = *(const floatx4*)(XW + 8 * kq + 4 * mm);
       }
       const float bco = S[GI_WR + o] + S[GI_WR + 128 + o];
-      // (reading layer l+1's conv operands right after barrier l, and this layer's residual
-      // weights ahead of the conv, measured 38.0 -> 38.9 us per step: rejected)
+      // (round 2: reading ALL of layer l+1's conv operands right after barrier l, and this layer's
+      // residual weights ahead of the conv, measured 38.0 -> 38.9 us per step; what is kept is
+      // the dilated half after the barrier and the residual weights just before the z write)
       // sub-layer cycle stamps (trace only): layers 16..23 of the traced step, 6 per layer
       // (compiled in only with -DLBWN_GEN_SUBSTAMPS=1: the lane-divergent stamp branches split the
       // layer into basic blocks the scheduler cannot overlap, 38.5 -> 44 us per step at B = 10)
