@@ -175,7 +175,8 @@ int lbwn_gemm_f32(const float* A, int64_t lda, int a_kcontig, const float* B, in
 
 /* The same product with B given ALSO as pre-split bf16 planes b3 (lbwn_split_planes of B with
  * rows = N: trans = 0 for B[n*ldb+k], 1 for B[k*ldb+n]), the form the training step uses for its
- * weight operands; no split-K.  B stays required for the f32 mode (mode 0 ignores b3). */
+ * weight operands; no split-K.  B stays required for the f32 mode (mode 0 ignores b3).
+ * b3 must be 16-byte aligned (else EINVAL) and hold lbwn_split_planes_elems_abi(N, K) elements. */
 int lbwn_gemm_f32_presplit(const float* A, int64_t lda, int a_kcontig, const uint16_t* b3, int N, const float* B,
                            int64_t ldb, int b_kcontig, float* C, int64_t ldc, int M, int K, const float* bias,
                            int relu_a, int relu_out, const float* mask, int64_t ldm, int accumulate, void* stream);

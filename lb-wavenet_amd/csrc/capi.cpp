@@ -62,6 +62,8 @@ int lbwn_gemm_f32_presplit(const float* A, int64_t lda, int a_kcontig, const uin
                            int64_t ldb, int b_kcontig, float* C, int64_t ldc, int M, int K, const float* bias,
                            int relu_a, int relu_out, const float* mask, int64_t ldm, int accumulate, void* stream) {
   LBWN_REQUIRE(b3 != nullptr, "gemm_f32_presplit: b3 is null");
+  // the x3r/x3q kernels read b3 with 16-byte loads over lbwn_split_planes_elems(N, K) elements
+  LBWN_REQUIRE(((uintptr_t)b3 & 15) == 0, "gemm_f32_presplit: b3 must be 16-byte aligned");
   lbwn_gemm_args g;
   memset(&g, 0, sizeof(g));
   g.A = A; g.lda = (long)lda; g.B = B; g.ldb = (long)ldb; g.C = C; g.ldc = (long)ldc;

@@ -52,6 +52,10 @@ struct lbwn_plan {
   int nblk;                      // layer-bwd blocks = slab partials per layer
   bool chain = false;            // persistent layer-chain kernels (n_res = n_dil = 32)
   int chain_grid = 0;            // resident blocks for the chain (set on first use)
+  int fwd_grid = 0;              // ... for the forward chain (its tile: lbwn_chain_fwd_tile(fwd_nw))
+  // forward chain form (LBWN_CHAIN_TILE at plan creation): 0 = 32-position waves on 128-position
+  // tiles (chain_fwd_kernel), 8 / 4 = 16-position waves on 128- / 64-position tiles
+  int fwd_nw = 0;
   // Backward side stream (chain plans): the head weight gradients (dPOST2, dPOST1) run on the
   // main stream before the chain; dSKIP follows the chain on the main stream while `aux2` runs
   // the HBM-bound slab reduction and dPRE scatter beside it.  A chain block takes a whole CU's
@@ -350,7 +354,15 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->oCPART = carve(cur, sizeof(float) * (size_t)lbwn_colpart_parts(M) * (p->Cp + p->Cs));
   // [status (16 B) | forward hand-off flags | backward hand-off flags], zeroed by ONE memset per
   // step (each flag block padded to 16 B)
-  p->nflag_bytes = (sizeof(unsigned) * (size_t)B * ((T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS) + 15) / 16 * 16;
+  {
+    const char* tv = getenv("LBWN_CHAIN_TILE");
+    if (tv && !strcmp(tv, "64")) p->fwd_nw = 4;
+    else if (tv && !strcmp(tv, "128")) p->fwd_nw = 8;
+    else if (tv && !strcmp(tv, "w32")) p->fwd_nw = 0;
+    else LBWN_REQUIRE(!tv || !tv[0], "LBWN_CHAIN_TILE must be 64, 128 or w32 (got '%s')", tv);
+  }
+  // one flag per tile of the finest chain tile (64 positions), so any form fits
+  p->nflag_bytes = (sizeof(unsigned) * (size_t)B * ((T + 63) / 64) + 15) / 16 * 16;
   p->oSTATUS = carve(cur, 16 + 2 * p->nflag_bytes);
   p->oFLAGS = p->oSTATUS + 16;
   {
@@ -393,7 +405,8 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     const W3Shape w = w3_shape(p, i);
     if (w.K % 32 == 0) p->oW3[i] = carve(cur, 2 * lbwn_split_planes_elems(w.rows, w.K));
   }
-  if (p->chain && p->Lo > 0 && lbwn_lc_in_chain_ok(p->Lo)) p->oLCX = carve(cur, 2 * (size_t)L * lbwn_lc_image_x3_elems());
+  if (p->chain && p->Lo > 0 && lbwn_lc_in_chain_ok(p->Lo))
+    p->oLCX = carve(cur, 2 * (size_t)L * std::max(lbwn_lc_image_x3_elems(), lbwn_lc_image16_elems()));
   p->oHEADP = carve(cur, sizeof(float) * 3 * 2048);
   p->oBSUM = carve(cur, sizeof(float) * (size_t)p->Cs);
   p->oWPK = carve(cur, sizeof(float) * (size_t)L * lbwn_layer_image_floats());
@@ -456,6 +469,8 @@ int ensure_device(lbwn_plan* p) {
   LBWN_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
   const int ntiles = p->B * ((p->T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS);
   p->chain_grid = std::max(1, std::min(ntiles, ncu));
+  const int tpf = lbwn_chain_fwd_tile(p->fwd_nw);
+  p->fwd_grid = std::max(1, std::min(p->B * ((p->T + tpf - 1) / tpf), ncu));
   if (p->overlap) {
     int least = 0, greatest = 0;
     LBWN_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -720,7 +735,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
       (e = lbwn_pack_layers_fb_x3_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b,
                                          at<unsigned short>(ws, p->oWPKX), at<float>(ws, p->oWPKB), L, Cr, Cd,
                                          P->skip_b, p->Cs, bsum, P->lc_sig, P->lc_gate, p->Lo,
-                                         lcx ? at<unsigned short>(ws, p->oLCX) : nullptr, pst)))
+                                         lcx ? at<unsigned short>(ws, p->oLCX) : nullptr, pst, p->fwd_nw != 0)))
     return e;
   const bool bsum_done = x3 && p->chain && P->skip_b;   // summed by the pack launch above
   if (x3) {
@@ -760,6 +775,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     c.flags_zeroed = 1;   // zeroed with the status word at the step start
     if (p->ctrace_blk >= 0) { c.trace = at<long long>(ws, p->oCTRACE); c.trace_blk = p->ctrace_blk; }
     c.B = B; c.T = T; c.H = H; c.L = L; c.nbl = p->nbl; c.Cr = Cr; c.Cd = Cd; c.grid = p->chain_grid;
+    if (c.SG && p->fwd_nw) { c.fwd_nw = p->fwd_nw; c.grid = p->fwd_grid; }
     Probe(p, st, "layer_fwd");
     if ((e = lbwn_chain_fwd_launch(c, st))) return e;
     Probe::end(p, st, "layer_fwd");

@@ -85,8 +85,13 @@ int lbwn_layer_image_x3_elems();
 int lbwn_pack_layers_fb_x3_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                                   const float* res, const float* res_b, unsigned short* fout, float* bout, int L,
                                   int Cr, int Cd, const float* skip_b, int Cs, float* bsum, const float* lc_sig,
-                                  const float* lc_gate, int Lo, unsigned short* lcout, hipStream_t st);
+                                  const float* lc_gate, int Lo, unsigned short* lcout, hipStream_t st,
+                                  int lc16 = 0);
 int lbwn_lc_image_x3_elems();
+int lbwn_lc_image16_elems();       // the 16-lane forward chain's LC image (lc16 = 1 above)
+// forward chain form: 0 = 32-position waves (chain_fwd_kernel, 128-position tiles), 4 / 8 =
+// 16-position waves (chain_fwd16_kernel) with 4 / 8 waves = 64- / 128-position tiles
+int lbwn_chain_fwd_tile(int fwd_nw);
 int lbwn_lc_in_chain_ok(int Lo);   // n_lc_out the forward chain's in-chain LC term supports
 int lbwn_pack_layers_x3_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                                const float* res, const float* res_b, unsigned short* out, int L, int Cr, int Cd,
@@ -133,6 +138,7 @@ struct lbwn_chain_args {
   int* tile_gid = nullptr;     // x3 backward + GC: [ntiles] uniform voice id per tile or -1
   // forward, bf16-split form: in-chain LC term (instead of cond): LC input [M][Lo], split images
   const float* lcact = nullptr; const unsigned short* lcimg = nullptr; int Lo = 0;
+  int fwd_nw = 0;              // forward form (lbwn_chain_fwd_tile); lcimg in the matching layout
 };
 int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st);
 int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st);

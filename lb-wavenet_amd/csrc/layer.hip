@@ -878,6 +878,385 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
   }
 }
 
+// ---- forward chain, 16-position waves (round 4) ---------------------------------------------
+// chain_fwd16_kernel<NW, LC, CM, TR>: the X3 forward chain on v_mfma_f32_16x16x32_bf16 with 16
+// positions per wave and NW waves per block: tile TP = 16·NW positions (the C4 tile axis:
+// NW = 8 → 128 positions with TWO waves per SIMD, NW = 4 → 64 positions).  The per-layer protocol
+// (halo hand-off, own tap of the next layer inside the store drain, double-buffered images, the
+// LC image two layers ahead) is chain_fwd_kernel's; what changes is the MFMA geometry:
+//   lane = (j = lane & 15: the wave's position, g = lane >> 4), and with q0 = 2(g >> 1), h = g & 1
+//   the lane's accumulator block b (0, 1) register r holds channel 8(q0 + b) + 4h + r — the same
+//   (q, h) channel groups chain_fwd_kernel's lanes hold, so z / σ go to the same rows / sg_off
+//   blocks and the residual's B operand (the lane's 8 z values) is in the split image's RT k order
+//   unchanged.  For that, conv A row i of block b reads out channel ch16(b, i) (the permutation
+//   that puts D row i = 4g + r on that channel).  The residual's rows are unpermuted: x_{l+1}
+//   block rb register r = channel 16rb + 4g + r.
+// Per wave and layer: conv 2 taps × (sig, gate) × 2 blocks × 6 products = 48 MFMAs of 16 cycles,
+// residual 2 blocks × 6 = 12 — per position the MFMA work of chain_fwd_kernel, in half the
+// positions per wave, so two waves share each SIMD at NW = 8 and hide each other's latencies.
+LBWN_DEV int ch16(int b, int i) { return 16 * (i >> 3) + 8 * b + 4 * ((i >> 2) & 1) + (i & 3); }
+
+// acc += A·B over one 32-deep k-step from split fragments (six products, small terms first)
+LBWN_DEV floatx4 mfma16x3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], floatx4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+  return acc;
+}
+
+// LC image of the 16-lane form: LCT16[o (sig 0..31 | gate 32..63)][plane][k 0..95] (k >= n_lc_out
+// zero: three whole 32-deep k-steps), rows of LC16_ROW = 3·96 + 8 bf16 (148 dwords: 4·odd).
+constexpr int LC16_KP = 96, LC16_ROW = 3 * LC16_KP + 8;
+constexpr int LC16IMG_US = 64 * LC16_ROW;                      // bf16 elements per layer image
+constexpr int LC16IMG_F = LC16IMG_US / 2;                      // = 9472 floats = 37 KiB
+static_assert(LC16IMG_F % 256 == 0, "LC16 image: whole 1-KiB DMA pieces");
+
+LBWN_DEV void pack_lc16_body(int l, const float* lsig, const float* lgate, unsigned short* out, int Lo, int Cd) {
+  unsigned short* img = out + (long)l * LC16IMG_US;
+  for (int e = threadIdx.x; e < 64 * (LC16_ROW / 2); e += blockDim.x) {
+    const int o = e / (LC16_ROW / 2), kk = 2 * (e % (LC16_ROW / 2));
+    unsigned short* row = img + o * LC16_ROW;
+    if (kk >= LC16_KP) {   // row pad (zero); plane slots are written below
+      if (kk >= 3 * LC16_KP) *(unsigned*)(row + kk) = 0u;
+      continue;
+    }
+    const float* w = (o < 32 ? lsig : lgate) + (long)l * Lo * Cd;
+    const int oc = o & 31;
+    floatx2 x = {0.f, 0.f};
+    if (oc < Cd) {
+      if (kk < Lo) x[0] = w[(long)kk * Cd + oc];
+      if (kk + 1 < Lo) x[1] = w[(long)(kk + 1) * Cd + oc];
+    }
+    unsigned hi, mi, lo;
+    split2(x, hi, mi, lo);
+    *(unsigned*)(row + kk) = hi;
+    *(unsigned*)(row + LC16_KP + kk) = mi;
+    *(unsigned*)(row + 2 * LC16_KP + kk) = lo;
+  }
+}
+
+template <int NW>
+LBWN_DEV void dma_lc16_image(const unsigned short* lcimg, int l, float* LCI, int w, int lane) {
+  const float* src = (const float*)lcimg + (long)l * LC16IMG_F + lane * 4;
+  constexpr int NP = LC16IMG_F / 256;
+#pragma unroll
+  for (int i = 0; i < (NP + NW - 1) / NW; ++i) {
+    const int pc = w + NW * i;
+    if (pc < NP) dma16(src + pc * 256, LCI + pc * 256);
+  }
+}
+
+// GC / COND term of layer l for this lane's channels: cv[2·kind + b] = channels 8(q0+b)+4h..+3
+// (kind 0 sig, 1 gate); CM as load_cond
+template <int CM>
+LBWN_DEV void load_cond16(const ChainFK& a, int l, int myid, long m, bool valid, int q0, int h, floatx4 (&cv)[4]) {
+  if (CM == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cv[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    return;
+  }
+  if (CM == 1) {
+    const float* g = a.gc_tab + (long)myid * a.gc_ld + (long)l * 64;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cv[i] = *(const floatx4*)(g + 32 * (i >> 1) + 8 * (q0 + (i & 1)) + 4 * h);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) cv[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (!valid) return;
+  if (a.gc_tab) {
+    const float* g = a.gc_tab + (long)myid * a.gc_ld + (long)l * 64;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cv[i] += *(const floatx4*)(g + 32 * (i >> 1) + 8 * (q0 + (i & 1)) + 4 * h);
+  }
+  if (a.cond) {
+    const float* c = a.cond + m * a.ldcond + (long)l * 64;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cv[i] += *(const floatx4*)(c + 32 * (i >> 1) + 8 * (q0 + (i & 1)) + 4 * h);
+  }
+}
+
+// acc[2·kind + b] = bias + conditioning
+LBWN_DEV void conv16_init(const float* bs, const floatx4 (&cv)[4], int q0, int h, floatx4 (&acc)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const floatx4 bv = *(const floatx4*)(bs + 32 * (i >> 1) + 8 * (q0 + (i & 1)) + 4 * h);
+    acc[i] = bv + cv[i];
+  }
+}
+
+// acc += Wtapᵀ·x for one tap: Wt = the split image's WT at this tap (rows XW_ROW), xrow = this
+// lane's position row in LDS (channels 8g..8g+7 = the B operand's k group); the operands of each
+// of the NP parts (4 / NP accumulator blocks) are read before its MFMAs (NP = 2 halves the live
+// fragments for the register-tight LC form)
+template <int NP = 1>
+LBWN_DEV void conv16_tap(const float* xrow, const unsigned short* Wt, int i16, int g, floatx4 (&acc)[4]) {
+  const floatx4 x0 = *(const floatx4*)(xrow + 8 * g), x1 = *(const floatx4*)(xrow + 8 * g + 4);
+  bf16x8 xb[3];
+#pragma unroll
+  for (int part = 0; part < NP; ++part) {
+    constexpr int NB = 4 / NP;
+    bf16x8 wf[NB][3];
+#pragma unroll
+    for (int ii = 0; ii < NB; ++ii) {
+      const int i = part * NB + ii, o = 32 * (i >> 1) + ch16(i & 1, i16);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) wf[ii][p] = *(const bf16x8*)(Wt + o * XW_ROW + 32 * p + 8 * g);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (part == 0) split8(x0, x1, xb);
+#pragma unroll
+    for (int ii = 0; ii < NB; ++ii) acc[part * NB + ii] = mfma16x3(wf[ii], xb, acc[part * NB + ii]);
+  }
+}
+
+// lc·[LC_SIGNAL_l | LC_GATE_l] onto the accumulators: A = LC16 image rows, B = the lane's LC input
+// row (k = 32s + 8g + j), held as raw f32 (lcv: 24 registers instead of 36 pre-split: at two
+// waves per SIMD the split form spilled) and split per k-step
+LBWN_DEV void lc16_terms(const unsigned short* LI, const floatx4 (&lcv)[6], int i16, int g, floatx4 (&acc)[4]) {
+#pragma unroll
+  for (int s2 = 0; s2 < 3; ++s2) {
+    bf16x8 xb[3];
+    split8(lcv[2 * s2], lcv[2 * s2 + 1], xb);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int o = 32 * (i >> 1) + ch16(i & 1, i16);
+      bf16x8 wf[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) wf[p] = *(const bf16x8*)(LI + o * LC16_ROW + LC16_KP * p + 32 * s2 + 8 * g);
+      acc[i] = mfma16x3(wf, xb, acc[i]);
+    }
+  }
+}
+
+template <int NW>
+constexpr int cf16_lds(bool lc) { return 3 * 16 * NW * XS + 2 * XIMG_F + (lc ? LC16IMG_F : 0); }
+static_assert(cf16_lds<8>(true) * 4 + 16 <= 160 * 1024, "chain fwd16 + LC LDS");
+
+template <int NW, bool LC, int CM, bool TR>
+__global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
+  constexpr int TP = 16 * NW, NT = 64 * NW;
+  constexpr int IMGF = XIMG_F;
+  constexpr int PF = (IMGF / 4 + NT - 1) / NT;          // float4 per thread to prefetch one image
+  constexpr int NR = TP * 8 / NT;                       // float4 per thread of a TP-row tile (2)
+  __shared__ __attribute__((aligned(16))) float sm[cf16_lds<NW>(LC)];
+  __shared__ int s_fail;
+  float* HALO = sm + 2 * TP * XS;
+  float* IMG0 = HALO + TP * XS;
+  auto img = [&](int l) { return IMG0 + (l & 1) * IMGF; };
+  float* LCI = IMG0 + 2 * IMGF;
+  const unsigned short* LCIu = (const unsigned short*)LCI;
+  const float* wsrc = (const float*)a.ximg;
+  auto bias_of = [&](const float* im) { return im + XB_OFF / 2; };
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i16 = lane & 15, g = lane >> 4, q0 = 2 * (g >> 1), h = g & 1;
+  const int r = 16 * w + i16;  // this lane's row of the tile
+  const int tps = (a.T + TP - 1) / TP, ntiles = a.B * tps;
+  if (tid == 0) s_fail = 0;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int b = tile / tps, tt = tile % tps, t0 = tt * TP;
+    const int t = t0 + r;
+    const bool valid = t < a.T;
+    const long m = (long)b * a.T + t;
+    const long sb = (long)b * (a.H + a.T) * 32;
+    constexpr bool has_cond = CM != 0;
+    const int myid = (a.gc_tab && valid) ? a.ids[m] : 0;
+    floatx4 cv[4];
+    load_cond16<CM>(a, 0, myid, m, valid && has_cond, q0, h, cv);
+    floatx4 lcv[6];   // LC: this lane's LC input row, k = 32s + 8g + 0..7 (zero past n_lc_out)
+    if (LC) {
+      const float* lrow = a.lcact + ((long)b * a.T + min(t, a.T - 1)) * a.Lo;
+#pragma unroll
+      for (int s2 = 0; s2 < 3; ++s2) {
+        const int k0 = 32 * s2 + 8 * g;
+        lcv[2 * s2] = *(const floatx4*)(lrow + min(k0, a.Lo - 4));       // clamped, then select
+        lcv[2 * s2 + 1] = *(const floatx4*)(lrow + min(k0 + 4, a.Lo - 4));
+        if (k0 >= a.Lo) lcv[2 * s2] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (k0 + 4 >= a.Lo) lcv[2 * s2 + 1] = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    __syncthreads();  // previous tile's LDS use done
+    if (LC) dma_lc16_image<NW>(a.lcimg, 0, LCI, w, lane);
+    {  // images of layers 0 and 1, every load before the first store
+      constexpr int NI = (2 * IMGF / 4 + NT - 1) / NT;
+      const int nimg4 = min(a.L, 2) * IMGF / 4;
+      floatx4 iv[NI];
+#pragma unroll
+      for (int i = 0; i < NI; ++i) iv[i] = *(const floatx4*)(wsrc + 4 * min(tid + NT * i, nimg4 - 1));
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int e = tid + NT * i;
+        if (e < nimg4) *(floatx4*)(img(0) + 4 * e) = iv[i];
+      }
+    }
+    {  // x_0 rows (embed output, pre-launch): unconditional clamped loads, then select
+      const float* xb = a.X + sb;
+      floatx4 v[NR];
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        const int e = tid + NT * i, rr = e >> 3, c4 = (e & 7) * 4;
+        v[i] = *(const floatx4*)(xb + (long)(a.H + min(t0 + rr, a.T - 1)) * 32 + c4);
+        if (t0 + rr >= a.T) v[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        const int e = tid + NT * i;
+        *(floatx4*)(sm + (e >> 3) * XS + (e & 7) * 4) = v[i];
+      }
+    }
+    if (LC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the LC image DMA
+    __syncthreads();
+    // layer 0's own tap W1·x_0[t] (+ its LC term)
+    floatx4 acc[4];
+    conv16_init(bias_of(img(0)), cv, q0, h, acc);
+    if (has_cond && a.L > 1) load_cond16<CM>(a, 1, myid, m, valid, q0, h, cv);
+    conv16_tap<LC ? 2 : 1>(sm + r * XS, (const unsigned short*)img(0) + 96, i16, g, acc);
+    if (LC) {
+      lc16_terms(LCIu, lcv, i16, g, acc);
+      if (a.L > 1) {
+        __syncthreads();   // every wave is past its LC_0 reads
+        dma_lc16_image<NW>(a.lcimg, 1, LCI, w, lane);   // lands with layer 0's halo loads
+      }
+    }
+    const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && tile == (int)blockIdx.x;
+#define FSTAMP(i) if (TR && trc) a.trace[16 * l + (i)] = clock64()
+    for (int l = 0; l < a.L; ++l) {
+      FSTAMP(0);
+      const int d = 1 << (l % a.nbl);
+      float* cur = sm + (l & 1) * TP * XS;
+      float* nxt = sm + ((l + 1) & 1) * TP * XS;
+      float* xl = a.X + (long)l * a.xls + sb;
+      const float* Wl = img(l);
+      const float* br = bias_of(Wl) + 64;
+      floatx4 pf[PF];
+      FSTAMP(1);
+      // wait for the producer of the halo rows
+      const int ptt = tt - max(1, d / TP);
+      if (l > 0 && ptt >= 0) {
+        if (tid == 0 && !s_fail) {
+          if (!wait_flag_ge(a.flags + (long)b * tps + ptt, (unsigned)l, a.status, 1u)) s_fail = 1;
+        }
+        __syncthreads();
+      }
+      FSTAMP(2);
+      {  // halo rows [0, min(d,TP)): sc1 loads (clamped rows), then the image of layer l+2 behind them
+        const int nh = min(d, TP);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(xl, (short)0, (int)((long)(a.H + a.T) * 32 * 4), BUF_DW3);
+        floatx4 hv[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int e = min(tid + NT * i, nh * 8 - 1), row = e >> 3, c4 = (e & 7) * 4;
+          hv[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((a.H + t0 + row - d) * 32 + c4) * 4, 0, 16);
+        }
+        {
+          const floatx4* src = (const floatx4*)(wsrc + (long)min(l + 2, a.L - 1) * IMGF);
+#pragma unroll
+          for (int i = 0; i < PF; ++i) pf[i] = src[min(tid + NT * i, IMGF / 4 - 1)];
+        }
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int e = tid + NT * i;
+          *(floatx4*)(HALO + (e >> 3) * XS + (e & 7) * 4) = hv[i];
+        }
+      }
+      __syncthreads();
+      FSTAMP(3);
+      // residual weights (RT rows 16rb + i16, k group g) read now
+      bf16x8 rf[2][3];
+      {
+        const unsigned short* rt = (const unsigned short*)Wl + 64 * XW_ROW + i16 * XR_ROW + 8 * g;
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) rf[rb][p] = *(const bf16x8*)(rt + 16 * rb * XR_ROW + 32 * p);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // dilated tap W0·x[t-d], gate
+      const float* xp = (r >= d) ? cur + (r - d) * XS : HALO + r * XS;
+      conv16_tap<LC ? 2 : 1>(xp, (const unsigned short*)Wl, i16, g, acc);
+      floatx4 z[2], sg[2];
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float sq;
+          z[bb][j] = gate_zs(acc[bb][j], acc[2 + bb][j], sq);
+          sg[bb][j] = sq;
+        }
+      FSTAMP(4);
+      if (l + 1 < a.L) {
+        // residual: x_{l+1} = x_l + br + RES·z → LDS (next layer's rows) and HBM (sc1 for halo rows)
+        floatx4 accr[2];
+        const float* xc = cur + r * XS;
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+          accr[rb] = *(const floatx4*)(xc + 16 * rb + 4 * g) + *(const floatx4*)(br + 16 * rb + 4 * g);
+        {
+          bf16x8 zb[3];
+          split8(z[0], z[1], zb);   // k = 8g + j: block 0 regs, then block 1 regs (RT's k order)
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) accr[rb] = mfma16x3(rf[rb], zb, accr[rb]);
+        }
+        float* xn = a.X + (long)(l + 1) * a.xls + sb;
+        const __amdgpu_buffer_rsrc_t rn =
+            __builtin_amdgcn_make_buffer_rsrc(xn, (short)0, (int)((long)(a.H + a.T) * 32 * 4), BUF_DW3);
+        float* nrow = nxt + r * XS;
+        const bool halo_row = r >= TP - min(1 << ((l + 1) % a.nbl), TP);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          *(floatx4*)(nrow + 16 * rb + 4 * g) = accr[rb];
+          const int off = ((a.H + t) * 32 + 16 * rb + 4 * g) * 4;
+          if (valid && halo_row) __builtin_amdgcn_raw_buffer_store_b128(accr[rb], rn, off, 0, 16);
+          if (valid && !halo_row) __builtin_amdgcn_raw_buffer_store_b128(accr[rb], rn, off, 0, 0);
+        }
+        FSTAMP(8);
+        // the next layer's own tap from the row this wave's lanes just wrote (wave-local)
+        wave_lds_fence();
+        const float* Wn = img(l + 1);
+        conv16_init(bias_of(Wn), cv, q0, h, acc);
+        if (has_cond && l + 2 < a.L) load_cond16<CM>(a, l + 2, myid, m, valid, q0, h, cv);
+        conv16_tap<LC ? 2 : 1>(nrow, (const unsigned short*)Wn + 96, i16, g, acc);
+        if (LC) lc16_terms(LCIu, lcv, i16, g, acc);
+      }
+      FSTAMP(5);
+      // publish x_{l+1}: every wave drains its stores, barrier, one lane signals
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      FSTAMP(9);
+      __syncthreads();
+      FSTAMP(10);
+      if (tid == 0 && l + 1 < a.L) publish_flag(a.flags + tile, (unsigned)(l + 1));
+      if (LC && l + 2 < a.L) dma_lc16_image<NW>(a.lcimg, l + 2, LCI, w, lane);
+      if (l + 2 < a.L) {
+        float* dst = IMG0 + (l & 1) * IMGF;
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+          const int e = tid + NT * i;
+          if (e < IMGF / 4) *(floatx4*)(dst + 4 * e) = pf[i];
+        }
+      }
+      FSTAMP(6);
+      // z (skip GEMM input) and σ rows (sg_off blocks for chain_bwd_x3_kernel), issued last
+      if (valid) {
+        float* zr = a.Z + m * a.ldz + (long)l * a.Cd;
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) *(floatx4*)(zr + 8 * (q0 + bb) + 4 * h) = z[bb];
+        if (a.SG) {
+          float* sgl = a.SG + (long)l * a.sgls;
+#pragma unroll
+          for (int bb = 0; bb < 2; ++bb) *(floatx4*)(sgl + sg_off(m, q0 + bb, h)) = sg[bb];
+        }
+      }
+      FSTAMP(7);
+    }
+#undef FSTAMP
+  }
+}
+
 // ---- deferred slab reduction -------------------------------------------------------------
 
 // Destination of slab column c (padded 32-channel layout) in reference layout.
@@ -1415,7 +1794,8 @@ __global__ void pack_layers_bx3_kernel(const float* sig, const float* gate, cons
 __global__ void pack_layers_fb_x3_kernel(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                                          const float* res, const float* res_b, unsigned short* fout, float* bout,
                                          int L, int Cr, int Cd, const float* skip_b, int Cs, float* bsum,
-                                         const float* lc_sig, const float* lc_gate, int Lo, unsigned short* lcout) {
+                                         const float* lc_sig, const float* lc_gate, int Lo, unsigned short* lcout,
+                                         int lc16) {
   const int l = blockIdx.x;
   const int nlc = lcout ? L : 0;
   if (l < L) {
@@ -1423,7 +1803,8 @@ __global__ void pack_layers_fb_x3_kernel(const float* sig, const float* gate, co
   } else if (l < 2 * L) {
     pack_bx3_body(l - L, sig, gate, res, bout, Cr, Cd);
   } else if (l < 2 * L + nlc) {
-    pack_lc_x3_body(l - 2 * L, lc_sig, lc_gate, lcout, Lo, Cd);
+    if (lc16) pack_lc16_body(l - 2 * L, lc_sig, lc_gate, lcout, Lo, Cd);
+    else pack_lc_x3_body(l - 2 * L, lc_sig, lc_gate, lcout, Lo, Cd);
   } else {
     const int n = (l - 2 * L - nlc) * blockDim.x + threadIdx.x;
     if (n < Cs) {
@@ -2147,6 +2528,8 @@ int lbwn_layer_dx_combine_launch(const float* out_a, const float* out_c0, float*
 }
 int lbwn_layer_image_x3_elems() { return XIMG_US; }
 int lbwn_lc_image_x3_elems() { return LCIMG_US; }
+int lbwn_lc_image16_elems() { return LC16IMG_US; }
+int lbwn_chain_fwd_tile(int fwd_nw) { return fwd_nw ? 16 * fwd_nw : LP; }
 int lbwn_lc_in_chain_ok(int Lo) { return Lo > 16 * (LC_K - 1) && Lo <= LC_KP && Lo % 4 == 0; }
 int lbwn_layer_image_bx3_floats() { return BIMG_F; }
 int lbwn_pack_layers_bx3_launch(const float* sig, const float* gate, const float* res, float* out, int L, int Cr,
@@ -2160,7 +2543,7 @@ int lbwn_pack_layers_bx3_launch(const float* sig, const float* gate, const float
 int lbwn_pack_layers_fb_x3_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                                   const float* res, const float* res_b, unsigned short* fout, float* bout, int L,
                                   int Cr, int Cd, const float* skip_b, int Cs, float* bsum, const float* lc_sig,
-                                  const float* lc_gate, int Lo, unsigned short* lcout, hipStream_t st) {
+                                  const float* lc_gate, int Lo, unsigned short* lcout, hipStream_t st, int lc16) {
   LBWN_REQUIRE(Cr <= 32 && Cd <= 32 && (((uintptr_t)fout) & 15) == 0 && (((uintptr_t)bout) & 15) == 0,
                "pack_layers_fb_x3: bad arguments");
   LBWN_REQUIRE(!lcout || (lc_sig && lc_gate && Lo >= 1 && Lo <= LC_KP && (((uintptr_t)lcout) & 15) == 0),
@@ -2168,7 +2551,8 @@ int lbwn_pack_layers_fb_x3_launch(const float* sig, const float* gate, const flo
   const int nsum = (skip_b && bsum) ? (Cs + 255) / 256 : 0;
   const int nlc = lcout ? L : 0;
   pack_layers_fb_x3_kernel<<<2 * L + nlc + nsum, 256, 0, st>>>(sig, gate, sig_b, gate_b, res, res_b, fout, bout, L, Cr,
-                                                               Cd, skip_b, Cs, bsum, lc_sig, lc_gate, Lo, lcout);
+                                                               Cd, skip_b, Cs, bsum, lc_sig, lc_gate, Lo, lcout,
+                                                               lc16);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
@@ -2234,6 +2618,18 @@ static void fwd_launch(bool traced, void (*plain)(ChainFK), void (*traced_k)(Cha
   else hipLaunchKernelGGL(plain, dim3(grid), dim3(256), 0, st, k);
 }
 
+// the 16-position-wave forward chain of NW waves (64·NW threads), by LC / conditioning mode
+template <int NW>
+static void launch_fwd16(bool tr, bool lc, int cm, int grid, const ChainFK& k, hipStream_t st) {
+  void (*f)(ChainFK);
+  if (lc) f = cm == 0 ? (tr ? chain_fwd16_kernel<NW, true, 0, true> : chain_fwd16_kernel<NW, true, 0, false>)
+                      : (tr ? chain_fwd16_kernel<NW, true, 1, true> : chain_fwd16_kernel<NW, true, 1, false>);
+  else if (cm == 0) f = tr ? chain_fwd16_kernel<NW, false, 0, true> : chain_fwd16_kernel<NW, false, 0, false>;
+  else if (cm == 1) f = tr ? chain_fwd16_kernel<NW, false, 1, true> : chain_fwd16_kernel<NW, false, 1, false>;
+  else f = tr ? chain_fwd16_kernel<NW, false, 2, true> : chain_fwd16_kernel<NW, false, 2, false>;
+  hipLaunchKernelGGL(f, dim3(grid), dim3(64 * NW), 0, st, k);
+}
+
 int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   LBWN_REQUIRE(c.Cr == 32 && c.Cd == 32, "chain fwd: n_res = n_dil = 32 only");
   LBWN_REQUIRE(c.grid >= 1 && c.flags && c.status, "chain fwd: bad launch state");
@@ -2254,13 +2650,19 @@ int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
                      (((uintptr_t)c.lcact) & 15) == 0 && (((uintptr_t)c.lcimg) & 15) == 0,
                  "chain fwd: in-chain LC needs the split images, %d < n_lc_out <= %d, aligned rows", 16 * (LC_K - 1),
                  LC_KP);
-  const int tps = (c.T + LP - 1) / LP;
+  LBWN_REQUIRE(c.fwd_nw == 0 || ((c.fwd_nw == 4 || c.fwd_nw == 8) && c.wpack_x3 && c.SG),
+               "chain fwd: 16-position waves need the split images and the SG rows, 4 or 8 waves");
+  const int tp = lbwn_chain_fwd_tile(c.fwd_nw);
+  const int tps = (c.T + tp - 1) / tp;
   // hand-off flags only: the status word is sticky for the whole step
   if (!c.flags_zeroed) {
     if (int e = lbwn_zero_launch(c.flags, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st)) return e;
   }
   const int cm = (!c.gc_tab && !c.cond) ? 0 : (c.gc_tab && !c.cond) ? 1 : 2;
-  if (lc) {
+  const bool tr = c.trace != nullptr;
+  if (c.fwd_nw == 8) launch_fwd16<8>(tr, lc, cm, c.grid, k, st);
+  else if (c.fwd_nw == 4) launch_fwd16<4>(tr, lc, cm, c.grid, k, st);
+  else if (lc) {
     if (cm == 0) fwd_launch(c.trace != nullptr, chain_fwd_kernel<true, true, 0, false>, chain_fwd_kernel<true, true, 0, true>, c.grid, k, st);
     else fwd_launch(c.trace != nullptr, chain_fwd_kernel<true, true, 1, false>, chain_fwd_kernel<true, true, 1, true>, c.grid, k, st);   // lc: cond is null
   } else if (c.wpack_x3) {

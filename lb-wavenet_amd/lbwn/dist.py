@@ -13,6 +13,23 @@ import torch
 import torch.distributed as dist
 
 
+STATUS_BITS = 8     # the plan's status word uses bits 0-1 (lbwn.h); 8 leave room
+
+
+def status_to_bits(word, out):
+    """int32 status word [1] -> one float per bit [STATUS_BITS], so that the all_reduce SUM of
+    the ranks' words is an OR per bit once thresholded (a SUM of the words themselves would
+    turn two ranks' bit 0 into bit 1 and blame the wrong chain)."""
+    sh = torch.arange(STATUS_BITS, dtype=torch.int32, device=word.device)
+    out.copy_(((word.view(torch.int32) >> sh) & 1).to(torch.float32))
+
+
+def bits_to_status(bits, word):
+    """Inverse of status_to_bits after the reduction: bit k set if any rank set it."""
+    sh = torch.arange(STATUS_BITS, dtype=torch.int32, device=word.device)
+    word.view(torch.int32).copy_(((bits > 0).to(torch.int32) << sh).sum(dtype=torch.int32).view(1))
+
+
 class DPContext:
     def __init__(self, world=1, rank=0, local_rank=0):
         self.world, self.rank, self.local_rank = world, rank, local_rank
@@ -30,9 +47,10 @@ class DPContext:
             dist.broadcast(net.flat, 0)
 
     def reduce_grads(self, net):
-        """Σ over ranks of the raw gradient buffer, of (Σxent, n_valid, Σ|argmax diff|) and of
-        the step status words (a timed-out chain on ANY rank makes every rank's optimizer skip
-        the step on the device, so no rank applies garbage gradients).
+        """Σ over ranks of the raw gradient buffer and of (Σxent, n_valid, Σ|argmax diff|), and
+        the OR of the step status words (a timed-out chain on ANY rank makes every rank's
+        optimizer skip the step on the device, so no rank applies garbage gradients; the bits
+        travel as per-bit counts, status_to_bits).
 
         Two buckets, each ONE message (a staging copy of its flat ranges):
           0 "head": POST1, POST2, their biases, SKIP_BIAS + the stats + the status word — final
@@ -75,15 +93,15 @@ class DPContext:
         if not self.enabled:
             return
         n = net.grad_flat.numel()
-        buf = torch.empty(n + 4, dtype=torch.float32, device=net.grad_flat.device)
+        buf = torch.empty(n + 3 + STATUS_BITS, dtype=torch.float32, device=net.grad_flat.device)
         sw = net.status_word()
         buf[:n].copy_(net.grad_flat)
         buf[n:n + 3].copy_(net.stats[:3])
-        buf[n + 3:n + 4].copy_(sw)
+        status_to_bits(sw, buf[n + 3:])
         dist.all_reduce(buf)
         net.grad_flat.copy_(buf[:n])
         net.stats[:3].copy_(buf[n:n + 3])
-        sw.copy_(buf[n + 3:n + 4])
+        bits_to_status(buf[n + 3:], sw)
 
     def _comm_stream(self, device):
         s = getattr(self, '_comm', None)
@@ -117,7 +135,7 @@ class _Buckets:
             head.append((kb['skip_b'], lay.n_total))
             rest.append((lay.n_weights, kb['skip_b']))
         self.ranges = [head, rest]
-        sizes = [sum(b - a for a, b in head) + 4, sum(b - a for a, b in rest)]
+        sizes = [sum(b - a for a, b in head) + 3 + STATUS_BITS, sum(b - a for a, b in rest)]
         self.buf = [torch.empty(n, dtype=torch.float32, device=net.grad_flat.device) for n in sizes]
 
     @staticmethod
@@ -135,7 +153,7 @@ class _Buckets:
             o += b - a
         if k == 0:
             self.buf[0][o:o + 3].copy_(net.stats[:3])
-            self.buf[0][o + 3:o + 4].copy_(net.status_word())
+            status_to_bits(net.status_word(), self.buf[0][o + 3:])
 
     def unpack(self, k, net):
         o = 0
@@ -144,7 +162,7 @@ class _Buckets:
             o += b - a
         if k == 0:
             net.stats[:3].copy_(self.buf[0][o:o + 3])
-            net.status_word().copy_(self.buf[0][o + 3:o + 4])
+            bits_to_status(self.buf[0][o + 3:], net.status_word())
 
 
 def init(backend=None, device_type='cuda'):

@@ -78,7 +78,10 @@ class WaveNetTrain:
         self._last = None
         self._sp_cache = None
         self.init_vars(seed)
-        self.global_step_host = 0    # host mirror of GLOBAL_STEP (advanced by the optimizer)
+        # host mirror of GLOBAL_STEP: counts the optimizer calls (attempted steps) so the print
+        # cadence needs no sync; re-read from counters[0] by check_status, since a step skipped
+        # on the device (chain timeout) does not advance GLOBAL_STEP
+        self.global_step_host = 0
         # checkpoint surface (ckpt.py:13-81; the saveables are self.vars, tmodel.py:330)
         self.ckpt = Checkpoint(ckpt_path, n_keep_checkpoints, resume_step)
         self.ckpt.add_saveable_objects(self.state_tensors())
@@ -229,6 +232,7 @@ class WaveNetTrain:
 
     def check_status(self, T=None):
         st = self.status(T)
+        self.global_step_host = int(self.counters[0].item())
         if st:
             raise RuntimeError('lbwn: chain hand-off timed out (status word %#x): the failed steps were '
                                'not applied' % st)

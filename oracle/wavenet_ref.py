@@ -507,11 +507,15 @@ def sample_from_logits(logits_row, u):
 
 
 def generate(arch, P, batch_sz, n_steps, seed=0, teacher_q=None, gc_ids=None,
-             pre_bias=True, return_logits=False):
+             pre_bias=True, return_logits=False, forced_q=None):
     """imodel.py:214-272 restated with ring lookback buffers (semantically the
     reference's shift-by-chunk buffers, imodel.py:88-98, :190-207).
     Step i: input = zero vector (i=0) else onehot(prev draw) or onehot(teacher_q[i-1]).
     ``pre_bias``=True adds PRE_BIAS (tmodel-consistent; imodel.py:75-77 omits it).
+    ``forced_q`` [B, >= n-1] (test use): step i's input is forced_q[:, i-1] per stream instead
+    of this run's own draw, so the logits and draws are evaluated along another run's
+    trajectory (e.g. the GPU's) and compared draw by draw without a single near-tie flip
+    making the two streams diverge.
     Returns (samples int[B,n], wav float[B,n], [logits[B,n,Q]])."""
     dt = P['PRE'].dtype
     L = n_layers(arch)
@@ -533,6 +537,8 @@ def generate(arch, P, batch_sz, n_steps, seed=0, teacher_q=None, gc_ids=None,
         else:
             if teacher_q is not None and i - 1 < len(teacher_q):
                 q = np.full(batch_sz, teacher_q[i - 1], np.int64)
+            elif forced_q is not None:
+                q = np.asarray(forced_q[:, i - 1], np.int64)
             else:
                 q = prev_q
             z = P['PRE'][q].copy()

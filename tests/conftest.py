@@ -28,3 +28,12 @@ def lib():
     """The HIP library, loaded the product way (fails loudly when missing)."""
     from lbwn import _lib
     return _lib.load()
+
+
+@pytest.fixture(params=['w32', '128', '64'])
+def chain_tile(request, monkeypatch):
+    """The forward chain's form (LBWN_CHAIN_TILE, read at plan creation): 'w32' = 32-position
+    waves on 128-position tiles (chain_fwd_kernel), '128' / '64' = 16-position waves on 128- /
+    64-position tiles (chain_fwd16_kernel with 8 / 4 waves) -- the C4 tile axis."""
+    monkeypatch.setenv('LBWN_CHAIN_TILE', request.param)
+    return request.param

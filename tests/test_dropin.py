@@ -264,8 +264,8 @@ def _bucket_worker(rank, world, port, out_path):
     g = torch.Generator().manual_seed(100 + rank)
     grads = torch.randn(lay.n_total, generator=g) * 10.0 ** torch.randint(-6, 4, (lay.n_total,), generator=g)
     stats = torch.tensor([123.25 + rank, 1000.0 + rank, 7.0 * rank, 0.5])
-    a = _FakeNet(grads.clone(), stats.clone(), lay, status=2 * rank)
-    b = _FakeNet(grads.clone(), stats.clone(), lay, status=2 * rank)
+    a = _FakeNet(grads.clone(), stats.clone(), lay, status=1 + 2 * rank)     # ranks: 0b01, 0b11
+    b = _FakeNet(grads.clone(), stats.clone(), lay, status=1 + 2 * rank)
     dp.reduce_grads(a)          # two buckets (head / rest)
     dp.reduce_grads_flat(b)     # one message
     if rank == 0:
@@ -278,8 +278,9 @@ def _bucket_worker(rank, world, port, out_path):
 def test_dp_bucketed_equals_flat(tmp_path):
     """The two-bucket all-reduce (lbwn.dist: head bucket beside the backward's tail, the rest
     after it) gives bitwise the flat one-message result, for the gradient, the loss stats and
-    the status word (any rank's timeout reaches every rank), over 2 gloo ranks at arch5's
-    layout (GC + LC kinds included)."""
+    the status word (any rank's timeout reaches every rank as the OR of the words: 0b01 | 0b11
+    = 0b11, where a SUM would read 0b100), over 2 gloo ranks at arch5's layout (GC + LC kinds
+    included)."""
     import torch.multiprocessing as mp
     out = str(tmp_path / 'bk.npz')
     port = 29500 + (os.getpid() + 13) % 1000
@@ -287,7 +288,7 @@ def test_dp_bucketed_equals_flat(tmp_path):
     r = np.load(out)
     assert np.array_equal(r['ga'].view(np.uint32), r['gb'].view(np.uint32))
     assert np.array_equal(r['sa'][:3], r['sb'][:3])
-    assert int(r['wa'][0]) == int(r['wb'][0]) == 2
+    assert int(r['wa'][0]) == int(r['wb'][0]) == 3
 
 
 def _ckpt_worker(rank, world, port, path):

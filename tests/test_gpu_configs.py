@@ -101,7 +101,7 @@ def _check_config(arch, B, T, seed=0, grads=True, z_identical=True):
     close(s, cache['S'].reshape(M, -1), 1e-5, 'skip sum')
 
 
-def test_arch5_deep_stack():
+def test_arch5_deep_stack(chain_tile):
     """C4 dims at B=2, T=1024: 4 mel frames per stream through the 4-stage upsample."""
     arch = _arch('arch5')
     assert arch['n_lc_in'] == arch['n_lc_out'] == 80 and arch['lc_upsample'] == [4, 4, 4, 4]
@@ -109,13 +109,13 @@ def test_arch5_deep_stack():
     _check_config(arch, 2, 1024)
 
 
-def test_arch5_tile_rounds():
+def test_arch5_tile_rounds(chain_tile):
     """arch5 with more 128-position tiles (4 x 66 = 264) than CUs, so the persistent chains
     run in rounds, at T = 8448 = 33 mel hops."""
     _check_config(_arch('arch5'), 4, 8448, seed=1, z_identical=False)
 
 
-def test_arch1_forward_loss():
+def test_arch1_forward_loss(chain_tile):
     """C1: arch1 (par/arch1.json, n_post1 normalised to n_post, GC 17/377, no use_bias key
     -> True), B=2, T=512 forward + loss + gradients."""
     arch = _arch('arch1')

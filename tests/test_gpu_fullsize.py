@@ -123,7 +123,7 @@ def test_restatement_matches_oracle():
 
 
 @pytest.mark.parametrize('arch_name,B', [('arch5', 32), ('arch3', 8)])
-def test_full_size_forward_backward(arch_name, B):
+def test_full_size_forward_backward(arch_name, B, chain_tile):
     """C4 (arch5, B=32) and C2 (arch3, B=8) at T=4096: every layer's z on the HIP path's own
     inputs, z end to end, the skip sum, SAVE, n_valid, mean xent and every gradient."""
     arch = _arch(arch_name)

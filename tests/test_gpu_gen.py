@@ -138,3 +138,46 @@ def test_gen_arch3_gemm_form(form):
     assert mism == 0, '%d / %d draws differ' % (mism, got.size)
     np.testing.assert_allclose(g.logits().cpu().numpy(), lg_ref[:, -1], rtol=0, atol=1e-4 * np.abs(lg_ref).max())
     assert int(g.tensor('step', torch.int64).item()) == n
+
+
+def _near_tie(lg_row, u, tol=5e-5):
+    """True when the inverse-CDF target u·Σe lies within tol·Σe of a CDF boundary of the
+    oracle's float64 logits: an fp32 evaluation of the same logits may then pick the
+    neighbouring code (sample_from_logits, oracle/wavenet_ref.py)."""
+    e = np.exp(lg_row - lg_row.max())
+    c = np.cumsum(e)
+    return float(np.min(np.abs(c - u * c[-1]))) <= tol * c[-1]
+
+
+@pytest.mark.parametrize('B,n', [(10, 2100), (80, 1100)])
+def test_gen_arch3_full_ring_depth(B, n, form):
+    """C3 at its own chunk size (1000, generate.py:17) and long enough that every lookback ring
+    wraps: with d <= 512 each layer's ring (slot t & (d-1)) is rewritten >= 2x (4x at B=10), so
+    the d = 512 layers' dilated taps read values this run wrote 512 steps earlier (imodel.py:88-122,
+    :190-207), and two chunk boundaries (graph replay -> replay -> a 100-step tail launch) are
+    crossed.  B = 80 runs as 5 stream groups of the persistent launch.
+
+    The oracle is evaluated along the GPU's own trajectory (forced_q = the GPU's draws), so
+    every one of the B·n draws is checked against the float64 logits it was drawn from; a
+    difference is allowed only at a near tie (u·Σe within 5e-5 of a CDF boundary), and at most
+    a couple of those.  With no difference, the free-running oracle's draws equal the GPU's
+    exactly (each step's input is then the same on both sides)."""
+    arch = load_arch(os.path.join(ROOT, 'par', 'arch3.json'))
+    g, P = make_gen(arch, B, chunk=1000)
+    n_out, wav, rem = g.run(n)
+    torch.cuda.synchronize()
+    assert g.persistent == (form == 'persistent')
+    assert int(g.tensor('status', torch.int32).item()) == 0
+    assert int(g.tensor('step', torch.int64).item()) == n
+    assert wav.shape == (B, (n // 1000) * 1000) and rem == n % 1000
+    got = g.samples().cpu().numpy()[:, :n]
+    assert len(np.unique(got)) > 16                      # the draws are not stuck on a few codes
+    ref, w_ref, lg = R.generate(arch, P, B, n, seed=7, return_logits=True, forced_q=got)
+    bad = np.argwhere(got != ref)
+    ties = [(int(b), int(i)) for b, i in bad if _near_tie(lg[b, i], R.philox_uniform(7, int(b), int(i)))]
+    assert len(ties) == len(bad), 'draws differ away from a CDF tie at (stream, step) %s' % (
+        [tuple(x) for x in bad[:8].tolist()],)
+    assert len(bad) <= 2, bad.tolist()
+    np.testing.assert_allclose(g.logits().cpu().numpy(), lg[:, -1], rtol=0, atol=1e-4 * np.abs(lg[:, -1]).max())
+    if len(bad) == 0:
+        np.testing.assert_allclose(wav.cpu().numpy(), w_ref[:, :wav.shape[1]], rtol=1e-6, atol=1e-6)

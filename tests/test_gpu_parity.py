@@ -286,7 +286,7 @@ def _run_oracle(arch, net, q, ids):
 
 @pytest.mark.parametrize('which,B,T,mode', [('small', 2, 256, 1), ('small', 3, 200, 1), ('arch3', 2, 512, 1),
                                             ('arch3', 2, 512, 0), ('arch3', 8, 4096, 1)])
-def test_plan_forward_backward(lib, gemm_mode, which, B, T, mode):
+def test_plan_forward_backward(lib, gemm_mode, which, B, T, mode, chain_tile):
     """mode 1: GEMMs and the forward chain's conv/residual on the bf16 cores by exact splitting;
     mode 0: every product on the f32 MFMA.  Same bars for both.  ('arch3', 8, 4096) is the
     benchmarked C2 shape itself: 256 tiles of the persistent chains, every gradient vs float64."""
@@ -346,7 +346,7 @@ def test_plan_forward_backward(lib, gemm_mode, which, B, T, mode):
 
 
 @pytest.mark.parametrize('B,T,nbl', [(4, 9000, 10), (2, 300, 3)])
-def test_chain_matches_per_layer(monkeypatch, B, T, nbl):
+def test_chain_matches_per_layer(monkeypatch, B, T, nbl, chain_tile):
     """The persistent chain kernel (tile hand-offs inside one launch) against the one-launch-
     per-layer kernels: same x_l for every layer and same z.  (4, 9000): 284 tiles > 256 CUs,
     so tiles run in rounds, with a ragged last tile; nbl=10 takes d up to the 512-row halo."""
@@ -389,7 +389,7 @@ def cond_arch(gc, lc, C=32):
 
 
 @pytest.mark.parametrize('gc,lc,C', [(1, 0, 32), (0, 1, 32), (1, 1, 32), (1, 1, 16)])
-def test_plan_conditioning(gc, lc, C):
+def test_plan_conditioning(gc, lc, C, chain_tile):
     """GC (tmodel.py:92-114, :150-154) and LC (tmodel.py:68-83, :155-160) through the plan:
     forward (SAVE, loss) and every gradient against the oracle.  C = 32 runs the persistent
     chain kernels, C = 16 the per-layer kernels."""
