@@ -443,27 +443,40 @@ class TrainBench:
         torch.cuda.empty_cache()
 
 
-def chain_dilation_sweep(arch_file, B, T, dp, steps=4, gc=None):
-    """C4's dilation sweep (BASELINE configs[3], SURVEY §8d "Shapes"): in-kernel clock stamps
-    of one chain block's tile (LBWN_CHAIN_TRACE, read at plan creation) give each layer's
-    start-to-start time in the forward and the backward chain; layers are grouped by dilation
-    d = 2^bl (tmodel.py:313-325), median over the n_blocks layers of each d and over steps.
-    The tile is the chains' 128 positions x 32 channels (4 waves, one block per CU): the only
-    LDS tile they template -- a 64-position tile leaves two of four SIMDs idle (the 65 KB of
-    double-buffered weight images per block do not fit twice in 160 KB), a 256-position one
-    needs 2 waves per SIMD at <= 256 registers (the chains hold 330-470)."""
+FWD_TILES = {'128': dict(positions=128, waves=8, waves_per_simd=2, kernel='chain_fwd16_kernel<8>'),
+             '64': dict(positions=64, waves=4, waves_per_simd=1, kernel='chain_fwd16_kernel<4>'),
+             'w32': dict(positions=128, waves=4, waves_per_simd=1, kernel='chain_fwd_kernel (32-position waves)')}
+
+
+def chain_dilation_sweep(arch_file, B, T, dp, steps=4, gc=None, tile=None):
+    """C4's LDS-tile x dilation sweep (BASELINE configs[3], SURVEY §8d "Shapes"): for one forward
+    chain tile (LBWN_CHAIN_TILE, read at plan creation: '128' / '64' = 16-position waves on 128- /
+    64-position tiles, 'w32' = 32-position waves on 128), the timed step and the in-kernel clock
+    stamps of one chain block's tile (LBWN_CHAIN_TRACE), which give each layer's start-to-start
+    time in the forward and the backward chain; layers grouped by dilation d = 2^bl
+    (tmodel.py:313-325), median over the n_blocks layers of each d and over steps.  The backward
+    chain keeps its 128-position tile (32-position waves) in every row."""
     import torch
     from lbwn.arch import load_arch, n_layers
     arch = load_arch(arch_file, num_global_cond=gc)
-    old = os.environ.get('LBWN_CHAIN_TRACE')
-    os.environ['LBWN_CHAIN_TRACE'] = '1'
+    saved = {k: os.environ.get(k) for k in ('LBWN_CHAIN_TRACE', 'LBWN_CHAIN_TILE')}
+
+    def restore():
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    if tile is not None:
+        os.environ['LBWN_CHAIN_TILE'] = tile
     try:
+        tb = TrainBench(arch, B, T, dp)          # untraced: the tile's step time
+        ms, _, _, _ = tb.run(5, 2)
+        tb.close()
+        os.environ['LBWN_CHAIN_TRACE'] = '1'
         tb = TrainBench(arch, B, T, dp)
     finally:
-        if old is None:
-            os.environ.pop('LBWN_CHAIN_TRACE', None)
-        else:
-            os.environ['LBWN_CHAIN_TRACE'] = old
+        restore()
     L, nbl = n_layers(arch), arch['n_block_layers']
     runs = []
     for i in range(steps + 1):
@@ -483,10 +496,17 @@ def chain_dilation_sweep(arch_file, B, T, dp, steps=4, gc=None):
         fc, bc = float(np.median(fwd[:, fl])), float(np.median(bwd[:, bls]))
         rows.append({'d': 1 << bl, 'fwd_cycles': round(fc), 'bwd_cycles': round(bc),
                      'fwd_us': round(fc / 2400.0, 3), 'bwd_us': round(bc / 2400.0, 3)})
-    return {'tile_positions': 128, 'tile_channels': 32, 'blocks_per_cu': 1, 'waves_per_block': 4,
+    t = tile or os.environ.get('LBWN_CHAIN_TILE') or DEFAULT_TILE
+    info = FWD_TILES.get(t, {})
+    return {'tile': t, 'fwd_tile_positions': info.get('positions'), 'fwd_waves_per_block': info.get('waves'),
+            'fwd_waves_per_simd': info.get('waves_per_simd'), 'fwd_kernel': info.get('kernel'),
+            'bwd_tile_positions': 128, 'tile_channels': 32, 'blocks_per_cu': 1, 'ms_per_step': ms,
             'clock': 'clock64 cycles, us at 2.4 GHz', 'traced_block': 1, 'per_dilation': rows,
             'note': 'per-layer start-to-start time of one chain block (its first tile), median over the '
-                    'n_blocks layers of each dilation and %d steps' % steps}
+                    'n_blocks layers of each dilation and %d steps; ms_per_step: 5 timed steps' % steps}
+
+
+DEFAULT_TILE = 'w32'    # the library's default forward chain form (engine.cpp, LBWN_CHAIN_TILE unset)
 
 
 CANDS = ['layer_bwd', 'dskip', 'layer_fwd', 'post1_fwd', 'dpost1', 'ds', 'post2_fwd', 'dpost2', 'dh']
@@ -656,7 +676,9 @@ def main(argv=None):
         par = lambda f: os.path.join(ROOT, 'par', f)   # noqa: E731
         out['c4'] = sub_bench(par('arch5.json'), 32, 4096, dp, 10, 3, label='C4: arch5 deep stack, B=32 x T=4096, '
                               'train fwd+bwd+Adam, 1 GPU')
-        out['c4']['sweep'] = chain_dilation_sweep(par('arch5.json'), 32, 4096, dp)
+        out['c4']['sweep'] = {'default_tile': os.environ.get('LBWN_CHAIN_TILE') or DEFAULT_TILE,
+                              'tiles': [chain_dilation_sweep(par('arch5.json'), 32, 4096, dp, tile=t)
+                                        for t in ('128', '64', 'w32')]}
         out['c5_per_gpu'] = sub_bench(par('arch5.json'), 8, 4096, dp, 10, 3,
                                       label='C5 per-GPU share on one GPU: arch5, B=8 x T=4096 (the N>1 runs '
                                             'default to this per rank: scaling reference)')

@@ -53,9 +53,11 @@ struct lbwn_plan {
   bool chain = false;            // persistent layer-chain kernels (n_res = n_dil = 32)
   int chain_grid = 0;            // resident blocks for the chain (set on first use)
   int fwd_grid = 0;              // ... for the forward chain (its tile: lbwn_chain_fwd_tile(fwd_nw))
-  // forward chain form (LBWN_CHAIN_TILE at plan creation): 0 = 32-position waves on 128-position
-  // tiles (chain_fwd_kernel), 8 / 4 = 16-position waves on 128- / 64-position tiles
-  int fwd_nw = 0;
+  // chain forms (LBWN_CHAIN_TILE = <fwd>[:<bwd>] at plan creation, each 128 / 64 / w32): 0 =
+  // 32-position waves on 128-position tiles (chain_fwd_kernel / chain_bwd_x3_kernel), 8 / 4 =
+  // 16-position waves on 128- / 64-position tiles (chain_fwd16_kernel / chain_bwd16_kernel)
+  int fwd_nw = 0, bwd_nw = 0;
+  int bwd_grid = 0;
   // Backward side stream (chain plans): the head weight gradients (dPOST2, dPOST1) run on the
   // main stream before the chain; dSKIP follows the chain on the main stream while `aux2` runs
   // the HBM-bound slab reduction and dPRE scatter beside it.  A chain block takes a whole CU's
@@ -278,8 +280,28 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     LBWN_REQUIRE(T % hop == 0, "plan: slice_sz %d is not a multiple of the mel hop %d", T, hop);
     LBWN_REQUIRE(a->n_lc_in % 4 == 0 && a->n_lc_out % 4 == 0, "plan: n_lc_in/n_lc_out must be multiples of 4");
   }
+  int fwd_nw = 0, bwd_nw = 0;   // chain forms (lbwn_plan::fwd_nw)
+  {
+    const char* tv = getenv("LBWN_CHAIN_TILE");
+    auto form = [](const char* v, size_t n, int* nw) {
+      if (n == 2 && !strncmp(v, "64", 2)) *nw = 4;
+      else if (n == 3 && !strncmp(v, "128", 3)) *nw = 8;
+      else if (n == 3 && !strncmp(v, "w32", 3)) *nw = 0;
+      else return false;
+      return true;
+    };
+    if (tv && tv[0]) {
+      const char* colon = strchr(tv, ':');
+      const size_t nf = colon ? (size_t)(colon - tv) : strlen(tv);
+      bool ok = form(tv, nf, &fwd_nw);
+      if (ok) ok = colon ? form(colon + 1, strlen(colon + 1), &bwd_nw) : form(tv, nf, &bwd_nw);
+      LBWN_REQUIRE(ok, "LBWN_CHAIN_TILE must be <fwd>[:<bwd>] with each 128, 64 or w32 (got '%s')", tv);
+    }
+  }
   lbwn_plan* p = new (std::nothrow) lbwn_plan();
   LBWN_REQUIRE(p, "plan: out of host memory");
+  p->fwd_nw = fwd_nw;
+  p->bwd_nw = bwd_nw;
   p->a = *a;
   p->B = B;
   p->T = T;
@@ -344,7 +366,7 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     p->oGA[i] = carve(cur, sizeof(float) * (size_t)M * p->Cr);
     p->oGC0[i] = carve(cur, sizeof(float) * (size_t)M * p->Cr);
   }
-  const int ntiles = B * ((T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS);
+  const int ntiles = B * ((T + 63) / 64);   // the finest chain tile: any backward form fits
   p->oSLAB = carve(cur, sizeof(float) * (size_t)L * std::max(nblk, ntiles) * lbwn_layer_slab_stride());
   p->oSPLIT = carve(cur, sizeof(float) * (size_t)p->split_floats);
   p->oSPLIT2 = carve(cur, sizeof(float) * (size_t)lbwn_pre_grad_ws_floats(p->Q, p->Cr));   // dPRE partials
@@ -354,13 +376,6 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->oCPART = carve(cur, sizeof(float) * (size_t)lbwn_colpart_parts(M) * (p->Cp + p->Cs));
   // [status (16 B) | forward hand-off flags | backward hand-off flags], zeroed by ONE memset per
   // step (each flag block padded to 16 B)
-  {
-    const char* tv = getenv("LBWN_CHAIN_TILE");
-    if (tv && !strcmp(tv, "64")) p->fwd_nw = 4;
-    else if (tv && !strcmp(tv, "128")) p->fwd_nw = 8;
-    else if (tv && !strcmp(tv, "w32")) p->fwd_nw = 0;
-    else LBWN_REQUIRE(!tv || !tv[0], "LBWN_CHAIN_TILE must be 64, 128 or w32 (got '%s')", tv);
-  }
   // one flag per tile of the finest chain tile (64 positions), so any form fits
   p->nflag_bytes = (sizeof(unsigned) * (size_t)B * ((T + 63) / 64) + 15) / 16 * 16;
   p->oSTATUS = carve(cur, 16 + 2 * p->nflag_bytes);
@@ -381,7 +396,7 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     const long ncond = 2L * L * p->Cd;
     p->oGCTAB = p->Ge ? carve(cur, f * (size_t)L * p->ncat1 * 2 * p->Cd) : 0;
     p->oGCD = p->Ge ? carve(cur, f * (size_t)L * p->ncat1 * 2 * p->Cd) : 0;
-    p->oTGID = p->Ge ? carve(cur, sizeof(int) * (size_t)B * ((T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS)) : 0;
+    p->oTGID = p->Ge ? carve(cur, sizeof(int) * (size_t)B * ((T + 63) / 64)) : 0;
     p->oGCPART = p->Ge ? carve(cur, f * (size_t)lbwn_gc_part_floats(L, p->Ge, p->Cd)) : 0;
     long rows = (long)B * (T / hop);
     for (int i = 0; i < 8; ++i) {
@@ -471,6 +486,8 @@ int ensure_device(lbwn_plan* p) {
   p->chain_grid = std::max(1, std::min(ntiles, ncu));
   const int tpf = lbwn_chain_fwd_tile(p->fwd_nw);
   p->fwd_grid = std::max(1, std::min(p->B * ((p->T + tpf - 1) / tpf), ncu));
+  const int tpb = lbwn_chain_fwd_tile(p->bwd_nw);
+  p->bwd_grid = std::max(1, std::min(p->B * ((p->T + tpb - 1) / tpb), ncu));
   if (p->overlap) {
     int least = 0, greatest = 0;
     LBWN_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -985,7 +1002,9 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   const int sstr = lbwn_layer_slab_stride();
   float* SLABS = at<float>(ws, p->oSLAB);
   if (p->chain) {
-    const int ntiles = B * ((T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS);
+    const bool b16 = p->bwd_nw && p->fwd_x3 && lbwn_gemm_mode() == 1;
+    const int tpb = lbwn_chain_fwd_tile(b16 ? p->bwd_nw : 0);
+    const int ntiles = B * ((T + tpb - 1) / tpb);
     lbwn_chain_args c;
     memset(&c, 0, sizeof(c));
     c.X = X; c.xls = p->x_layer_stride; c.DZ = DZ; c.ldz = ldz; c.wpack = WPK; c.ids = ids;
@@ -1003,6 +1022,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     p->bwd_flags_fresh = false;
     if (p->ctrace_blk >= 0) { c.trace = at<long long>(ws, p->oCTRACE); c.trace_blk = p->ctrace_blk; }
     c.B = B; c.T = T; c.H = p->H; c.L = L; c.nbl = p->nbl; c.Cr = Cr; c.Cd = Cd; c.grid = p->chain_grid;
+    if (b16) { c.bwd_nw = p->bwd_nw; c.grid = p->bwd_grid; }
     Probe(p, st, "layer_bwd");
     if ((e = lbwn_chain_bwd_launch(c, st))) return e;
     Probe::end(p, st, "layer_bwd");

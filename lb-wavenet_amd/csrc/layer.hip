@@ -101,9 +101,10 @@ __global__ void pack_layers_kernel(const float* sig, const float* gate, const fl
 //   then bs[64], br[32] as f32.
 constexpr int XW_ROW = 200, XR_ROW = 104;
 constexpr int XB_OFF = 64 * XW_ROW + 32 * XR_ROW;             // bf16 offset of the f32 biases
-constexpr int XIMG_US = XB_OFF + 2 * 96;                       // bf16 elements per layer image
-constexpr int XIMG_F = XIMG_US / 2;                            // = 8160 floats, multiple of 4
-static_assert(XIMG_F % 4 == 0 && XB_OFF % 8 == 0, "x3 image alignment");
+// bf16 elements per layer image, padded to 32 whole 1-KiB LDS-DMA pieces (the pad is never read)
+constexpr int XIMG_US = (XB_OFF + 2 * 96 + 511) / 512 * 512;
+constexpr int XIMG_F = XIMG_US / 2;                            // = 8192 floats
+static_assert(XIMG_F % 256 == 0 && XB_OFF % 8 == 0, "x3 image alignment");
 
 // Split image of a layer's LC projection for the forward chain's in-chain LC term
 // (tmodel.py:155-160: v_k += lc·LC_k), bf16 units: LCT[o (sig 0..31 | gate 32..63)][plane][k 0..79]
@@ -1040,7 +1041,11 @@ template <int NW, bool LC, int CM, bool TR>
 __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
   constexpr int TP = 16 * NW, NT = 64 * NW;
   constexpr int IMGF = XIMG_F;
-  constexpr int PF = (IMGF / 4 + NT - 1) / NT;          // float4 per thread to prefetch one image
+  // the LC form (register-tight at two waves per SIMD) moves the image of layer l+2 by LDS-DMA
+  // after the publish barrier (landing with the next layer's halo loads, like the LC image);
+  // the others prefetch it into registers behind the halo loads and write it after the barrier
+  constexpr bool DMAIMG = LC;
+  constexpr int PF = DMAIMG ? 1 : (IMGF / 4 + NT - 1) / NT;   // float4 per thread to prefetch one image
   constexpr int NR = TP * 8 / NT;                       // float4 per thread of a TP-row tile (2)
   __shared__ __attribute__((aligned(16))) float sm[cf16_lds<NW>(LC)];
   __shared__ int s_fail;
@@ -1153,7 +1158,7 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
           const int e = min(tid + NT * i, nh * 8 - 1), row = e >> 3, c4 = (e & 7) * 4;
           hv[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((a.H + t0 + row - d) * 32 + c4) * 4, 0, 16);
         }
-        {
+        if (!DMAIMG) {
           const floatx4* src = (const floatx4*)(wsrc + (long)min(l + 2, a.L - 1) * IMGF);
 #pragma unroll
           for (int i = 0; i < PF; ++i) pf[i] = src[min(tid + NT * i, IMGF / 4 - 1)];
@@ -1231,7 +1236,13 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
       FSTAMP(10);
       if (tid == 0 && l + 1 < a.L) publish_flag(a.flags + tile, (unsigned)(l + 1));
       if (LC && l + 2 < a.L) dma_lc16_image<NW>(a.lcimg, l + 2, LCI, w, lane);
-      if (l + 2 < a.L) {
+      if (DMAIMG && l + 2 < a.L) {
+        const float* src = wsrc + (long)(l + 2) * IMGF + lane * 4;
+        float* dst = IMG0 + (l & 1) * IMGF;
+#pragma unroll
+        for (int i = 0; i < IMGF / 256 / NW; ++i) dma16(src + (w + NW * i) * 256, dst + (w + NW * i) * 256);
+      }
+      if (!DMAIMG && l + 2 < a.L) {
         float* dst = IMG0 + (l & 1) * IMGF;
 #pragma unroll
         for (int i = 0; i < PF; ++i) {
@@ -2214,6 +2225,372 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
   }
 }
 
+// ---- backward chain, 16-position waves (round 4) --------------------------------------------
+// chain_bwd16_kernel<NW, TR>: chain_bwd_x3_kernel's layer walk, hand-off protocol, images and slab
+// layout with 16 positions per wave and NW waves per block (tile TP = 16·NW: NW = 8 puts two
+// waves on each SIMD).  Lane = (j = lane & 15: the wave's position, g = lane >> 4); two channel
+// layouts per lane (q0 = 2(g >> 1), h = g & 1):
+//   N  (x / g / out_a / out_c0): block xb register r = channel 16xb + 4g + r;
+//   Zl (dz / z / σ / dv, the forward's z layout): block b register r = channel 8(q0 + b) + 4h + r.
+//  * dz = dZ + RES·g on v_mfma_f32_16x16x4_f32 (f32 products, as chain_bwd_x3_kernel): A row i of
+//    block b = z channel ch16(b, i), k = g's channel 16xb + 4g + r;
+//  * dx = W·dv on 16x16x32 bf16 splits, k-step S = sig / gate: the lane's 8 dv values of kind S
+//    (Zl blocks 0, 1) are exactly the backward image's k order kk = 32S + 8g + e (WD unchanged);
+//  * dSIG / dGATE: wave w takes weight-gradient tile w & 3 (2·kind + tap) over positions
+//    [(w >> 2)·TP/NH, +TP/NH) (NH = NW/4 position halves) on 32x32x16 bf16 splits (k = 16
+//    positions), and dRES quarter w & 3 over the same positions on 16x16x4 f32; with NH = 2 the
+//    two halves' partials are summed through LDS by waves 0-3.
+// LDS rows: Xp / Xc / ZT unpadded (LDS-DMA), DVs / DVg / G / OC padded to XS = 36 floats (the
+// b128 own-row writes of 16 consecutive rows fall on 16 distinct bank groups).
+template <int NW>
+constexpr int cb16_lds() { return BIMG_F + 3 * 16 * NW * 32 + 4 * 16 * NW * XS + 8 * 96; }
+static_assert(cb16_lds<8>() * 4 + 16 <= 160 * 1024, "chain bwd16 LDS");
+static_assert(8 * 1280 <= 3 * 128 * 32, "bwd16: the partial scratch must fit in Xp | Xc | ZT");
+
+// GC rows of a wave whose 16 positions are not one voice: dv column sums per run of equal ids,
+// one atomic per run and column (as gc_scatter_x3, 16 positions)
+LBWN_DEV void gc_scatter16(float* gtab, long ld, const float* DVs, const float* DVg, int w, int lane, int Cd,
+                           unsigned starts, int pid) {
+  const int o = lane, oc = o & 31;
+  const float* pl = o < 32 ? DVs : DVg;
+  const int col = o < 32 ? oc : Cd + oc;
+  unsigned rest = starts;
+  while (rest) {   // wave-uniform
+    const int p0 = __ffs(rest) - 1;
+    rest &= rest - 1;
+    const int p1 = rest ? __ffs(rest) - 1 : 16;
+    const int id = __shfl(pid, p0);
+    if (id < 0) continue;   // positions past T
+    float s = 0.f;
+    for (int p = p0; p < p1; ++p) s += pl[(16 * w + p) * XS + oc];
+    if (oc < Cd) atomicAdd(gtab + (long)id * ld + col, s);
+  }
+}
+
+template <int NW, bool TR>
+__global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
+  constexpr int TP = 16 * NW, NT = 64 * NW, NH = NW / 4, PH = TP / NH;   // PH: positions per half
+  constexpr int NR = TP * 8 / NT;                                        // float4 per thread of a tile (2)
+  __shared__ __attribute__((aligned(16))) float sm[cb16_lds<NW>()];
+  __shared__ int s_fail;
+  float* IMG = sm;
+  const unsigned short* WD = (const unsigned short*)IMG;
+  const float* Rs = IMG + BD_US / 2;
+  float* Xp = IMG + BIMG_F;
+  float* Xc = Xp + TP * 32;
+  float* ZT = Xc + TP * 32;
+  float* DVs = ZT + TP * 32;
+  float* DVg = DVs + TP * XS;
+  float* G = DVg + TP * XS;
+  float* OC = G + TP * XS;
+  float* part = OC + TP * XS;   // [8][96] bias partials
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i16 = lane & 15, g = lane >> 4, q0 = 2 * (g >> 1), h = g & 1;
+  const int r = 16 * w + i16;
+  const int tps = (a.T + TP - 1) / TP, ntiles = a.B * tps;
+  const int oc_bytes = (int)std::min<long>(a.ocls * 4, 0x7fffffffL);
+  if (tid == 0) s_fail = 0;
+  for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
+    const int tile = ntiles - 1 - it;
+    const int b = tile / tps, tt = tile % tps, t0 = tt * TP;
+    const int t = t0 + r;
+    const bool valid = t < a.T;
+    const long mb = (long)b * a.T, m = mb + t, mc = mb + min(t, a.T - 1);
+    const long sb = (long)b * (a.H + a.T) * 32;
+    const int myid = (a.gc_tab && valid) ? a.ids[m] : 0;
+    const int tile_id = a.gc_tab ? a.ids[mb + t0] : 0;
+    const bool tile_uni = __syncthreads_and(!valid || myid == tile_id);
+    if (a.tile_gid && tid == 0) a.tile_gid[tile] = tile_uni ? tile_id : -1;
+    // this wave's id runs over its 16 positions (lanes j of the first group), -1 past T
+    const int gc_pid = valid ? myid : -1;
+    const int gc_prev = __shfl(gc_pid, max(lane - 1, 0) & 15);
+    const unsigned gc_starts = (unsigned)(__ballot(g == 0 && (i16 == 0 || gc_pid != gc_prev)) & 0xffffull);
+    // per-layer rows of this lane's position (Zl channels): dZ, z, σ, issued a layer ahead
+    floatx4 dzr[2], zr[2], sgr[2];
+    auto load_regs = [&](int l) {
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb) {
+        dzr[bb] = *(const floatx4*)(a.DZ + l * a.dzls + sg_off(mc, q0 + bb, h));
+        zr[bb] = *(const floatx4*)(a.Zf + mc * a.lddz + (long)l * 32 + 8 * (q0 + bb) + 4 * h);
+        sgr[bb] = *(const floatx4*)(a.SG + (long)l * a.sgls + sg_off(mc, q0 + bb, h));
+      }
+    };
+    auto dma_image = [&](int l) {
+      const float* src = a.bimg + (long)l * BIMG_F + lane * 4;
+      for (int i = w; i < BIMG_F / 256; i += NW) dma16(src + i * 256, IMG + i * 256);
+    };
+    __syncthreads();  // previous tile's LDS use done
+    dma_image(a.L - 1);
+    load_regs(a.L - 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    floatx4 oa[2];  // out_a of layer l+1, own row (N layout)
+    oa[0] = oa[1] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && it == (int)blockIdx.x;
+#define XSTAMP(i) if (TR && trc) a.trace[16 * l + (i)] = clock64()
+    for (int l = a.L - 1; l >= 0; --l) {
+      XSTAMP(0);
+      const int d = 1 << (l % a.nbl);
+      const int dn = (l + 1 < a.L) ? 1 << ((l + 1) % a.nbl) : 0;
+      // 1. G = dx_{l+1} rows: out_c0_{l+1}[t + dn] (own OC / the producer's published rows) + out_a
+      if (dn) {
+        const int ptt = tt + max(1, dn / TP);
+        if (ptt < tps) {
+          if (tid == 0 && !s_fail) {
+            if (!wait_flag_ge(a.flags + (long)b * tps + ptt, (unsigned)(a.L - l - 1), a.status, 2u)) s_fail = 1;
+          }
+          __syncthreads();
+        }
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)(l + 1) * a.ocls, (short)0, oc_bytes, BUF_DW3);
+        floatx4 gl[NR], go[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int e = tid + NT * i, row = e >> 3, c4 = (e & 7) * 4, sr = row + dn;
+          const int ts = min(t0 + sr, a.T - 1);
+          gl[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
+          go[i] = *(const floatx4*)(OC + min(sr, TP - 1) * XS + c4);
+        }
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int e = tid + NT * i, row = e >> 3, c4 = (e & 7) * 4, sr = row + dn, ts = t0 + sr;
+          floatx4 v = sr < TP ? go[i] : gl[i];
+          if (ts >= a.T) v = floatx4{0.f, 0.f, 0.f, 0.f};
+          *(floatx4*)(G + row * XS + c4) = v;
+        }
+        // lands this wave's part of the weight image (DMA'd during the last layer) and the
+        // prefetched rows; the barrier then covers every wave's part
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb) asm volatile("" ::"v"(dzr[bb]), "v"(zr[bb]), "v"(sgr[bb]));
+      const float* xl = a.X + (long)l * a.xls + sb;
+      // this layer's x rows (x[t-d] | x[t]) and z rows by LDS-DMA into Xp / Xc / ZT, 8 rows per piece
+      auto dma_rows3 = [&](int k) {
+        const int row = 8 * k + (lane >> 3), c4 = (lane & 7) * 4;
+        const int trow = min(t0 + row, a.T - 1);
+        dma16(xl + (long)(a.H + trow - d) * 32 + c4, Xp + 8 * k * 32);
+        dma16(xl + (long)(a.H + trow) * 32 + c4, Xc + 8 * k * 32);
+        dma16(a.Zf + (mb + trow) * a.lddz + (long)l * 32 + c4, ZT + 8 * k * 32);
+      };
+      XSTAMP(1);
+      floatx4 gv[2];
+#pragma unroll
+      for (int xb = 0; xb < 2; ++xb) {   // own row: + out_a (the top layer writes it, g = 0)
+        float* gp = G + r * XS + 16 * xb + 4 * g;
+        floatx4 v = dn ? *(const floatx4*)gp : floatx4{0.f, 0.f, 0.f, 0.f};
+        v += oa[xb];
+        gv[xb] = v;
+        *(floatx4*)gp = v;
+      }
+      // 2. dz = dZ + RES·g  (f32 MFMA 16x16x4: k = g's channel 16xb + 4g + rr)
+      floatx4 dz[2];
+      {
+        floatx4 rx[2][2];
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+          for (int xb = 0; xb < 2; ++xb) rx[bb][xb] = *(const floatx4*)(Rs + ch16(bb, i16) * XS + 16 * xb + 4 * g);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) dz[bb] = valid ? dzr[bb] : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int xb = 0; xb < 2; ++xb) {
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb)
+              dz[bb] = __builtin_amdgcn_mfma_f32_16x16x4f32(rx[bb][xb][rr], gv[xb][rr], dz[bb], 0, 0, 0);
+          // x / z rows of this layer: pieces k = w, w + NW, ... (3·TP/8 rows of 8 over the block)
+#pragma unroll
+          for (int k2 = 0; k2 < TP / 8 / NW / 2 + 1; ++k2) {
+            const int k = w + NW * (2 * k2 + xb);
+            if (k < TP / 8) dma_rows3(k);
+          }
+        }
+      }
+      // 3. dv from z and σ: tanh = z/σ (σ = 0 only where dv is 0 anyway)
+      floatx4 dvs[2], dvg[2];
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float zz = zr[bb][e], sg = sgr[bb][e];
+          const float th = sg > 1e-30f ? zz * __builtin_amdgcn_rcpf(sg) : 0.f;
+          dvs[bb][e] = dz[bb][e] * sg * (1.f - th * th);
+          dvg[bb][e] = dz[bb][e] * zz * (1.f - sg);
+        }
+      {
+        float* dvo = (a.dv_out && valid) ? a.dv_out + m * a.lddv + (long)l * 64 : nullptr;
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+          const int c = 8 * (q0 + bb) + 4 * h;
+          *(floatx4*)(DVs + r * XS + c) = dvs[bb];
+          *(floatx4*)(DVg + r * XS + c) = dvg[bb];
+          if (dvo) {
+            *(floatx4*)(dvo + c) = dvs[bb];
+            *(floatx4*)(dvo + 32 + c) = dvg[bb];
+          }
+        }
+      }
+      XSTAMP(2);
+      // 4. dx on the bf16 cores: out_a = g + W1·dv, out_c0 = W0·dv (k-steps S = 0 sig, 1 gate)
+      floatx4 acc_a[2] = {gv[0], gv[1]}, acc_c[2];
+      acc_c[0] = acc_c[1] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int S = 0; S < 2; ++S) {
+        bf16x8 fa[2][3], fc[2][3];
+#pragma unroll
+        for (int xb = 0; xb < 2; ++xb)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            fa[xb][p] = *(const bf16x8*)(WD + (32 + 16 * xb + i16) * XW_ROW + 64 * p + 32 * S + 8 * g);
+            fc[xb][p] = *(const bf16x8*)(WD + (16 * xb + i16) * XW_ROW + 64 * p + 32 * S + 8 * g);
+          }
+        bf16x8 bx[3];
+        if (S == 0) split8(dvs[0], dvs[1], bx);
+        else split8(dvg[0], dvg[1], bx);
+#pragma unroll
+        for (int xb = 0; xb < 2; ++xb) {
+          acc_a[xb] = mfma16x3(fa[xb], bx, acc_a[xb]);
+          acc_c[xb] = mfma16x3(fc[xb], bx, acc_c[xb]);
+        }
+      }
+      {
+        const __amdgpu_buffer_rsrc_t rw =
+            __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)l * a.ocls, (short)0, oc_bytes, BUF_DW3);
+        const bool pub = l > 0 && valid && r < min(d, TP);
+#pragma unroll
+        for (int xb = 0; xb < 2; ++xb) {
+          *(floatx4*)(OC + r * XS + 16 * xb + 4 * g) = acc_c[xb];
+          if (pub) __builtin_amdgcn_raw_buffer_store_b128(acc_c[xb], rw, (int)((m * 32 + 16 * xb + 4 * g) * 4), 0, 16);
+        }
+      }
+      if (l == 0 && valid) {
+#pragma unroll
+        for (int xb = 0; xb < 2; ++xb) {
+          *(floatx4*)(a.dx0_a + m * 32 + 16 * xb + 4 * g) = acc_a[xb];
+          *(floatx4*)(a.dx0_c + m * 32 + 16 * xb + 4 * g) = acc_c[xb];
+        }
+      }
+      oa[0] = acc_a[0];
+      oa[1] = acc_a[1];
+      XSTAMP(3);
+      // 5. publish out_c0_l (the drain also lands this layer's x / z DMA pieces)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // DV, G, OC, Xp/Xc/ZT complete; the weight image is dead
+      if (tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
+      if (a.gc_dtab && !tile_uni) gc_scatter16(a.gc_dtab + (long)l * 64, a.gc_ld, DVs, DVg, w, lane, 32, gc_starts, gc_pid);
+      XSTAMP(4);
+      // 6. dSIG / dGATE tile t4 = w & 3 (2·kind + tap) over this wave's position half:
+      //    A[i = in][k = pos] = X_tap[pos][in], B[k = pos][j = o] = DV_kind[pos][o]
+      const int t4 = w & 3, p0 = (w >> 2) * PH;
+      floatx16 accT;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) accT[q] = 0.f;
+      {
+        const float* XA = (t4 & 1) ? Xc : Xp;
+        const float* DB = (t4 & 2) ? DVg : DVs;
+        const int pi = lane & 31, hh = lane >> 5;
+        float xa[PH / 16][8], db[PH / 16][8];
+#pragma unroll
+        for (int s2 = 0; s2 < PH / 16; ++s2)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int p = p0 + 16 * s2 + 8 * hh + e;
+            xa[s2][e] = XA[p * 32 + pi];
+            db[s2][e] = DB[p * XS + pi];
+          }
+        XSTAMP(8);
+        if (l > 0) {   // the next layer's image and rows, behind this layer's operand reads
+          dma_image(l - 1);
+          load_regs(l - 1);
+        }
+        XSTAMP(9);
+#pragma unroll
+        for (int s2 = 0; s2 < PH / 16; ++s2) {
+          bf16x8 fx[3], fd[3];
+          split8(floatx4{xa[s2][0], xa[s2][1], xa[s2][2], xa[s2][3]}, floatx4{xa[s2][4], xa[s2][5], xa[s2][6], xa[s2][7]}, fx);
+          split8(floatx4{db[s2][0], db[s2][1], db[s2][2], db[s2][3]}, floatx4{db[s2][4], db[s2][5], db[s2][6], db[s2][7]}, fd);
+          accT = mfma_x3(fx, fd, accT);
+        }
+      }
+      XSTAMP(5);
+      // 7. dRES quarter t4 (16x16: z channels 16(t4>>1).., res out 16(t4&1)..) over the same
+      //    positions on v_mfma_f32_16x16x4_f32: A[i=c][k=pos] = z[pos][c], B[k=pos][j=o] = g[pos][o]
+      floatx4 accR = {0.f, 0.f, 0.f, 0.f};
+      {
+        const int cz = 16 * (t4 >> 1) + i16, og = 16 * (t4 & 1) + i16;
+#pragma unroll
+        for (int c8 = 0; c8 < PH / 32; ++c8) {
+          float za[8], ga[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int p = p0 + 32 * c8 + 4 * e + g;
+            za[e] = ZT[p * 32 + cz];
+            ga[e] = G[p * XS + og];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) accR = __builtin_amdgcn_mfma_f32_16x16x4f32(za[e], ga[e], accR, 0, 0, 0);
+        }
+      }
+      XSTAMP(11);
+      // 8. bias partials (column sums of DVs, DVg, G: waves 0-2; lane = (row class pc, 4-column
+      //    group c4), rows pc + 8p)
+      float* slab = a.slab + ((long)l * ntiles + tile) * SLAB;
+      if (w < 3) {
+        const int c4 = (lane & 7) * 4, pc = lane >> 3;
+        const float* pl = w == 0 ? DVs : w == 1 ? DVg : G;
+        floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < TP / 8; ++p) s4 += *(const floatx4*)(pl + (pc + 8 * p) * XS + c4);
+        *(floatx4*)(part + pc * 96 + 32 * w + c4) = s4;
+      }
+      __syncthreads();   // every read of Xp/Xc/ZT/DV/G of this layer is done; part complete
+      if (tid < 96) {
+        float s1 = 0.f;
+#pragma unroll
+        for (int pc = 0; pc < 8; ++pc) s1 += part[pc * 96 + tid];
+        slab[5120 + tid] = s1;
+      }
+      XSTAMP(12);
+      // weight-gradient partials to the slab: with two position halves, each wave parks its
+      // partials lane-linear in Xp.. (dead until the next layer's G-build barrier) and waves 0-3
+      // sum halves 0 + 1 of their tile / quarter in a fixed order
+      if (NH == 1) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) slab[t4 * 1024 + acc_row(q, lane >> 5) * 32 + (lane & 31)] = accT[q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) slab[4096 + (16 * (t4 >> 1) + 4 * g + q) * 32 + 16 * (t4 & 1) + i16] = accR[q];
+      } else {
+        float* SCR = Xp + w * 1280;
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4)
+          *(floatx4*)(SCR + (q4 * 64 + lane) * 4) = floatx4{accT[4 * q4], accT[4 * q4 + 1], accT[4 * q4 + 2], accT[4 * q4 + 3]};
+        *(floatx4*)(SCR + 1024 + lane * 4) = accR;
+        __syncthreads();
+        XSTAMP(13);
+        if (w < 4) {
+          const float* S0 = Xp + w * 1280;
+          const float* S1 = Xp + (w + 4) * 1280;
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) {
+            const floatx4 v = *(const floatx4*)(S0 + (q4 * 64 + lane) * 4) + *(const floatx4*)(S1 + (q4 * 64 + lane) * 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) slab[w * 1024 + acc_row(4 * q4 + e, lane >> 5) * 32 + (lane & 31)] = v[e];
+          }
+          const floatx4 v = *(const floatx4*)(S0 + 1024 + lane * 4) + *(const floatx4*)(S1 + 1024 + lane * 4);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) slab[4096 + (16 * (w >> 1) + 4 * g + q) * 32 + 16 * (w & 1) + i16] = v[q];
+        }
+      }
+      XSTAMP(6);
+    }
+#undef XSTAMP
+  }
+}
+
 // Sum every layer's slab partials: grid (column groups, L).
 __global__ __launch_bounds__(256) void layer_reduce_all_kernel(RedK a, long slab_layer, long dsig_l, long dres_l,
                                                                long db_l) {
@@ -2693,13 +3070,22 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   const bool x3 = c.bimg && c.SG && c.Z;
   if (x3) LBWN_REQUIRE((((uintptr_t)c.bimg) & 15) == 0 && (((uintptr_t)c.SG) & 15) == 0 && (c.ldz & 3) == 0,
                        "chain bwd x3: misaligned images / rows");
-  const int tps = (c.T + LP - 1) / LP;
+  LBWN_REQUIRE(c.bwd_nw == 0 || ((c.bwd_nw == 4 || c.bwd_nw == 8) && x3),
+               "chain bwd: 16-position waves need the bf16-split form, 4 or 8 waves");
+  const int tp = lbwn_chain_fwd_tile(c.bwd_nw);
+  const int tps = (c.T + tp - 1) / tp;
   // hand-off flags only: the status word is sticky for the whole step
   if (!c.flags_zeroed) {
     if (int e = lbwn_zero_launch(c.flags, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st)) return e;
   }
   LBWN_REQUIRE(x3 == (c.dzls > 0), "chain bwd: the bf16-split chain reads dZ in chain order (dzls), the f32 chain in rows");
-  if (x3 && k.trace) chain_bwd_x3_kernel<true><<<c.grid, 256, 0, st>>>(k);
+  if (c.bwd_nw == 8) {
+    if (k.trace) chain_bwd16_kernel<8, true><<<c.grid, 512, 0, st>>>(k);
+    else chain_bwd16_kernel<8, false><<<c.grid, 512, 0, st>>>(k);
+  } else if (c.bwd_nw == 4) {
+    if (k.trace) chain_bwd16_kernel<4, true><<<c.grid, 256, 0, st>>>(k);
+    else chain_bwd16_kernel<4, false><<<c.grid, 256, 0, st>>>(k);
+  } else if (x3 && k.trace) chain_bwd_x3_kernel<true><<<c.grid, 256, 0, st>>>(k);
   else if (x3) chain_bwd_x3_kernel<false><<<c.grid, 256, 0, st>>>(k);
   else chain_bwd_kernel<<<c.grid, 256, 0, st>>>(k);
   LBWN_CHECK_LAUNCH();

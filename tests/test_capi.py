@@ -72,3 +72,22 @@ def test_torch_ops_registered_device_only():
         z, xo = torch.ops.lbwn.dilconv_gate(xf, wf, wf, torch.empty(16, device='cuda'), torch.empty(16, device='cuda'),
                                             torch.empty(16, 32, device='cuda'), torch.empty(32, device='cuda'), 4, 4)
         assert tuple(z.shape) == (2, 100, 16) and tuple(xo.shape) == (2, 100, 32)
+
+
+def test_plan_chain_tile_env(monkeypatch):
+    """LBWN_CHAIN_TILE = <fwd>[:<bwd>] (each 128 / 64 / w32) selects the chains' form at plan
+    creation; anything else is refused there (EINVAL), before any device work."""
+    import ctypes
+    from lbwn import _lib
+    lib = _lib.load()
+    a = _lib.Arch()
+    a.n_blocks, a.n_block_layers, a.n_quant, a.n_res, a.n_dil, a.n_skip, a.n_post = 5, 10, 256, 32, 32, 512, 512
+    h = ctypes.c_void_p()
+    for v in ('128', '64', 'w32', '128:w32', 'w32:64', ''):
+        monkeypatch.setenv('LBWN_CHAIN_TILE', v)
+        assert lib.lbwn_plan_create(ctypes.byref(a), 8, 4096, ctypes.byref(h)) == 0, v
+        lib.lbwn_plan_destroy(h)
+    for v in ('96', '128:', ':64', '128:64:w32', 'w16'):
+        monkeypatch.setenv('LBWN_CHAIN_TILE', v)
+        assert lib.lbwn_plan_create(ctypes.byref(a), 8, 4096, ctypes.byref(h)) == 22, v
+        assert b'LBWN_CHAIN_TILE' in lib.lbwn_last_error()

@@ -3,9 +3,9 @@
 set -o pipefail
 mkdir -p gpurun_out
 TAG=${1:-t}
-K=${2:+-k "$2"}
-eval timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $K \
-  > gpurun_out/pytest_$TAG.log 2>&1
+ARGS=(tests -m gpu -x -v --timeout 300 --timeout-method thread)
+[ -n "$2" ] && ARGS+=(-k "$2")
+timeout -k 10 900 python -u -m pytest "${ARGS[@]}" > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?
 tail -30 gpurun_out/pytest_$TAG.log
 exit $rc
