@@ -443,9 +443,10 @@ class TrainBench:
         torch.cuda.empty_cache()
 
 
-FWD_TILES = {'128': dict(positions=128, waves=8, waves_per_simd=2, kernel='chain_fwd16_kernel<8>'),
-             '64': dict(positions=64, waves=4, waves_per_simd=1, kernel='chain_fwd16_kernel<4>'),
-             'w32': dict(positions=128, waves=4, waves_per_simd=1, kernel='chain_fwd_kernel (32-position waves)')}
+FWD_TILES = {'128': dict(positions=128, waves=8, waves_per_simd=2, kernel='chain_fwd16_kernel<8> / chain_bwd16_kernel<8>'),
+             '64': dict(positions=64, waves=4, waves_per_simd=1, kernel='chain_fwd16_kernel<4> / chain_bwd16_kernel<4>'),
+             'w32': dict(positions=128, waves=4, waves_per_simd=1,
+                         kernel='chain_fwd_kernel / chain_bwd_x3_kernel (32-position waves)')}
 
 
 def chain_dilation_sweep(arch_file, B, T, dp, steps=4, gc=None, tile=None):
@@ -454,8 +455,8 @@ def chain_dilation_sweep(arch_file, B, T, dp, steps=4, gc=None, tile=None):
     64-position tiles, 'w32' = 32-position waves on 128), the timed step and the in-kernel clock
     stamps of one chain block's tile (LBWN_CHAIN_TRACE), which give each layer's start-to-start
     time in the forward and the backward chain; layers grouped by dilation d = 2^bl
-    (tmodel.py:313-325), median over the n_blocks layers of each d and over steps.  The backward
-    chain keeps its 128-position tile (32-position waves) in every row."""
+    (tmodel.py:313-325), median over the n_blocks layers of each d and over steps.  The tile
+    applies to both chains (chain_fwd16_kernel / chain_bwd16_kernel, or the w32 pair)."""
     import torch
     from lbwn.arch import load_arch, n_layers
     arch = load_arch(arch_file, num_global_cond=gc)
@@ -500,13 +501,14 @@ def chain_dilation_sweep(arch_file, B, T, dp, steps=4, gc=None, tile=None):
     info = FWD_TILES.get(t, {})
     return {'tile': t, 'fwd_tile_positions': info.get('positions'), 'fwd_waves_per_block': info.get('waves'),
             'fwd_waves_per_simd': info.get('waves_per_simd'), 'fwd_kernel': info.get('kernel'),
-            'bwd_tile_positions': 128, 'tile_channels': 32, 'blocks_per_cu': 1, 'ms_per_step': ms,
+            'bwd_tile_positions': info.get('positions'), 'tile_channels': 32, 'blocks_per_cu': 1,
+            'ms_per_step': ms,
             'clock': 'clock64 cycles, us at 2.4 GHz', 'traced_block': 1, 'per_dilation': rows,
             'note': 'per-layer start-to-start time of one chain block (its first tile), median over the '
                     'n_blocks layers of each dilation and %d steps; ms_per_step: 5 timed steps' % steps}
 
 
-DEFAULT_TILE = 'w32'    # the library's default forward chain form (engine.cpp, LBWN_CHAIN_TILE unset)
+DEFAULT_TILE = '128'    # the library's default chain form (engine.cpp, LBWN_CHAIN_TILE unset)
 
 
 CANDS = ['layer_bwd', 'dskip', 'layer_fwd', 'post1_fwd', 'dpost1', 'ds', 'post2_fwd', 'dpost2', 'dh']

@@ -53,10 +53,10 @@ struct lbwn_plan {
   bool chain = false;            // persistent layer-chain kernels (n_res = n_dil = 32)
   int chain_grid = 0;            // resident blocks for the chain (set on first use)
   int fwd_grid = 0;              // ... for the forward chain (its tile: lbwn_chain_fwd_tile(fwd_nw))
-  // chain forms (LBWN_CHAIN_TILE = <fwd>[:<bwd>] at plan creation, each 128 / 64 / w32): 0 =
-  // 32-position waves on 128-position tiles (chain_fwd_kernel / chain_bwd_x3_kernel), 8 / 4 =
-  // 16-position waves on 128- / 64-position tiles (chain_fwd16_kernel / chain_bwd16_kernel)
-  int fwd_nw = 0, bwd_nw = 0;
+  // chain forms (LBWN_CHAIN_TILE = <fwd>[:<bwd>] at plan creation, each 128 / 64 / w32; default
+  // 128): 0 = 32-position waves on 128-position tiles (chain_fwd_kernel / chain_bwd_x3_kernel),
+  // 8 / 4 = 16-position waves on 128- / 64-position tiles (chain_fwd16_kernel / chain_bwd16_kernel)
+  int fwd_nw = 8, bwd_nw = 8;
   int bwd_grid = 0;
   // Backward side stream (chain plans): the head weight gradients (dPOST2, dPOST1) run on the
   // main stream before the chain; dSKIP follows the chain on the main stream while `aux2` runs
@@ -280,7 +280,9 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     LBWN_REQUIRE(T % hop == 0, "plan: slice_sz %d is not a multiple of the mel hop %d", T, hop);
     LBWN_REQUIRE(a->n_lc_in % 4 == 0 && a->n_lc_out % 4 == 0, "plan: n_lc_in/n_lc_out must be multiples of 4");
   }
-  int fwd_nw = 0, bwd_nw = 0;   // chain forms (lbwn_plan::fwd_nw)
+  // chain forms (lbwn_plan::fwd_nw): default 16-position waves on 128-position tiles (same-box A/B,
+  // profiles/r04_ab_chain16_tiles.txt: arch3 forward chain 278 -> 241 us, backward 492 -> 419 us)
+  int fwd_nw = 8, bwd_nw = 8;
   {
     const char* tv = getenv("LBWN_CHAIN_TILE");
     auto form = [](const char* v, size_t n, int* nw) {

@@ -2513,6 +2513,7 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
           split8(floatx4{xa[s2][0], xa[s2][1], xa[s2][2], xa[s2][3]}, floatx4{xa[s2][4], xa[s2][5], xa[s2][6], xa[s2][7]}, fx);
           split8(floatx4{db[s2][0], db[s2][1], db[s2][2], db[s2][3]}, floatx4{db[s2][4], db[s2][5], db[s2][6], db[s2][7]}, fd);
           accT = mfma_x3(fx, fd, accT);
+          if (s2 == 0) XSTAMP(10);
         }
       }
       XSTAMP(5);

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round-4 measurement pass: GPU tests, smoke, the bench line, rocprof kernel stats + one step's
+# timeline, chain traces, PMC traffic and request sizes.  Usage: bash tools/gpu_r4_full.sh TAG [skip-tests]
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${1:-r4}
+if [ "$2" != "skip-tests" ]; then
+  bash tools/gpu_tests.sh $TAG || exit 1
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { tail -5 gpurun_out/smoke_$TAG.log; exit 1; }
+fi
+timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -20 gpurun_out/bench_$TAG.err; exit 1; }
+echo bench ok
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python bench.py --steps 10 --no-gen --no-cpu-baseline --no-extras > gpurun_out/prof_$TAG.log 2>&1 || exit 1
+S=$(find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1)
+python tools/prof_summary.py "$S" gpurun_out/stats_$TAG.md 20 $TAG
+K=$(find gpurun_out/prof_$TAG -name '*kernel_trace.csv' | head -1)
+python tools/step_timeline.py "$K" > gpurun_out/timeline_$TAG.txt 2>&1
+timeout -k 10 120 python tools/chain_trace.py > gpurun_out/chaintrace_$TAG.txt 2>&1 || exit 1
+bash tools/pmc_traffic.sh > gpurun_out/pmc_traffic_$TAG.log 2>&1 || exit 1
+bash tools/pmc_req.sh > gpurun_out/pmc_req_$TAG.log 2>&1 || exit 1
+echo full ok

@@ -12,6 +12,7 @@ import sys
 
 GEMM_ORDER = ['skip_fwd', 'post1_fwd', 'post2_fwd', 'dh', 'ds', 'dz', 'dpost2', 'dpost1', 'dskip']
 NAMED = {'chain_fwd_kernel': 'layer_fwd', 'chain_bwd_kernel': 'layer_bwd', 'chain_bwd_x3_kernel': 'layer_bwd',
+         'chain_fwd16_kernel': 'layer_fwd', 'chain_bwd16_kernel': 'layer_bwd',
          'head_kernel': 'head', 'head_reg_kernel': 'head',
          'layer_reduce_all_kernel': 'layer_reduce', 'pre_grad_part_kernel': 'dpre'}
 
