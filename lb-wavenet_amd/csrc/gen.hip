@@ -990,70 +990,55 @@ LBWN_DEV void persist_head(const PersistK& a, int m, float* sm, int b0, int B, l
     }
     __syncthreads();
     if (tr && s == n - 1) tr[3] = wall_clock64();
-    // C. post1 partial over rows 16kg..16kg+15 of column hcol, 4 streams at a time (independent
-    //    chains), the 32 row groups summed through LDS
+    // C. h = relu(relu(skip + Σb)·POST1[:, cols] + b1) for this block's 16 columns and all 16
+    //    stream slots on v_mfma_f32_16x16x4_f32 (exact f32 products): wave wv takes K rows
+    //    64wv .. 64wv+63 (16 MFMAs; A[i = stream][k] = RS, B[k][j = column] = P1T), the eight
+    //    16x16 partials are summed through LDS in a fixed order.  (Round 3's per-thread FMA form
+    //    re-read each RS row for all 16 columns: ~390 KB of LDS reads, ~1.1 us.)
     {
-      floatx4 w4[4];
+      const int i16 = lane & 15, kk = lane >> 4, k0 = 64 * wv;
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      float av[16], bv[16];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) w4[q] = *(const floatx4*)(P1T + c * 516 + 16 * kg + 4 * q);
-      for (int g0 = 0; g0 < B; g0 += 4) {
-        floatx4 x[4][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) x[j][q] = *(const floatx4*)(RS + min(g0 + j, P_MAXB - 1) * 512 + 16 * kg + 4 * q);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float pp = 0.f;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            pp = fmaf(x[j][q][0], w4[q][0], pp);
-            pp = fmaf(x[j][q][1], w4[q][1], pp);
-            pp = fmaf(x[j][q][2], w4[q][2], pp);
-            pp = fmaf(x[j][q][3], w4[q][3], pp);
-          }
-          if (g0 + j < B) HP[(kg * 16 + g0 + j) * 16 + c] = pp;
-        }
+      for (int s4 = 0; s4 < 16; ++s4) {
+        av[s4] = RS[i16 * 512 + k0 + 4 * s4 + kk];
+        bv[s4] = P1T[i16 * 516 + k0 + 4 * s4 + kk];
       }
+#pragma unroll
+      for (int s4 = 0; s4 < 16; ++s4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s4], bv[s4], acc, 0, 0, 0);
+      *(floatx4*)(HP + (wv * 64 + lane) * 4) = acc;   // lane-linear: D[4kk + e][i16]
     }
     if (tr && s == n - 1) tr[8 + L + 120] = wall_clock64();
     __syncthreads();
     if (tr && s == n - 1) tr[8 + L + 121] = wall_clock64();
-    {
-      const int sb = tid >> 4;
-      if (sb < B) {
-        float v[32], h = 0.f;
+    if (tid < 256) {   // (stream 4·(tid>>6... : element (lane l = tid & 63, e = tid >> 6) of every wave's D
+      const int l = tid & 63, e = tid >> 6, sb = 4 * (l >> 4) + e, cc = l & 15;
+      float v[8], hsum = 0.f;
 #pragma unroll
-        for (int g = 0; g < 32; ++g) v[g] = HP[(g * 16 + sb) * 16 + c];
+      for (int g = 0; g < 8; ++g) v[g] = HP[(g * 64 + l) * 4 + e];
 #pragma unroll
-        for (int g = 0; g < 32; ++g) h += v[g];
-        HS[sb * 16 + c] = hcol < Cp ? fmaxf(h + b1, 0.f) : 0.f;
-      }
+      for (int g = 0; g < 8; ++g) hsum += v[g];
+      const float b1c = (m * 16 + cc < Cp && a.post1_b) ? a.post1_b[m * 16 + cc] : 0.f;
+      HS[sb * 16 + cc] = (m * 16 + cc < Cp) ? fmaxf(hsum + b1c, 0.f) : 0.f;
     }
     __syncthreads();
     if (tr && s == n - 1) tr[8 + L + 122] = wall_clock64();
-    // partial logits over this block's 16 h rows: column q = tid, 4 streams at a time
-    if (tid < Q) {
-      float p2[16];
+    // partial logits over this block's 16 h rows: 16 code columns per MFMA block, blocks wv and
+    // wv + 8 of the Q/16: A[i = stream][k = r] = HS, B[k][j = code] = P2S; lane (code, 4 streams)
+    {
+      const int i16 = lane & 15, kk = lane >> 4;
+      float av[4];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) p2[r] = P2S[r * Q + tid];
-      for (int g0 = 0; g0 < B; g0 += 4) {
-        floatx4 hv[4][4];
+      for (int s4 = 0; s4 < 4; ++s4) av[s4] = HS[i16 * 16 + 4 * s4 + kk];
+      for (int qb = wv; qb < (Q + 15) / 16; qb += 8) {
+        const int q = min(16 * qb + i16, Q - 1);
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s4], P2S[(4 * s4 + kk) * Q + q], acc, 0, 0, 0);
+        if (16 * qb + i16 < Q) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) hv[j][q] = *(const floatx4*)(HS + min(g0 + j, P_MAXB - 1) * 16 + 4 * q);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float lp = 0.f;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            lp = fmaf(hv[j][q][0], p2[4 * q], lp);
-            lp = fmaf(hv[j][q][1], p2[4 * q + 1], lp);
-            lp = fmaf(hv[j][q][2], p2[4 * q + 2], lp);
-            lp = fmaf(hv[j][q][3], p2[4 * q + 3], lp);
-          }
-          if (g0 + j < B) put_granule(a.lg + ((long)m * a.B + b0 + g0 + j) * Q + tid, tag, lp);
+          for (int e = 0; e < 4; ++e)
+            if (4 * kk + e < B) put_granule(a.lg + ((long)m * a.B + b0 + 4 * kk + e) * Q + q, tag, acc[e]);
         }
       }
     }

@@ -2247,6 +2247,16 @@ constexpr int cb16_lds() { return BIMG_F + 3 * 16 * NW * 32 + 4 * 16 * NW * XS +
 static_assert(cb16_lds<8>() * 4 + 16 <= 160 * 1024, "chain bwd16 LDS");
 static_assert(8 * 1280 <= 3 * 128 * 32, "bwd16: the partial scratch must fit in Xp | Xc | ZT");
 
+// Σ over the 16 lanes of a DPP row (lanes 16k .. 16k+15): quad xor 1, xor 2, half-row mirror, row
+// mirror; every lane of the row ends with the row total (a fixed tree: deterministic)
+LBWN_DEV float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, true));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, true));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, true));
+  return v;
+}
+
 // GC rows of a wave whose 16 positions are not one voice: dv column sums per run of equal ids,
 // one atomic per run and column (as gc_scatter_x3, 16 positions)
 LBWN_DEV void gc_scatter16(float* gtab, long ld, const float* DVs, const float* DVg, int w, int lane, int Cd,
@@ -2433,6 +2443,30 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
           }
         }
       }
+      // bias partials: column sums of dv (sig, gate) and g over this wave's 16 positions from the
+      // lanes' own registers (DPP row sums across the 16 position lanes), one part per wave, read
+      // after step 8's barrier (waves 0-2 re-reading 128 LDS rows each there, with the others
+      // idle at the barrier, took ~3k cycles per layer)
+      {
+        floatx4 ss[2], sgt[2], sx[2];
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            ss[bb][e] = row16_sum(dvs[bb][e]);
+            sgt[bb][e] = row16_sum(dvg[bb][e]);
+            sx[bb][e] = row16_sum(gv[bb][e]);
+          }
+        if (i16 == 0) {
+          float* pw = part + w * 96;
+#pragma unroll
+          for (int bb = 0; bb < 2; ++bb) {
+            *(floatx4*)(pw + 8 * (q0 + bb) + 4 * h) = ss[bb];
+            *(floatx4*)(pw + 32 + 8 * (q0 + bb) + 4 * h) = sgt[bb];
+            *(floatx4*)(pw + 64 + 16 * bb + 4 * g) = sx[bb];
+          }
+        }
+      }
       XSTAMP(2);
       // 4. dx on the bf16 cores: out_a = g + W1·dv, out_c0 = W0·dv (k-steps S = 0 sig, 1 gate)
       floatx4 acc_a[2] = {gv[0], gv[1]}, acc_c[2];
@@ -2537,22 +2571,13 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         }
       }
       XSTAMP(11);
-      // 8. bias partials (column sums of DVs, DVg, G: waves 0-2; lane = (row class pc, 4-column
-      //    group c4), rows pc + 8p)
+      // 8. bias partials: the per-wave column sums were parked in part (step 3)
       float* slab = a.slab + ((long)l * ntiles + tile) * SLAB;
-      if (w < 3) {
-        const int c4 = (lane & 7) * 4, pc = lane >> 3;
-        const float* pl = w == 0 ? DVs : w == 1 ? DVg : G;
-        floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int p = 0; p < TP / 8; ++p) s4 += *(const floatx4*)(pl + (pc + 8 * p) * XS + c4);
-        *(floatx4*)(part + pc * 96 + 32 * w + c4) = s4;
-      }
       __syncthreads();   // every read of Xp/Xc/ZT/DV/G of this layer is done; part complete
       if (tid < 96) {
         float s1 = 0.f;
 #pragma unroll
-        for (int pc = 0; pc < 8; ++pc) s1 += part[pc * 96 + tid];
+        for (int pw = 0; pw < NW; ++pw) s1 += part[pw * 96 + tid];
         slab[5120 + tid] = s1;
       }
       XSTAMP(12);
