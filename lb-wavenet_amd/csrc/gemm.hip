@@ -788,9 +788,18 @@ __global__ __launch_bounds__(512, 1) void gemm_x3r_kernel(lbwn_gemm_args g) {
 // l = (r = l & 15, q = l >> 4) supplies A[16mi + r][8q + j] (one 32-B run of a row per mi: a row's
 // four lanes cover its 128-B line) and B[8q + j][16ni + r]; the k-step runs as two halves of 4
 // column blocks.
-template <int NB>   // 16-column blocks: 8 (128 columns) or 6 (96: N <= 96, arch5's dlc)
+// LBWN_GEMM_WIDE=0 keeps dZ on 128-column tiles (same-box A/B switch)
+static bool lbwn_gemm_wide_tiles() {
+  static const int v = [] { const char* e = getenv("LBWN_GEMM_WIDE"); return (e && e[0] == '0') ? 0 : 1; }();
+  return v != 0;
+}
+
+template <int NB>   // 16-column blocks: 8 (128 columns), 10 (160: dZ's N = 1600) or 6 (96: N <= 96, arch5's dlc)
 __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
-  constexpr int NTHR = 512, BM = 256, BN = 16 * NB, NH = NB / 2;
+  // the k-step's column blocks run in NP parts of NH (B fragments live for one part: NB = 10 in
+  // two parts of 5 spilled 32 VGPRs)
+  constexpr int NP = NB == 10 ? 5 : 2;
+  constexpr int NTHR = 512, BM = 256, BN = 16 * NB, NH = NB / NP;
   constexpr int SLOT = BN * X3_ROW;
   __shared__ __attribute__((aligned(16))) unsigned short smem[2 * SLOT];
 
@@ -879,8 +888,11 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
     a_load(std::integral_constant<int, S>(), min(kt + 3, last));
     sp.template store<S>(nxt);
     sp.template load<S>(min(kt + 3, last));
-    b_frags(cur, 1, fb);
-    mfmas(fa, fb, 1);
+#pragma unroll
+    for (int part = 1; part < NP; ++part) {
+      b_frags(cur, part, fb);
+      mfmas(fa, fb, part);
+    }
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -1071,6 +1083,12 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
       grid.x = (unsigned)(((a.M + 255) / 256) * ((a.N + 95) / 96));
       if (X3Q) gemm_x3q_kernel<6><<<grid, 512, 0, st>>>(g);
       else gemm_x3r_kernel<3><<<grid, 512, 0, st>>>(g);
+    } else if (X3Q && a.N % 160 == 0 && a.N > 512 && lbwn_gemm_wide_tiles()) {
+      // N = 1600 (dZ): 160-column tiles, so the grid is whole rounds of 256 blocks (M/256 x 10 at
+      // C2 = 1280 = 5 rounds) instead of 128-column ones (13 column tiles, the last half empty:
+      // 1664 = 6.5 rounds)
+      grid.x = (unsigned)(((a.M + 255) / 256) * (a.N / 160));
+      gemm_x3q_kernel<10><<<grid, 512, 0, st>>>(g);
     } else if (X3Q) {
       gemm_x3q_kernel<8><<<grid, 512, 0, st>>>(g);
     } else {

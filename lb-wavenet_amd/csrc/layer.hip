@@ -443,7 +443,15 @@ struct ChainFK {
   // in-chain LC term (chain_fwd_kernel<true, true>): the upsampled LC input [M][Lo] and the L
   // split LC images (LCIMG_US bf16 each)
   const float* lcact; const unsigned short* lcimg; int Lo;
+  // granule hand-off (chain_fwd16_kernel<..., GR>): halo rows of x_l as {value, tag} words
+  // [L][ntiles][TP][32], tag = epoch·1024 + l (lbwn_chain_epoch, advanced once per step)
+  unsigned long long* hog;
 };
+
+// Step epoch of the granule hand-offs: advanced by lbwn_step_begin_launch at every training step's
+// start (stream-ordered, so a captured graph replays it too); module-scope device state, one per
+// device, monotonic in the process
+__device__ unsigned lbwn_chain_epoch;
 
 // lc·[LC_SIGNAL_l | LC_GATE_l] onto the accumulators (tmodel.py:155-160): A = the layer's LC
 // image rows (out channel), B = this lane's LC input row, pre-split once per tile (lcb); the
@@ -1037,7 +1045,9 @@ template <int NW>
 constexpr int cf16_lds(bool lc) { return 3 * 16 * NW * XS + 2 * XIMG_F + (lc ? LC16IMG_F : 0); }
 static_assert(cf16_lds<8>(true) * 4 + 16 <= 160 * 1024, "chain fwd16 + LC LDS");
 
-template <int NW, bool LC, int CM, bool TR>
+// GR: halo rows cross tiles as tagged granules (8-B {value, tag} stores, polled by the consumer)
+// instead of sc1 rows + drain + barrier + flag: the producer's halo is out as soon as its stores land
+template <int NW, bool LC, int CM, bool TR, bool GR>
 __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
   constexpr int TP = 16 * NW, NT = 64 * NW;
   constexpr int IMGF = XIMG_F;
@@ -1061,6 +1071,7 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
   const int i16 = lane & 15, g = lane >> 4, q0 = 2 * (g >> 1), h = g & 1;
   const int r = 16 * w + i16;  // this lane's row of the tile
   const int tps = (a.T + TP - 1) / TP, ntiles = a.B * tps;
+  const unsigned ep1024 = GR ? lbwn_chain_epoch * 1024u : 0u;
   if (tid == 0) s_fail = 0;
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int b = tile / tps, tt = tile % tps, t0 = tt * TP;
@@ -1141,7 +1152,8 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
       FSTAMP(1);
       // wait for the producer of the halo rows
       const int ptt = tt - max(1, d / TP);
-      if (l > 0 && ptt >= 0) {
+      const bool handoff = l > 0 && ptt >= 0;
+      if (!GR && handoff) {
         if (tid == 0 && !s_fail) {
           if (!wait_flag_ge(a.flags + (long)b * tps + ptt, (unsigned)l, a.status, 1u)) s_fail = 1;
         }
@@ -1153,10 +1165,43 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc(xl, (short)0, (int)((long)(a.H + a.T) * 32 * 4), BUF_DW3);
         floatx4 hv[NR];
+        if (GR && handoff) {
+          // poll this thread's granules of the producer tile's rows until every tag is layer l's
+          const unsigned tag = ep1024 + (unsigned)l;
+          const unsigned long long* src = a.hog + ((long)l * ntiles + (long)b * tps + ptt) * TP * 32;
+          long long t_start = 0;
+          for (unsigned spins = 1;; ++spins) {
+            bool ok = true;
 #pragma unroll
-        for (int i = 0; i < NR; ++i) {
-          const int e = min(tid + NT * i, nh * 8 - 1), row = e >> 3, c4 = (e & 7) * 4;
-          hv[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((a.H + t0 + row - d) * 32 + c4) * 4, 0, 16);
+            for (int i = 0; i < NR; ++i) {
+              const int e = min(tid + NT * i, nh * 8 - 1), row = e >> 3, c4 = (e & 7) * 4;
+              const int srow = t0 - d + row - ptt * TP;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const unsigned long long x = __hip_atomic_load(src + srow * 32 + c4 + j, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+                hv[i][j] = __uint_as_float((unsigned)x);
+                ok &= (unsigned)(x >> 32) == tag;
+              }
+            }
+            if (ok) break;
+            if ((spins & 15) == 0) {
+              const long long now = wall_clock64();
+              if (t_start == 0) t_start = now;
+              else if (now - t_start > SPIN_TIMEOUT || s_fail) {
+                __hip_atomic_fetch_or((gu32*)a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_fail = 1;
+                break;
+              }
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < NR; ++i) {
+            const int e = min(tid + NT * i, nh * 8 - 1), row = e >> 3, c4 = (e & 7) * 4;
+            hv[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((a.H + t0 + row - d) * 32 + c4) * 4, 0, 16);
+          }
         }
         if (!DMAIMG) {
           const floatx4* src = (const floatx4*)(wsrc + (long)min(l + 2, a.L - 1) * IMGF);
@@ -1212,12 +1257,30 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
             __builtin_amdgcn_make_buffer_rsrc(xn, (short)0, (int)((long)(a.H + a.T) * 32 * 4), BUF_DW3);
         float* nrow = nxt + r * XS;
         const bool halo_row = r >= TP - min(1 << ((l + 1) % a.nbl), TP);
+        if (GR) {
+          // halo rows as tagged granules for the consumer tiles (no drain, no flag), every row plain
+          // into X (read after the launch: backward, SAVE)
+          unsigned long long* dst = a.hog + ((long)(l + 1) * ntiles + tile) * TP * 32 + r * 32;
+          const unsigned long long tg = (unsigned long long)(ep1024 + (unsigned)(l + 1)) << 32;
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
-          *(floatx4*)(nrow + 16 * rb + 4 * g) = accr[rb];
-          const int off = ((a.H + t) * 32 + 16 * rb + 4 * g) * 4;
-          if (valid && halo_row) __builtin_amdgcn_raw_buffer_store_b128(accr[rb], rn, off, 0, 16);
-          if (valid && !halo_row) __builtin_amdgcn_raw_buffer_store_b128(accr[rb], rn, off, 0, 0);
+          for (int rb = 0; rb < 2; ++rb) {
+            *(floatx4*)(nrow + 16 * rb + 4 * g) = accr[rb];
+            if (valid) __builtin_amdgcn_raw_buffer_store_b128(accr[rb], rn, ((a.H + t) * 32 + 16 * rb + 4 * g) * 4, 0, 0);
+            if (valid && halo_row) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                __hip_atomic_store(dst + 16 * rb + 4 * g + j, tg | __float_as_uint(accr[rb][j]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) {
+            *(floatx4*)(nrow + 16 * rb + 4 * g) = accr[rb];
+            const int off = ((a.H + t) * 32 + 16 * rb + 4 * g) * 4;
+            if (valid && halo_row) __builtin_amdgcn_raw_buffer_store_b128(accr[rb], rn, off, 0, 16);
+            if (valid && !halo_row) __builtin_amdgcn_raw_buffer_store_b128(accr[rb], rn, off, 0, 0);
+          }
         }
         FSTAMP(8);
         // the next layer's own tap from the row this wave's lanes just wrote (wave-local)
@@ -1229,12 +1292,14 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
         if (LC) lc16_terms(LCIu, lcv, i16, g, acc);
       }
       FSTAMP(5);
-      // publish x_{l+1}: every wave drains its stores, barrier, one lane signals
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // publish x_{l+1}: every wave drains its stores, barrier, one lane signals (GR: the granules
+      // are the hand-off; the barrier only retires this layer's reads of IMG[l&1] / LC before
+      // they are overwritten, and the drain only lands the LDS-DMA pieces / image prefetch)
+      if (!GR || DMAIMG || LC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       FSTAMP(9);
       __syncthreads();
       FSTAMP(10);
-      if (tid == 0 && l + 1 < a.L) publish_flag(a.flags + tile, (unsigned)(l + 1));
+      if (!GR && tid == 0 && l + 1 < a.L) publish_flag(a.flags + tile, (unsigned)(l + 1));
       if (LC && l + 2 < a.L) dma_lc16_image<NW>(a.lcimg, l + 2, LCI, w, lane);
       if (DMAIMG && l + 2 < a.L) {
         const float* src = wsrc + (long)(l + 2) * IMGF + lane * 4;
@@ -3022,15 +3087,20 @@ static void fwd_launch(bool traced, void (*plain)(ChainFK), void (*traced_k)(Cha
 }
 
 // the 16-position-wave forward chain of NW waves (64·NW threads), by LC / conditioning mode
+template <int NW, bool GR>
+static void launch_fwd16_g(bool tr, bool lc, int cm, int grid, const ChainFK& k, hipStream_t st) {
+  void (*f)(ChainFK);
+  if (lc) f = cm == 0 ? (tr ? chain_fwd16_kernel<NW, true, 0, true, GR> : chain_fwd16_kernel<NW, true, 0, false, GR>)
+                      : (tr ? chain_fwd16_kernel<NW, true, 1, true, GR> : chain_fwd16_kernel<NW, true, 1, false, GR>);
+  else if (cm == 0) f = tr ? chain_fwd16_kernel<NW, false, 0, true, GR> : chain_fwd16_kernel<NW, false, 0, false, GR>;
+  else if (cm == 1) f = tr ? chain_fwd16_kernel<NW, false, 1, true, GR> : chain_fwd16_kernel<NW, false, 1, false, GR>;
+  else f = tr ? chain_fwd16_kernel<NW, false, 2, true, GR> : chain_fwd16_kernel<NW, false, 2, false, GR>;
+  hipLaunchKernelGGL(f, dim3(grid), dim3(64 * NW), 0, st, k);
+}
 template <int NW>
 static void launch_fwd16(bool tr, bool lc, int cm, int grid, const ChainFK& k, hipStream_t st) {
-  void (*f)(ChainFK);
-  if (lc) f = cm == 0 ? (tr ? chain_fwd16_kernel<NW, true, 0, true> : chain_fwd16_kernel<NW, true, 0, false>)
-                      : (tr ? chain_fwd16_kernel<NW, true, 1, true> : chain_fwd16_kernel<NW, true, 1, false>);
-  else if (cm == 0) f = tr ? chain_fwd16_kernel<NW, false, 0, true> : chain_fwd16_kernel<NW, false, 0, false>;
-  else if (cm == 1) f = tr ? chain_fwd16_kernel<NW, false, 1, true> : chain_fwd16_kernel<NW, false, 1, false>;
-  else f = tr ? chain_fwd16_kernel<NW, false, 2, true> : chain_fwd16_kernel<NW, false, 2, false>;
-  hipLaunchKernelGGL(f, dim3(grid), dim3(64 * NW), 0, st, k);
+  if (k.hog) launch_fwd16_g<NW, true>(tr, lc, cm, grid, k, st);
+  else launch_fwd16_g<NW, false>(tr, lc, cm, grid, k, st);
 }
 
 int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
@@ -3046,7 +3116,9 @@ int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   k.ximg = c.wpack_x3;
   k.SG = c.SG; k.sgls = c.sgls;
   k.lcact = c.lcact; k.lcimg = c.lcimg; k.Lo = c.Lo;
+  k.hog = c.fwd_nw ? c.hog : nullptr;
   LBWN_REQUIRE(!c.wpack_x3 || (((uintptr_t)c.wpack_x3) & 15) == 0, "chain fwd: split images not 16-B aligned");
+  LBWN_REQUIRE(!k.hog || c.L < 1024, "chain fwd: granule hand-off tags need L < 1024");
   const bool lc = c.lcimg != nullptr;
   if (lc)
     LBWN_REQUIRE(c.wpack_x3 && c.lcact && !c.cond && c.Lo > 16 * (LC_K - 1) && c.Lo <= LC_KP && c.Lo % 4 == 0 &&
@@ -3131,6 +3203,23 @@ int lbwn_layer_reduce_all_launch(const lbwn_layer_red_args& r, int L, long slab_
 }
 
 int lbwn_slab_floats() { return SLAB; }
+
+namespace {
+__global__ void step_begin_kernel(unsigned* p, long n) {
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) p[e] = 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 0) lbwn_chain_epoch = lbwn_chain_epoch + 1u;
+}
+}  // namespace
+
+// The training step's first launch: zero the status word and the chains' flag blocks (n_bytes) and
+// advance the granule hand-offs' epoch (one kernel: the step's launch gaps cost ~2 us each)
+int lbwn_step_begin_launch(void* words, size_t n_bytes, hipStream_t st) {
+  LBWN_REQUIRE(n_bytes % 4 == 0, "step begin: byte count must be a multiple of 4");
+  const long n = (long)(n_bytes / 4);
+  step_begin_kernel<<<(int)std::max<long>(1, std::min<long>((n + 255) / 256, 1024)), 256, 0, st>>>((unsigned*)words, n);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
 
 namespace {
 // gtab[id][l·64 + c] += Σ over tiles with tile_gid == id (in tile order) of the tile's dv column
