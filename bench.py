@@ -472,7 +472,7 @@ def chain_dilation_sweep(arch_file, B, T, dp, steps=4, gc=None, tile=None):
         os.environ['LBWN_CHAIN_TILE'] = tile
     try:
         tb = TrainBench(arch, B, T, dp)          # untraced: the tile's step time
-        ms, _, _, _ = tb.run(5, 2)
+        ms, _, _, _ = tb.run(10, 3)
         tb.close()
         os.environ['LBWN_CHAIN_TRACE'] = '1'
         tb = TrainBench(arch, B, T, dp)
@@ -505,7 +505,8 @@ def chain_dilation_sweep(arch_file, B, T, dp, steps=4, gc=None, tile=None):
             'ms_per_step': ms,
             'clock': 'clock64 cycles, us at 2.4 GHz', 'traced_block': 1, 'per_dilation': rows,
             'note': 'per-layer start-to-start time of one chain block (its first tile), median over the '
-                    'n_blocks layers of each dilation and %d steps; ms_per_step: 5 timed steps' % steps}
+                    'n_blocks layers of each dilation and %d steps; ms_per_step: 10 timed steps after 3 '
+                    'warmup' % steps}
 
 
 DEFAULT_TILE = '128'    # the library's default chain form (engine.cpp, LBWN_CHAIN_TILE unset)

@@ -62,8 +62,8 @@ struct lbwn_plan {
   // forward hand-off of the 16-position-wave chain (LBWN_FWD_HANDOFF at plan creation): flags
   // (sc1 rows + drain + flag) or tagged granules (oHOG, zeroed before a workspace's first use by
   // this plan: hog_clean_ws)
-  bool fwd_gran = false;
-  size_t oHOG = 0, nHOG = 0;
+  bool fwd_gran = false, bwd_gran = false;
+  size_t oHOG = 0, nHOG = 0, oHOGB = 0;   // one zeroed region: [forward granules | backward granules]
   const void* hog_clean_ws = nullptr;
   // Backward side stream (chain plans): the head weight gradients (dPOST2, dPOST1) run on the
   // main stream before the chain; dSKIP follows the chain on the main stream while `aux2` runs
@@ -307,19 +307,25 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
       LBWN_REQUIRE(ok, "LBWN_CHAIN_TILE must be <fwd>[:<bwd>] with each 128, 64 or w32 (got '%s')", tv);
     }
   }
-  bool fwd_gran = false;
+  bool fwd_gran = false, bwd_gran = false;
   {
     const char* hv = getenv("LBWN_FWD_HANDOFF");
     if (hv && hv[0]) {
       LBWN_REQUIRE(!strcmp(hv, "gran") || !strcmp(hv, "flag"), "LBWN_FWD_HANDOFF must be gran or flag (got '%s')", hv);
       fwd_gran = !strcmp(hv, "gran");
     }
+    hv = getenv("LBWN_BWD_HANDOFF");
+    if (hv && hv[0]) {
+      LBWN_REQUIRE(!strcmp(hv, "gran") || !strcmp(hv, "flag"), "LBWN_BWD_HANDOFF must be gran or flag (got '%s')", hv);
+      bwd_gran = !strcmp(hv, "gran");
+    }
   }
   lbwn_plan* p = new (std::nothrow) lbwn_plan();
   LBWN_REQUIRE(p, "plan: out of host memory");
   p->fwd_nw = fwd_nw;
   p->bwd_nw = bwd_nw;
-  p->fwd_gran = fwd_gran && fwd_nw != 0 && a->n_blocks * a->n_block_layers < 1024;
+  p->fwd_gran = fwd_gran && fwd_nw != 0 && a->n_blocks * a->n_block_layers < 512;
+  p->bwd_gran = bwd_gran && bwd_nw != 0 && a->n_blocks * a->n_block_layers < 512;
   p->a = *a;
   p->B = B;
   p->T = T;
@@ -440,10 +446,13 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   }
   if (p->chain && p->Lo > 0 && lbwn_lc_in_chain_ok(p->Lo))
     p->oLCX = carve(cur, 2 * (size_t)L * std::max(lbwn_lc_image_x3_elems(), lbwn_lc_image16_elems()));
-  if (p->chain && p->fwd_gran) {
-    const int tpf = lbwn_chain_fwd_tile(p->fwd_nw);
-    p->nHOG = 8 * (size_t)L * B * ((T + tpf - 1) / tpf) * tpf * 32;
+  if (p->chain && (p->fwd_gran || p->bwd_gran)) {
+    const int tpf = lbwn_chain_fwd_tile(p->fwd_nw), tpb = lbwn_chain_fwd_tile(p->bwd_nw);
+    const size_t nf = p->fwd_gran ? 8 * (size_t)L * B * ((T + tpf - 1) / tpf) * tpf * 32 : 0;
+    const size_t nb = p->bwd_gran ? 8 * (size_t)L * B * ((T + tpb - 1) / tpb) * tpb * 32 : 0;
+    p->nHOG = nf + nb;
     p->oHOG = carve(cur, p->nHOG);
+    p->oHOGB = p->oHOG + nf;
   }
   p->oHEADP = carve(cur, sizeof(float) * 3 * 2048);
   p->oBSUM = carve(cur, sizeof(float) * (size_t)p->Cs);
@@ -845,7 +854,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     if (c.SG && p->fwd_nw) {
       c.fwd_nw = p->fwd_nw;
       c.grid = p->fwd_grid;
-      if (p->oHOG) c.hog = at<unsigned long long>(ws, p->oHOG);
+      if (p->fwd_gran) c.hog = at<unsigned long long>(ws, p->oHOG);
     }
     Probe(p, st, "layer_fwd");
     if ((e = lbwn_chain_fwd_launch(c, st))) return e;
@@ -1076,7 +1085,11 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     p->bwd_flags_fresh = false;
     if (p->ctrace_blk >= 0) { c.trace = at<long long>(ws, p->oCTRACE); c.trace_blk = p->ctrace_blk; }
     c.B = B; c.T = T; c.H = p->H; c.L = L; c.nbl = p->nbl; c.Cr = Cr; c.Cd = Cd; c.grid = p->chain_grid;
-    if (b16) { c.bwd_nw = p->bwd_nw; c.grid = p->bwd_grid; }
+    if (b16) {
+      c.bwd_nw = p->bwd_nw;
+      c.grid = p->bwd_grid;
+      if (p->bwd_gran) c.hogb = at<unsigned long long>(ws, p->oHOGB);
+    }
     Probe(p, st, "layer_bwd");
     if ((e = lbwn_chain_bwd_launch(c, st))) return e;
     Probe::end(p, st, "layer_bwd");

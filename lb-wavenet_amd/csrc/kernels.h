@@ -141,6 +141,7 @@ struct lbwn_chain_args {
   int fwd_nw = 0;              // forward form (lbwn_chain_fwd_tile); lcimg in the matching layout
   int bwd_nw = 0;              // backward form: 0 = chain_bwd_x3_kernel (128), 4 / 8 = chain_bwd16_kernel
   unsigned long long* hog = nullptr;   // forward (fwd_nw != 0): granule hand-off buffer [L][ntiles][TP][32], or null (flags)
+  unsigned long long* hogb = nullptr;  // backward (bwd_nw != 0): the same for out_c0, or null (flags)
 };
 // zero the status + flag words and advance the granule epoch (the training step's first launch)
 int lbwn_step_begin_launch(void* words, size_t n_bytes, hipStream_t st);

@@ -1409,6 +1409,9 @@ struct ChainBK {
   // bf16-split form (chain_bwd_x3_kernel): z rows (row stride lddz), σ rows [L][M][32], images
   const float* Zf; const float* SG; long sgls; const float* bimg;
   int* tile_gid;               // GC: per tile its uniform voice id or -1 (x3 chain), or null
+  // granule hand-off (chain_bwd16_kernel<..., GR>): out_c0 rows r < min(d, TP) of each (layer,
+  // tile) as {value, tag} words [L][ntiles][TP][32], tag = epoch·1024 + 512 + l
+  unsigned long long* hogb;
 };
 
 // dv rows of wave w's 32 positions (DV, position-major) scatter-added into the GC gradient
@@ -2342,7 +2345,8 @@ LBWN_DEV void gc_scatter16(float* gtab, long ld, const float* DVs, const float* 
   }
 }
 
-template <int NW, bool TR>
+// GR: out_c0 rows cross tiles as tagged granules (no sc1 rows, drain-before-flag or flag)
+template <int NW, bool TR, bool GR>
 __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
   constexpr int TP = 16 * NW, NT = 64 * NW, NH = NW / 4, PH = TP / NH;   // PH: positions per half
   constexpr int NR = TP * 8 / NT;                                        // float4 per thread of a tile (2)
@@ -2364,6 +2368,7 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
   const int r = 16 * w + i16;
   const int tps = (a.T + TP - 1) / TP, ntiles = a.B * tps;
   const int oc_bytes = (int)std::min<long>(a.ocls * 4, 0x7fffffffL);
+  const unsigned ep1024 = GR ? lbwn_chain_epoch * 1024u : 0u;
   if (tid == 0) s_fail = 0;
   for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
     const int tile = ntiles - 1 - it;
@@ -2410,21 +2415,58 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
       // 1. G = dx_{l+1} rows: out_c0_{l+1}[t + dn] (own OC / the producer's published rows) + out_a
       if (dn) {
         const int ptt = tt + max(1, dn / TP);
-        if (ptt < tps) {
+        if (!GR && ptt < tps) {
           if (tid == 0 && !s_fail) {
             if (!wait_flag_ge(a.flags + (long)b * tps + ptt, (unsigned)(a.L - l - 1), a.status, 2u)) s_fail = 1;
           }
           __syncthreads();
         }
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)(l + 1) * a.ocls, (short)0, oc_bytes, BUF_DW3);
         floatx4 gl[NR], go[NR];
+        if (GR) {
+          // rows of the producer tile (sr >= TP, inside T): poll their granules until layer l+1's tag
+          const unsigned tag = ep1024 + 512u + (unsigned)(l + 1);
+          const unsigned long long* src = a.hogb + ((long)(l + 1) * ntiles + (long)b * tps + min(ptt, tps - 1)) * TP * 32;
 #pragma unroll
-        for (int i = 0; i < NR; ++i) {
-          const int e = tid + NT * i, row = e >> 3, c4 = (e & 7) * 4, sr = row + dn;
-          const int ts = min(t0 + sr, a.T - 1);
-          gl[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
-          go[i] = *(const floatx4*)(OC + min(sr, TP - 1) * XS + c4);
+          for (int i = 0; i < NR; ++i) {
+            const int e = tid + NT * i, row = e >> 3, c4 = (e & 7) * 4, sr = row + dn;
+            go[i] = *(const floatx4*)(OC + min(sr, TP - 1) * XS + c4);
+            gl[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+            if (sr >= TP && t0 + sr < a.T) {
+              const int srow = t0 + sr - ptt * TP;
+              long long t_start = 0;
+              for (unsigned spins = 1;; ++spins) {
+                bool ok = true;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                  const unsigned long long x =
+                      __hip_atomic_load(src + srow * 32 + c4 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  gl[i][j] = __uint_as_float((unsigned)x);
+                  ok &= (unsigned)(x >> 32) == tag;
+                }
+                if (ok) break;
+                if ((spins & 15) == 0) {
+                  const long long now = wall_clock64();
+                  if (t_start == 0) t_start = now;
+                  else if (now - t_start > SPIN_TIMEOUT || s_fail) {
+                    __hip_atomic_fetch_or((gu32*)a.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    s_fail = 1;
+                    break;
+                  }
+                }
+                __builtin_amdgcn_s_sleep(1);
+              }
+            }
+          }
+        } else {
+          const __amdgpu_buffer_rsrc_t rs =
+              __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)(l + 1) * a.ocls, (short)0, oc_bytes, BUF_DW3);
+#pragma unroll
+          for (int i = 0; i < NR; ++i) {
+            const int e = tid + NT * i, row = e >> 3, c4 = (e & 7) * 4, sr = row + dn;
+            const int ts = min(t0 + sr, a.T - 1);
+            gl[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
+            go[i] = *(const floatx4*)(OC + min(sr, TP - 1) * XS + c4);
+          }
         }
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
@@ -2559,10 +2601,18 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         const __amdgpu_buffer_rsrc_t rw =
             __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)l * a.ocls, (short)0, oc_bytes, BUF_DW3);
         const bool pub = l > 0 && valid && r < min(d, TP);
+        unsigned long long* hdst = GR ? a.hogb + ((long)l * ntiles + tile) * TP * 32 + r * 32 : nullptr;
+        const unsigned long long htag = (unsigned long long)(ep1024 + 512u + (unsigned)l) << 32;
 #pragma unroll
         for (int xb = 0; xb < 2; ++xb) {
           *(floatx4*)(OC + r * XS + 16 * xb + 4 * g) = acc_c[xb];
-          if (pub) __builtin_amdgcn_raw_buffer_store_b128(acc_c[xb], rw, (int)((m * 32 + 16 * xb + 4 * g) * 4), 0, 16);
+          if (GR && pub) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              __hip_atomic_store(hdst + 16 * xb + 4 * g + j, htag | __float_as_uint(acc_c[xb][j]), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+          }
+          if (!GR && pub) __builtin_amdgcn_raw_buffer_store_b128(acc_c[xb], rw, (int)((m * 32 + 16 * xb + 4 * g) * 4), 0, 16);
         }
       }
       if (l == 0 && valid) {
@@ -2578,7 +2628,7 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
       // 5. publish out_c0_l (the drain also lands this layer's x / z DMA pieces)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // DV, G, OC, Xp/Xc/ZT complete; the weight image is dead
-      if (tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
+      if (!GR && tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
       if (a.gc_dtab && !tile_uni) gc_scatter16(a.gc_dtab + (long)l * 64, a.gc_ld, DVs, DVg, w, lane, 32, gc_starts, gc_pid);
       XSTAMP(4);
       // 6. dSIG / dGATE tile t4 = w & 3 (2·kind + tap) over this wave's position half:
@@ -3177,12 +3227,23 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
     if (int e = lbwn_zero_launch(c.flags, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st)) return e;
   }
   LBWN_REQUIRE(x3 == (c.dzls > 0), "chain bwd: the bf16-split chain reads dZ in chain order (dzls), the f32 chain in rows");
+  k.hogb = c.bwd_nw ? c.hogb : nullptr;
   if (c.bwd_nw == 8) {
-    if (k.trace) chain_bwd16_kernel<8, true><<<c.grid, 512, 0, st>>>(k);
-    else chain_bwd16_kernel<8, false><<<c.grid, 512, 0, st>>>(k);
+    if (k.hogb) {
+      if (k.trace) chain_bwd16_kernel<8, true, true><<<c.grid, 512, 0, st>>>(k);
+      else chain_bwd16_kernel<8, false, true><<<c.grid, 512, 0, st>>>(k);
+    } else {
+      if (k.trace) chain_bwd16_kernel<8, true, false><<<c.grid, 512, 0, st>>>(k);
+      else chain_bwd16_kernel<8, false, false><<<c.grid, 512, 0, st>>>(k);
+    }
   } else if (c.bwd_nw == 4) {
-    if (k.trace) chain_bwd16_kernel<4, true><<<c.grid, 256, 0, st>>>(k);
-    else chain_bwd16_kernel<4, false><<<c.grid, 256, 0, st>>>(k);
+    if (k.hogb) {
+      if (k.trace) chain_bwd16_kernel<4, true, true><<<c.grid, 256, 0, st>>>(k);
+      else chain_bwd16_kernel<4, false, true><<<c.grid, 256, 0, st>>>(k);
+    } else {
+      if (k.trace) chain_bwd16_kernel<4, true, false><<<c.grid, 256, 0, st>>>(k);
+      else chain_bwd16_kernel<4, false, false><<<c.grid, 256, 0, st>>>(k);
+    }
   } else if (x3 && k.trace) chain_bwd_x3_kernel<true><<<c.grid, 256, 0, st>>>(k);
   else if (x3) chain_bwd_x3_kernel<false><<<c.grid, 256, 0, st>>>(k);
   else chain_bwd_kernel<<<c.grid, 256, 0, st>>>(k);
