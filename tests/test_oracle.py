@@ -184,6 +184,26 @@ def test_generation_teacher_forced_equals_training_forward():
     np.testing.assert_allclose(glog[0, 1:], lg[0], rtol=1e-10, atol=1e-10)
 
 
+def test_generation_forced_trajectory():
+    """generate(..., forced_q=) (the GPU full-ring-depth test's checker): forcing a run's own
+    draws reproduces it exactly, and forcing another trajectory changes only the inputs -- each
+    draw is then the inverse-CDF draw of the logits computed along that trajectory.  The d <= 4
+    rings wrap >= 7x in 30 steps."""
+    arch = arch_tiny(gc=0)
+    P, _, _, _, _ = _setup(arch, B=2, T=8)
+    s0, w0, lg0 = R.generate(arch, P, 2, 30, seed=3, return_logits=True)
+    s1, w1, lg1 = R.generate(arch, P, 2, 30, seed=3, return_logits=True, forced_q=s0)
+    np.testing.assert_array_equal(s0, s1)
+    np.testing.assert_array_equal(lg0, lg1)
+    other = (s0 + 17) % arch['n_quant']
+    s2, _, lg2 = R.generate(arch, P, 2, 30, seed=3, return_logits=True, forced_q=other)
+    np.testing.assert_array_equal(lg2[:, 0], lg0[:, 0])            # step 0: zero input either way
+    assert not np.allclose(lg2[:, 1:], lg0[:, 1:])
+    for b in range(2):
+        for i in range(30):
+            assert s2[b, i] == R.sample_from_logits(lg2[b, i], R.philox_uniform(3, b, i))
+
+
 def test_adam_tf1():
     opt = R.AdamTF1(0.1)
     P = {'w': np.array([1.0, -2.0])}
