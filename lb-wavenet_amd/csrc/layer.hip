@@ -1825,7 +1825,11 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
 // of the dv registers used as the B operand; then Rs f32 [c][XS] for the dz product.  Padded to
 // a whole number of 1-KiB DMA pieces.
 constexpr int BD_US = 2 * 32 * XW_ROW;
-constexpr int BIMG_F = (BD_US / 2 + 32 * XS + 255) / 256 * 256;   // 7680 floats
+// + RSX (bf16 units, after Rs): the split residual image of chain_bwd16_kernel's dz product,
+// [z channel][plane][kk] in rows of XR_ROW, kk = 8g + e holding g channel (e < 4 ? 4g + e :
+// 16 + 4g + e - 4): the k order of the lane's g values (N layout) as the 16x16x32 B operand
+constexpr int RSX_OFF = BD_US + 2 * 32 * XS;                       // bf16 offset of RSX
+constexpr int BIMG_F = (RSX_OFF / 2 + 32 * XR_ROW / 2 + 255) / 256 * 256;   // 9216 floats (36 pieces)
 constexpr int CBX_LDS = BIMG_F + 7 * LP * 32 + 8 * 96;            // IMG | Xp Xc ZT | DVs DVg G OC | part
 static_assert(CBX_LDS * 4 + 16 <= 160 * 1024, "chain bwd x3 LDS");
 
@@ -1857,7 +1861,23 @@ LBWN_DEV void pack_bx3_body(int l, const float* sig, const float* gate, const fl
     const int c = e / XS, o = e % XS;
     rs[e] = (c < Cd && o < Cr) ? wr[c * Cr + o] : 0.f;
   }
-  for (int e = BD_US / 2 + 32 * XS + threadIdx.x; e < BIMG_F; e += blockDim.x) img[e] = 0.f;
+  unsigned short* rsx = (unsigned short*)img + RSX_OFF;
+  for (int e = threadIdx.x; e < 32 * 16; e += blockDim.x) {
+    const int zc = e >> 4, kk = 2 * (e & 15), gg = kk >> 3, e0 = kk & 7;
+    floatx2 x = {0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int ee = e0 + u, c = ee < 4 ? 4 * gg + ee : 16 + 4 * gg + ee - 4;
+      if (zc < Cd && c < Cr) x[u] = wr[zc * Cr + c];
+    }
+    unsigned hi, mi, lo;
+    split2(x, hi, mi, lo);
+    unsigned short* row = rsx + zc * XR_ROW + kk;
+    *(unsigned*)(row) = hi;
+    *(unsigned*)(row + 32) = mi;
+    *(unsigned*)(row + 64) = lo;
+  }
+  for (int e = RSX_OFF / 2 + 32 * XR_ROW / 2 + threadIdx.x; e < BIMG_F; e += blockDim.x) img[e] = 0.f;
 }
 
 __global__ void pack_layers_x3_kernel(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
@@ -2192,9 +2212,9 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
             dg[s2][j] = DVg[CONF(32) ? p * 32 : swz(p, pi)];
           }
         XSTAMP(8);
-        if (l > 0) {   // image pieces w, w+4, ... (30 of 1 KiB)
+        if (l > 0) {   // image pieces w, w+4, ... (36 of 1 KiB)
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
+          for (int i = 0; i < (BIMG_F / 256 + 3) / 4; ++i) {
             const int pc = w + 4 * i;
             if (pc < BIMG_F / 256 && !CONF(1024)) dma16(isrc + pc * 256, IMG + pc * 256);
           }
@@ -2501,27 +2521,25 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         gv[xb] = v;
         *(floatx4*)gp = v;
       }
-      // 2. dz = dZ + RES·g  (f32 MFMA 16x16x4: k = g's channel 16xb + 4g + rr)
+      // 2. dz = dZ + RES·g on 16x16x32 splits: B = the lane's g values (k = 8g + e, RSX's k order),
+      //    A = RSX rows ch16(b, i16); the x / z row DMA pieces go out between the two blocks
       floatx4 dz[2];
       {
-        floatx4 rx[2][2];
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-          for (int xb = 0; xb < 2; ++xb) rx[bb][xb] = *(const floatx4*)(Rs + ch16(bb, i16) * XS + 16 * xb + 4 * g);
+        const unsigned short* RX = (const unsigned short*)IMG + RSX_OFF;
+        bf16x8 gb[3];
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) dz[bb] = valid ? dzr[bb] : floatx4{0.f, 0.f, 0.f, 0.f};
+        split8(gv[0], gv[1], gb);
 #pragma unroll
-        for (int xb = 0; xb < 2; ++xb) {
+        for (int bb = 0; bb < 2; ++bb) {
+          bf16x8 af[3];
 #pragma unroll
-          for (int rr = 0; rr < 4; ++rr)
-#pragma unroll
-            for (int bb = 0; bb < 2; ++bb)
-              dz[bb] = __builtin_amdgcn_mfma_f32_16x16x4f32(rx[bb][xb][rr], gv[xb][rr], dz[bb], 0, 0, 0);
+          for (int p = 0; p < 3; ++p) af[p] = *(const bf16x8*)(RX + ch16(bb, i16) * XR_ROW + 32 * p + 8 * g);
+          dz[bb] = mfma16x3(af, gb, dz[bb]);
           // x / z rows of this layer: pieces k = w, w + NW, ... (3·TP/8 rows of 8 over the block)
 #pragma unroll
           for (int k2 = 0; k2 < TP / 8 / NW / 2 + 1; ++k2) {
-            const int k = w + NW * (2 * k2 + xb);
+            const int k = w + NW * (2 * k2 + bb);
             if (k < TP / 8) dma_rows3(k);
           }
         }
@@ -2641,48 +2659,62 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         const float* XA = (t4 & 1) ? Xc : Xp;
         const float* DB = (t4 & 2) ? DVg : DVs;
         const int pi = lane & 31, hh = lane >> 5;
-        float xa[PH / 16][8], db[PH / 16][8];
+        // k-steps in two groups of PH/32: the first group's operands are read before the DMA issue
+        // (its asm is a compiler barrier for LDS reads), the second group's after (all four up
+        // front held 64 registers and spilled)
+        constexpr int KG = PH / 32;
+        float xa[KG][8], db[KG][8];
+        auto rd = [&](int grp) {
 #pragma unroll
-        for (int s2 = 0; s2 < PH / 16; ++s2)
+          for (int s2 = 0; s2 < KG; ++s2)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int p = p0 + 16 * s2 + 8 * hh + e;
-            xa[s2][e] = XA[p * 32 + pi];
-            db[s2][e] = DB[p * XS + pi];
+            for (int e = 0; e < 8; ++e) {
+              const int p = p0 + 16 * (KG * grp + s2) + 8 * hh + e;
+              xa[s2][e] = XA[p * 32 + pi];
+              db[s2][e] = DB[p * XS + pi];
+            }
+        };
+        auto ks = [&]() {
+#pragma unroll
+          for (int s2 = 0; s2 < KG; ++s2) {
+            bf16x8 fx[3], fd[3];
+            split8(floatx4{xa[s2][0], xa[s2][1], xa[s2][2], xa[s2][3]}, floatx4{xa[s2][4], xa[s2][5], xa[s2][6], xa[s2][7]}, fx);
+            split8(floatx4{db[s2][0], db[s2][1], db[s2][2], db[s2][3]}, floatx4{db[s2][4], db[s2][5], db[s2][6], db[s2][7]}, fd);
+            accT = mfma_x3(fx, fd, accT);
           }
+        };
+        rd(0);
         XSTAMP(8);
         if (l > 0) {   // the next layer's image and rows, behind this layer's operand reads
           dma_image(l - 1);
           load_regs(l - 1);
         }
         XSTAMP(9);
-#pragma unroll
-        for (int s2 = 0; s2 < PH / 16; ++s2) {
-          bf16x8 fx[3], fd[3];
-          split8(floatx4{xa[s2][0], xa[s2][1], xa[s2][2], xa[s2][3]}, floatx4{xa[s2][4], xa[s2][5], xa[s2][6], xa[s2][7]}, fx);
-          split8(floatx4{db[s2][0], db[s2][1], db[s2][2], db[s2][3]}, floatx4{db[s2][4], db[s2][5], db[s2][6], db[s2][7]}, fd);
-          accT = mfma_x3(fx, fd, accT);
-          if (s2 == 0) XSTAMP(10);
-        }
+        ks();
+        XSTAMP(10);
+        rd(1);
+        ks();
       }
       XSTAMP(5);
       // 7. dRES quarter t4 (16x16: z channels 16(t4>>1).., res out 16(t4&1)..) over the same
-      //    positions on v_mfma_f32_16x16x4_f32: A[i=c][k=pos] = z[pos][c], B[k=pos][j=o] = g[pos][o]
+      //    positions on 16x16x32 splits (k = 32 positions): A[i=c][k=pos] = z[pos][c], B[k=pos][j=o] =
+      //    g[pos][o], each lane's 8 positions 8g..8g+7 of the k-step
       floatx4 accR = {0.f, 0.f, 0.f, 0.f};
       {
         const int cz = 16 * (t4 >> 1) + i16, og = 16 * (t4 & 1) + i16;
 #pragma unroll
         for (int c8 = 0; c8 < PH / 32; ++c8) {
-          float za[8], ga[8];
+          floatx4 za[2], ga[2];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const int p = p0 + 32 * c8 + 4 * e + g;
-            za[e] = ZT[p * 32 + cz];
-            ga[e] = G[p * XS + og];
+            const int p = p0 + 32 * c8 + 8 * g + e;
+            za[e >> 2][e & 3] = ZT[p * 32 + cz];
+            ga[e >> 2][e & 3] = G[p * XS + og];
           }
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) accR = __builtin_amdgcn_mfma_f32_16x16x4f32(za[e], ga[e], accR, 0, 0, 0);
+          bf16x8 fz[3], fg[3];
+          split8(za[0], za[1], fz);
+          split8(ga[0], ga[1], fg);
+          accR = mfma16x3(fz, fg, accR);
         }
       }
       XSTAMP(11);

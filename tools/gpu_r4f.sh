@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 bash tools/gpu_tests.sh r4f "gen or full_size or plan_forward_backward" || exit 1
 bash tools/gen_ab.sh r3gen > gpurun_out/gen_ab_r4f.txt 2>&1; cat gpurun_out/gen_ab_r4f.txt
 timeout -k 10 120 python tools/gen_trace.py 10 > gpurun_out/gentrace_r4f.txt 2>&1; cat gpurun_out/gentrace_r4f.txt
-CONFIGS="arch3:8 arch5:8" timeout -k 10 600 bash tools/ab_step.sh r4bias > gpurun_out/ab_bias_r4f.txt 2>&1; cat gpurun_out/ab_bias_r4f.txt
+CONFIGS="arch3:8 arch5:8" timeout -k 10 700 bash tools/ab_step.sh r4bias prevdz > gpurun_out/ab_bias_r4f.txt 2>&1; cat gpurun_out/ab_bias_r4f.txt
 for r in 1 2; do for w in 1 0; do
   LBWN_GEMM_WIDE=$w timeout -k 10 200 python bench.py --no-cpu-baseline --no-extras --no-gen --steps 30 > gpurun_out/abw_$w.json 2>/dev/null || exit 1
   python -c "import json; d=json.load(open('gpurun_out/abw_$w.json')); print('round $r wide $w', round(d['ms_per_step'],4))"
