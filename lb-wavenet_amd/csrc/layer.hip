@@ -1022,12 +1022,26 @@ LBWN_DEV void conv16_tap(const float* xrow, const unsigned short* Wt, int i16, i
   }
 }
 
+typedef short shortx4 __attribute__((ext_vector_type(4)));
+
+// 4 consecutive-k values -> the three bf16x4 fragments of v_mfma_f32_16x16x16_bf16
+LBWN_DEV void split4(floatx4 a, shortx4 (&f)[3]) {
+  unsigned h0, m0, l0, h1, m1, l1;
+  split2((floatx2){a[0], a[1]}, h0, m0, l0);
+  split2((floatx2){a[2], a[3]}, h1, m1, l1);
+  f[0] = __builtin_bit_cast(shortx4, (uintx2){h0, h1});
+  f[1] = __builtin_bit_cast(shortx4, (uintx2){m0, m1});
+  f[2] = __builtin_bit_cast(shortx4, (uintx2){l0, l1});
+}
+
 // lc·[LC_SIGNAL_l | LC_GATE_l] onto the accumulators: A = LC16 image rows, B = the lane's LC input
-// row (k = 32s + 8g + j), held as raw f32 (lcv: 24 registers instead of 36 pre-split: at two
-// waves per SIMD the split form spilled) and split per k-step
-LBWN_DEV void lc16_terms(const unsigned short* LI, const floatx4 (&lcv)[6], int i16, int g, floatx4 (&acc)[4]) {
+// row, held as raw f32 (lcv: 20 registers instead of 36 pre-split: at two waves per SIMD the split
+// form spilled) and split per k-step.  K = 80 runs as two 32-deep k-steps (16x16x32, k = 32s + 8g +
+// j) and one 16-deep tail (v_mfma_f32_16x16x16_bf16, k = 64 + 4g + j: half the cycles of a
+// zero-padded third 32-deep step)
+LBWN_DEV void lc16_terms(const unsigned short* LI, const floatx4 (&lcv)[5], int i16, int g, floatx4 (&acc)[4]) {
 #pragma unroll
-  for (int s2 = 0; s2 < 3; ++s2) {
+  for (int s2 = 0; s2 < 2; ++s2) {
     bf16x8 xb[3];
     split8(lcv[2 * s2], lcv[2 * s2 + 1], xb);
 #pragma unroll
@@ -1038,6 +1052,22 @@ LBWN_DEV void lc16_terms(const unsigned short* LI, const floatx4 (&lcv)[6], int 
       for (int p = 0; p < 3; ++p) wf[p] = *(const bf16x8*)(LI + o * LC16_ROW + LC16_KP * p + 32 * s2 + 8 * g);
       acc[i] = mfma16x3(wf, xb, acc[i]);
     }
+  }
+  shortx4 tb[3];
+  split4(lcv[4], tb);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int o = 32 * (i >> 1) + ch16(i & 1, i16);
+    shortx4 wf[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) wf[p] = *(const shortx4*)(LI + o * LC16_ROW + LC16_KP * p + 64 + 4 * g);
+    // small terms first: a2b0, a1b1, a0b2, a1b0, a0b1, a0b0
+    acc[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[2], tb[0], acc[i], 0, 0, 0);
+    acc[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[1], tb[1], acc[i], 0, 0, 0);
+    acc[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[0], tb[2], acc[i], 0, 0, 0);
+    acc[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[1], tb[0], acc[i], 0, 0, 0);
+    acc[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[0], tb[1], acc[i], 0, 0, 0);
+    acc[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[0], tb[0], acc[i], 0, 0, 0);
   }
 }
 
@@ -1083,16 +1113,14 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
     const int myid = (a.gc_tab && valid) ? a.ids[m] : 0;
     floatx4 cv[4];
     load_cond16<CM>(a, 0, myid, m, valid && has_cond, q0, h, cv);
-    floatx4 lcv[6];   // LC: this lane's LC input row, k = 32s + 8g + 0..7 (zero past n_lc_out)
+    floatx4 lcv[5];   // LC: this lane's LC input row, k = 32s + 8g + 0..7 (s < 2), 64 + 4g + 0..3 (zero past n_lc_out)
     if (LC) {
       const float* lrow = a.lcact + ((long)b * a.T + min(t, a.T - 1)) * a.Lo;
 #pragma unroll
-      for (int s2 = 0; s2 < 3; ++s2) {
-        const int k0 = 32 * s2 + 8 * g;
-        lcv[2 * s2] = *(const floatx4*)(lrow + min(k0, a.Lo - 4));       // clamped, then select
-        lcv[2 * s2 + 1] = *(const floatx4*)(lrow + min(k0 + 4, a.Lo - 4));
-        if (k0 >= a.Lo) lcv[2 * s2] = floatx4{0.f, 0.f, 0.f, 0.f};
-        if (k0 + 4 >= a.Lo) lcv[2 * s2 + 1] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < 5; ++q) {
+        const int k0 = q < 4 ? 32 * (q >> 1) + 8 * g + 4 * (q & 1) : 64 + 4 * g;
+        lcv[q] = *(const floatx4*)(lrow + min(k0, a.Lo - 4));       // clamped, then select
+        if (k0 >= a.Lo) lcv[q] = floatx4{0.f, 0.f, 0.f, 0.f};
       }
     }
     __syncthreads();  // previous tile's LDS use done
