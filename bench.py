@@ -50,14 +50,12 @@ def chain_forms():
 
 def chain_ceiling(name, arch, x3):
     """Peak of the arithmetic the chain kernel actually runs (f32-equivalent FLOP/s), per
-    algorithmic FLOP: in the bf16-split build the 16-position-wave backward chain
-    (chain_bwd16_kernel, the default) runs dx, dSIG/dGATE, dz and dRES all as split products;
-    the 32-position-wave one (w32) did dx and dSIG/dGATE (16·Cr·Cd per position and layer) split
-    and dz, dRES (4·Cr·Cd) on the f32 MFMA; the forward chain does its conv and residual
-    (10·Cr·Cd) as split products."""
+    algorithmic FLOP: in the bf16-split build the backward chain (either form) does dx and
+    dSIG/dGATE (16·Cr·Cd per position and layer) as split products and dz, dRES (4·Cr·Cd) on the
+    f32 MFMA; the forward chain does its conv and residual (10·Cr·Cd) as split products."""
     if not x3:
         return FP32_MFMA_PEAK
-    if name == 'layer_bwd' and chain_forms()[1] == 'w32':
+    if name == 'layer_bwd':
         return 20.0 / (16.0 / X3_PEAK + 4.0 / FP32_MFMA_PEAK)
     return X3_PEAK
 
@@ -426,8 +424,7 @@ class TrainBench:
                'avg_launch_us': avg * 1e6, 'work_per_launch': work,
                'traffic': traffic_from_profiles(name) if traffic else None}
         if bound == 'mfma':
-            out['arith'] = (('bf16-split (6 products) for dx and dSIG/dGATE, f32 MFMA for dz and dRES'
-                             if chain_forms()[1] == 'w32' else 'bf16-split (6 products) for dx, dz, dSIG/dGATE and dRES')
+            out['arith'] = ('bf16-split (6 products) for dx and dSIG/dGATE, f32 MFMA for dz and dRES'
                             if x3 and name == 'layer_bwd' else ('bf16-split' if x3 else 'f32 MFMA'))
             out['frac_of_f32_peak'] = ach / FP32_MFMA_PEAK
         if name == 'layer_fwd':

@@ -8,7 +8,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <mutex>
 #include <new>
 
 #include "../../include/lbwn.h"
@@ -59,12 +58,6 @@ struct lbwn_plan {
   // 8 / 4 = 16-position waves on 128- / 64-position tiles (chain_fwd16_kernel / chain_bwd16_kernel)
   int fwd_nw = 8, bwd_nw = 8;
   int bwd_grid = 0;
-  // forward hand-off of the 16-position-wave chain (LBWN_FWD_HANDOFF at plan creation): flags
-  // (sc1 rows + drain + flag) or tagged granules (oHOG, zeroed before a workspace's first use by
-  // this plan: hog_clean_ws)
-  bool fwd_gran = false, bwd_gran = false;
-  size_t oHOG = 0, nHOG = 0, oHOGB = 0;   // one zeroed region: [forward granules | backward granules]
-  const void* hog_clean_ws = nullptr;
   // Backward side stream (chain plans): the head weight gradients (dPOST2, dPOST1) run on the
   // main stream before the chain; dSKIP follows the chain on the main stream while `aux2` runs
   // the HBM-bound slab reduction and dPRE scatter beside it.  A chain block takes a whole CU's
@@ -307,25 +300,10 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
       LBWN_REQUIRE(ok, "LBWN_CHAIN_TILE must be <fwd>[:<bwd>] with each 128, 64 or w32 (got '%s')", tv);
     }
   }
-  bool fwd_gran = false, bwd_gran = false;
-  {
-    const char* hv = getenv("LBWN_FWD_HANDOFF");
-    if (hv && hv[0]) {
-      LBWN_REQUIRE(!strcmp(hv, "gran") || !strcmp(hv, "flag"), "LBWN_FWD_HANDOFF must be gran or flag (got '%s')", hv);
-      fwd_gran = !strcmp(hv, "gran");
-    }
-    hv = getenv("LBWN_BWD_HANDOFF");
-    if (hv && hv[0]) {
-      LBWN_REQUIRE(!strcmp(hv, "gran") || !strcmp(hv, "flag"), "LBWN_BWD_HANDOFF must be gran or flag (got '%s')", hv);
-      bwd_gran = !strcmp(hv, "gran");
-    }
-  }
   lbwn_plan* p = new (std::nothrow) lbwn_plan();
   LBWN_REQUIRE(p, "plan: out of host memory");
   p->fwd_nw = fwd_nw;
   p->bwd_nw = bwd_nw;
-  p->fwd_gran = fwd_gran && fwd_nw != 0 && a->n_blocks * a->n_block_layers < 512;
-  p->bwd_gran = bwd_gran && bwd_nw != 0 && a->n_blocks * a->n_block_layers < 512;
   p->a = *a;
   p->B = B;
   p->T = T;
@@ -446,14 +424,6 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   }
   if (p->chain && p->Lo > 0 && lbwn_lc_in_chain_ok(p->Lo))
     p->oLCX = carve(cur, 2 * (size_t)L * std::max(lbwn_lc_image_x3_elems(), lbwn_lc_image16_elems()));
-  if (p->chain && (p->fwd_gran || p->bwd_gran)) {
-    const int tpf = lbwn_chain_fwd_tile(p->fwd_nw), tpb = lbwn_chain_fwd_tile(p->bwd_nw);
-    const size_t nf = p->fwd_gran ? 8 * (size_t)L * B * ((T + tpf - 1) / tpf) * tpf * 32 : 0;
-    const size_t nb = p->bwd_gran ? 8 * (size_t)L * B * ((T + tpb - 1) / tpb) * tpb * 32 : 0;
-    p->nHOG = nf + nb;
-    p->oHOG = carve(cur, p->nHOG);
-    p->oHOGB = p->oHOG + nf;
-  }
   p->oHEADP = carve(cur, sizeof(float) * 3 * 2048);
   p->oBSUM = carve(cur, sizeof(float) * (size_t)p->Cs);
   p->oWPK = carve(cur, sizeof(float) * (size_t)L * lbwn_layer_image_floats());
@@ -730,30 +700,6 @@ int lc_upsample_bwd(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G, vo
 
 }  // namespace
 
-// Granule buffers hold tags of earlier steps (process-monotonic epochs: never equal to the current
-// one) once this plan has zeroed them on this workspace; another plan using the same workspace (or
-// a new workspace) may leave anything there, so the plan re-zeroes whenever the last granule user
-// of the workspace was not this plan.
-static std::mutex g_hog_mu;
-static const void* g_hog_ws[16];
-static const lbwn_plan* g_hog_plan[16];
-static bool hog_is_clean(lbwn_plan* p, void* ws) {
-  std::lock_guard<std::mutex> lk(g_hog_mu);
-  int slot = -1;
-  for (int i = 0; i < 16; ++i)
-    if (g_hog_ws[i] == ws) slot = i;
-  const bool clean = slot >= 0 && g_hog_plan[slot] == p && p->hog_clean_ws == ws;
-  if (slot < 0) {
-    static int next = 0;
-    slot = next;
-    next = (next + 1) % 16;
-  }
-  g_hog_ws[slot] = ws;
-  g_hog_plan[slot] = p;
-  p->hog_clean_ws = ws;
-  return clean;
-}
-
 int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* wav_q, const int* ids,
                        const float* mel, float* save, float* stats, void* stream) {
   LBWN_REQUIRE(p && P && ws && wav_q && ids && save && stats, "train_forward: null argument");
@@ -766,10 +712,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   P = &Ppad;
   // the sticky status word (chain spin timeouts OR their codes in) lives for one step:
   // zeroed here, read by the host after the step (lbwn_plan_tensor "status")
-  if ((e = lbwn_step_begin_launch(at<char>(ws, p->oSTATUS), 16 + 2 * p->nflag_bytes, st))) return e;
-  if (p->oHOG && !hog_is_clean(p, ws)) {   // no tag of an earlier run / plan may sit in the granules
-    if ((e = lbwn_zero_launch(at<char>(ws, p->oHOG), p->nHOG, st))) return e;
-  }
+  if ((e = lbwn_zero_launch(at<char>(ws, p->oSTATUS), 16 + 2 * p->nflag_bytes, st))) return e;
   p->bwd_flags_fresh = true;
   // the fused LC upsample depends only on the mel input and the upsample filters: it runs on
   // aux2 beside the weight packs, embedding, GC table and D-sep prepend, joined before the chain
@@ -851,11 +794,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     c.flags_zeroed = 1;   // zeroed with the status word at the step start
     if (p->ctrace_blk >= 0) { c.trace = at<long long>(ws, p->oCTRACE); c.trace_blk = p->ctrace_blk; }
     c.B = B; c.T = T; c.H = H; c.L = L; c.nbl = p->nbl; c.Cr = Cr; c.Cd = Cd; c.grid = p->chain_grid;
-    if (c.SG && p->fwd_nw) {
-      c.fwd_nw = p->fwd_nw;
-      c.grid = p->fwd_grid;
-      if (p->fwd_gran) c.hog = at<unsigned long long>(ws, p->oHOG);
-    }
+    if (c.SG && p->fwd_nw) { c.fwd_nw = p->fwd_nw; c.grid = p->fwd_grid; }
     Probe(p, st, "layer_fwd");
     if ((e = lbwn_chain_fwd_launch(c, st))) return e;
     Probe::end(p, st, "layer_fwd");
@@ -1085,11 +1024,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     p->bwd_flags_fresh = false;
     if (p->ctrace_blk >= 0) { c.trace = at<long long>(ws, p->oCTRACE); c.trace_blk = p->ctrace_blk; }
     c.B = B; c.T = T; c.H = p->H; c.L = L; c.nbl = p->nbl; c.Cr = Cr; c.Cd = Cd; c.grid = p->chain_grid;
-    if (b16) {
-      c.bwd_nw = p->bwd_nw;
-      c.grid = p->bwd_grid;
-      if (p->bwd_gran) c.hogb = at<unsigned long long>(ws, p->oHOGB);
-    }
+    if (b16) { c.bwd_nw = p->bwd_nw; c.grid = p->bwd_grid; }
     Probe(p, st, "layer_bwd");
     if ((e = lbwn_chain_bwd_launch(c, st))) return e;
     Probe::end(p, st, "layer_bwd");

@@ -140,11 +140,7 @@ struct lbwn_chain_args {
   const float* lcact = nullptr; const unsigned short* lcimg = nullptr; int Lo = 0;
   int fwd_nw = 0;              // forward form (lbwn_chain_fwd_tile); lcimg in the matching layout
   int bwd_nw = 0;              // backward form: 0 = chain_bwd_x3_kernel (128), 4 / 8 = chain_bwd16_kernel
-  unsigned long long* hog = nullptr;   // forward (fwd_nw != 0): granule hand-off buffer [L][ntiles][TP][32], or null (flags)
-  unsigned long long* hogb = nullptr;  // backward (bwd_nw != 0): the same for out_c0, or null (flags)
 };
-// zero the status + flag words and advance the granule epoch (the training step's first launch)
-int lbwn_step_begin_launch(void* words, size_t n_bytes, hipStream_t st);
 int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st);
 int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st);
 int lbwn_layer_reduce_all_launch(const lbwn_layer_red_args& r, int L, long slab_layer, hipStream_t st);

@@ -443,15 +443,7 @@ struct ChainFK {
   // in-chain LC term (chain_fwd_kernel<true, true>): the upsampled LC input [M][Lo] and the L
   // split LC images (LCIMG_US bf16 each)
   const float* lcact; const unsigned short* lcimg; int Lo;
-  // granule hand-off (chain_fwd16_kernel<..., GR>): halo rows of x_l as {value, tag} words
-  // [L][ntiles][TP][32], tag = epoch·1024 + l (lbwn_chain_epoch, advanced once per step)
-  unsigned long long* hog;
 };
-
-// Step epoch of the granule hand-offs: advanced by lbwn_step_begin_launch at every training step's
-// start (stream-ordered, so a captured graph replays it too); module-scope device state, one per
-// device, monotonic in the process
-__device__ unsigned lbwn_chain_epoch;
 
 // lc·[LC_SIGNAL_l | LC_GATE_l] onto the accumulators (tmodel.py:155-160): A = the layer's LC
 // image rows (out channel), B = this lane's LC input row, pre-split once per tile (lcb); the
@@ -1022,26 +1014,12 @@ LBWN_DEV void conv16_tap(const float* xrow, const unsigned short* Wt, int i16, i
   }
 }
 
-typedef short shortx4 __attribute__((ext_vector_type(4)));
-
-// 4 consecutive-k values -> the three bf16x4 fragments of v_mfma_f32_16x16x16_bf16
-LBWN_DEV void split4(floatx4 a, shortx4 (&f)[3]) {
-  unsigned h0, m0, l0, h1, m1, l1;
-  split2((floatx2){a[0], a[1]}, h0, m0, l0);
-  split2((floatx2){a[2], a[3]}, h1, m1, l1);
-  f[0] = __builtin_bit_cast(shortx4, (uintx2){h0, h1});
-  f[1] = __builtin_bit_cast(shortx4, (uintx2){m0, m1});
-  f[2] = __builtin_bit_cast(shortx4, (uintx2){l0, l1});
-}
-
 // lc·[LC_SIGNAL_l | LC_GATE_l] onto the accumulators: A = LC16 image rows, B = the lane's LC input
-// row, held as raw f32 (lcv: 20 registers instead of 36 pre-split: at two waves per SIMD the split
-// form spilled) and split per k-step.  K = 80 runs as two 32-deep k-steps (16x16x32, k = 32s + 8g +
-// j) and one 16-deep tail (v_mfma_f32_16x16x16_bf16, k = 64 + 4g + j: half the cycles of a
-// zero-padded third 32-deep step)
-LBWN_DEV void lc16_terms(const unsigned short* LI, const floatx4 (&lcv)[5], int i16, int g, floatx4 (&acc)[4]) {
+// row (k = 32s + 8g + j), held as raw f32 (lcv: 24 registers instead of 36 pre-split: at two
+// waves per SIMD the split form spilled) and split per k-step
+LBWN_DEV void lc16_terms(const unsigned short* LI, const floatx4 (&lcv)[6], int i16, int g, floatx4 (&acc)[4]) {
 #pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
+  for (int s2 = 0; s2 < 3; ++s2) {
     bf16x8 xb[3];
     split8(lcv[2 * s2], lcv[2 * s2 + 1], xb);
 #pragma unroll
@@ -1053,31 +1031,13 @@ LBWN_DEV void lc16_terms(const unsigned short* LI, const floatx4 (&lcv)[5], int 
       acc[i] = mfma16x3(wf, xb, acc[i]);
     }
   }
-  shortx4 tb[3];
-  split4(lcv[4], tb);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int o = 32 * (i >> 1) + ch16(i & 1, i16);
-    shortx4 wf[3];
-#pragma unroll
-    for (int p = 0; p < 3; ++p) wf[p] = *(const shortx4*)(LI + o * LC16_ROW + LC16_KP * p + 64 + 4 * g);
-    // small terms first: a2b0, a1b1, a0b2, a1b0, a0b1, a0b0
-    acc[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[2], tb[0], acc[i], 0, 0, 0);
-    acc[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[1], tb[1], acc[i], 0, 0, 0);
-    acc[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[0], tb[2], acc[i], 0, 0, 0);
-    acc[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[1], tb[0], acc[i], 0, 0, 0);
-    acc[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[0], tb[1], acc[i], 0, 0, 0);
-    acc[i] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wf[0], tb[0], acc[i], 0, 0, 0);
-  }
 }
 
 template <int NW>
 constexpr int cf16_lds(bool lc) { return 3 * 16 * NW * XS + 2 * XIMG_F + (lc ? LC16IMG_F : 0); }
 static_assert(cf16_lds<8>(true) * 4 + 16 <= 160 * 1024, "chain fwd16 + LC LDS");
 
-// GR: halo rows cross tiles as tagged granules (8-B {value, tag} stores, polled by the consumer)
-// instead of sc1 rows + drain + barrier + flag: the producer's halo is out as soon as its stores land
-template <int NW, bool LC, int CM, bool TR, bool GR>
+template <int NW, bool LC, int CM, bool TR>
 __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
   constexpr int TP = 16 * NW, NT = 64 * NW;
   constexpr int IMGF = XIMG_F;
@@ -1101,7 +1061,6 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
   const int i16 = lane & 15, g = lane >> 4, q0 = 2 * (g >> 1), h = g & 1;
   const int r = 16 * w + i16;  // this lane's row of the tile
   const int tps = (a.T + TP - 1) / TP, ntiles = a.B * tps;
-  const unsigned ep1024 = GR ? lbwn_chain_epoch * 1024u : 0u;
   if (tid == 0) s_fail = 0;
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int b = tile / tps, tt = tile % tps, t0 = tt * TP;
@@ -1113,14 +1072,16 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
     const int myid = (a.gc_tab && valid) ? a.ids[m] : 0;
     floatx4 cv[4];
     load_cond16<CM>(a, 0, myid, m, valid && has_cond, q0, h, cv);
-    floatx4 lcv[5];   // LC: this lane's LC input row, k = 32s + 8g + 0..7 (s < 2), 64 + 4g + 0..3 (zero past n_lc_out)
+    floatx4 lcv[6];   // LC: this lane's LC input row, k = 32s + 8g + 0..7 (zero past n_lc_out)
     if (LC) {
       const float* lrow = a.lcact + ((long)b * a.T + min(t, a.T - 1)) * a.Lo;
 #pragma unroll
-      for (int q = 0; q < 5; ++q) {
-        const int k0 = q < 4 ? 32 * (q >> 1) + 8 * g + 4 * (q & 1) : 64 + 4 * g;
-        lcv[q] = *(const floatx4*)(lrow + min(k0, a.Lo - 4));       // clamped, then select
-        if (k0 >= a.Lo) lcv[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int s2 = 0; s2 < 3; ++s2) {
+        const int k0 = 32 * s2 + 8 * g;
+        lcv[2 * s2] = *(const floatx4*)(lrow + min(k0, a.Lo - 4));       // clamped, then select
+        lcv[2 * s2 + 1] = *(const floatx4*)(lrow + min(k0 + 4, a.Lo - 4));
+        if (k0 >= a.Lo) lcv[2 * s2] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (k0 + 4 >= a.Lo) lcv[2 * s2 + 1] = floatx4{0.f, 0.f, 0.f, 0.f};
       }
     }
     __syncthreads();  // previous tile's LDS use done
@@ -1180,8 +1141,7 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
       FSTAMP(1);
       // wait for the producer of the halo rows
       const int ptt = tt - max(1, d / TP);
-      const bool handoff = l > 0 && ptt >= 0;
-      if (!GR && handoff) {
+      if (l > 0 && ptt >= 0) {
         if (tid == 0 && !s_fail) {
           if (!wait_flag_ge(a.flags + (long)b * tps + ptt, (unsigned)l, a.status, 1u)) s_fail = 1;
         }
@@ -1193,43 +1153,10 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc(xl, (short)0, (int)((long)(a.H + a.T) * 32 * 4), BUF_DW3);
         floatx4 hv[NR];
-        if (GR && handoff) {
-          // poll this thread's granules of the producer tile's rows until every tag is layer l's
-          const unsigned tag = ep1024 + (unsigned)l;
-          const unsigned long long* src = a.hog + ((long)l * ntiles + (long)b * tps + ptt) * TP * 32;
-          long long t_start = 0;
-          for (unsigned spins = 1;; ++spins) {
-            bool ok = true;
 #pragma unroll
-            for (int i = 0; i < NR; ++i) {
-              const int e = min(tid + NT * i, nh * 8 - 1), row = e >> 3, c4 = (e & 7) * 4;
-              const int srow = t0 - d + row - ptt * TP;
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                const unsigned long long x = __hip_atomic_load(src + srow * 32 + c4 + j, __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT);
-                hv[i][j] = __uint_as_float((unsigned)x);
-                ok &= (unsigned)(x >> 32) == tag;
-              }
-            }
-            if (ok) break;
-            if ((spins & 15) == 0) {
-              const long long now = wall_clock64();
-              if (t_start == 0) t_start = now;
-              else if (now - t_start > SPIN_TIMEOUT || s_fail) {
-                __hip_atomic_fetch_or((gu32*)a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_fail = 1;
-                break;
-              }
-            }
-            __builtin_amdgcn_s_sleep(1);
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < NR; ++i) {
-            const int e = min(tid + NT * i, nh * 8 - 1), row = e >> 3, c4 = (e & 7) * 4;
-            hv[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((a.H + t0 + row - d) * 32 + c4) * 4, 0, 16);
-          }
+        for (int i = 0; i < NR; ++i) {
+          const int e = min(tid + NT * i, nh * 8 - 1), row = e >> 3, c4 = (e & 7) * 4;
+          hv[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((a.H + t0 + row - d) * 32 + c4) * 4, 0, 16);
         }
         if (!DMAIMG) {
           const floatx4* src = (const floatx4*)(wsrc + (long)min(l + 2, a.L - 1) * IMGF);
@@ -1285,30 +1212,12 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
             __builtin_amdgcn_make_buffer_rsrc(xn, (short)0, (int)((long)(a.H + a.T) * 32 * 4), BUF_DW3);
         float* nrow = nxt + r * XS;
         const bool halo_row = r >= TP - min(1 << ((l + 1) % a.nbl), TP);
-        if (GR) {
-          // halo rows as tagged granules for the consumer tiles (no drain, no flag), every row plain
-          // into X (read after the launch: backward, SAVE)
-          unsigned long long* dst = a.hog + ((long)(l + 1) * ntiles + tile) * TP * 32 + r * 32;
-          const unsigned long long tg = (unsigned long long)(ep1024 + (unsigned)(l + 1)) << 32;
 #pragma unroll
-          for (int rb = 0; rb < 2; ++rb) {
-            *(floatx4*)(nrow + 16 * rb + 4 * g) = accr[rb];
-            if (valid) __builtin_amdgcn_raw_buffer_store_b128(accr[rb], rn, ((a.H + t) * 32 + 16 * rb + 4 * g) * 4, 0, 0);
-            if (valid && halo_row) {
-#pragma unroll
-              for (int j = 0; j < 4; ++j)
-                __hip_atomic_store(dst + 16 * rb + 4 * g + j, tg | __float_as_uint(accr[rb][j]), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            }
-          }
-        } else {
-#pragma unroll
-          for (int rb = 0; rb < 2; ++rb) {
-            *(floatx4*)(nrow + 16 * rb + 4 * g) = accr[rb];
-            const int off = ((a.H + t) * 32 + 16 * rb + 4 * g) * 4;
-            if (valid && halo_row) __builtin_amdgcn_raw_buffer_store_b128(accr[rb], rn, off, 0, 16);
-            if (valid && !halo_row) __builtin_amdgcn_raw_buffer_store_b128(accr[rb], rn, off, 0, 0);
-          }
+        for (int rb = 0; rb < 2; ++rb) {
+          *(floatx4*)(nrow + 16 * rb + 4 * g) = accr[rb];
+          const int off = ((a.H + t) * 32 + 16 * rb + 4 * g) * 4;
+          if (valid && halo_row) __builtin_amdgcn_raw_buffer_store_b128(accr[rb], rn, off, 0, 16);
+          if (valid && !halo_row) __builtin_amdgcn_raw_buffer_store_b128(accr[rb], rn, off, 0, 0);
         }
         FSTAMP(8);
         // the next layer's own tap from the row this wave's lanes just wrote (wave-local)
@@ -1320,14 +1229,12 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
         if (LC) lc16_terms(LCIu, lcv, i16, g, acc);
       }
       FSTAMP(5);
-      // publish x_{l+1}: every wave drains its stores, barrier, one lane signals (GR: the granules
-      // are the hand-off; the barrier only retires this layer's reads of IMG[l&1] / LC before
-      // they are overwritten, and the drain only lands the LDS-DMA pieces / image prefetch)
-      if (!GR || DMAIMG || LC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // publish x_{l+1}: every wave drains its stores, barrier, one lane signals
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       FSTAMP(9);
       __syncthreads();
       FSTAMP(10);
-      if (!GR && tid == 0 && l + 1 < a.L) publish_flag(a.flags + tile, (unsigned)(l + 1));
+      if (tid == 0 && l + 1 < a.L) publish_flag(a.flags + tile, (unsigned)(l + 1));
       if (LC && l + 2 < a.L) dma_lc16_image<NW>(a.lcimg, l + 2, LCI, w, lane);
       if (DMAIMG && l + 2 < a.L) {
         const float* src = wsrc + (long)(l + 2) * IMGF + lane * 4;
@@ -1437,9 +1344,6 @@ struct ChainBK {
   // bf16-split form (chain_bwd_x3_kernel): z rows (row stride lddz), σ rows [L][M][32], images
   const float* Zf; const float* SG; long sgls; const float* bimg;
   int* tile_gid;               // GC: per tile its uniform voice id or -1 (x3 chain), or null
-  // granule hand-off (chain_bwd16_kernel<..., GR>): out_c0 rows r < min(d, TP) of each (layer,
-  // tile) as {value, tag} words [L][ntiles][TP][32], tag = epoch·1024 + 512 + l
-  unsigned long long* hogb;
 };
 
 // dv rows of wave w's 32 positions (DV, position-major) scatter-added into the GC gradient
@@ -1853,11 +1757,7 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
 // of the dv registers used as the B operand; then Rs f32 [c][XS] for the dz product.  Padded to
 // a whole number of 1-KiB DMA pieces.
 constexpr int BD_US = 2 * 32 * XW_ROW;
-// + RSX (bf16 units, after Rs): the split residual image of chain_bwd16_kernel's dz product,
-// [z channel][plane][kk] in rows of XR_ROW, kk = 8g + e holding g channel (e < 4 ? 4g + e :
-// 16 + 4g + e - 4): the k order of the lane's g values (N layout) as the 16x16x32 B operand
-constexpr int RSX_OFF = BD_US + 2 * 32 * XS;                       // bf16 offset of RSX
-constexpr int BIMG_F = (RSX_OFF / 2 + 32 * XR_ROW / 2 + 255) / 256 * 256;   // 9216 floats (36 pieces)
+constexpr int BIMG_F = (BD_US / 2 + 32 * XS + 255) / 256 * 256;   // 7680 floats
 constexpr int CBX_LDS = BIMG_F + 7 * LP * 32 + 8 * 96;            // IMG | Xp Xc ZT | DVs DVg G OC | part
 static_assert(CBX_LDS * 4 + 16 <= 160 * 1024, "chain bwd x3 LDS");
 
@@ -1889,23 +1789,7 @@ LBWN_DEV void pack_bx3_body(int l, const float* sig, const float* gate, const fl
     const int c = e / XS, o = e % XS;
     rs[e] = (c < Cd && o < Cr) ? wr[c * Cr + o] : 0.f;
   }
-  unsigned short* rsx = (unsigned short*)img + RSX_OFF;
-  for (int e = threadIdx.x; e < 32 * 16; e += blockDim.x) {
-    const int zc = e >> 4, kk = 2 * (e & 15), gg = kk >> 3, e0 = kk & 7;
-    floatx2 x = {0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int ee = e0 + u, c = ee < 4 ? 4 * gg + ee : 16 + 4 * gg + ee - 4;
-      if (zc < Cd && c < Cr) x[u] = wr[zc * Cr + c];
-    }
-    unsigned hi, mi, lo;
-    split2(x, hi, mi, lo);
-    unsigned short* row = rsx + zc * XR_ROW + kk;
-    *(unsigned*)(row) = hi;
-    *(unsigned*)(row + 32) = mi;
-    *(unsigned*)(row + 64) = lo;
-  }
-  for (int e = RSX_OFF / 2 + 32 * XR_ROW / 2 + threadIdx.x; e < BIMG_F; e += blockDim.x) img[e] = 0.f;
+  for (int e = BD_US / 2 + 32 * XS + threadIdx.x; e < BIMG_F; e += blockDim.x) img[e] = 0.f;
 }
 
 __global__ void pack_layers_x3_kernel(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
@@ -2240,9 +2124,9 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
             dg[s2][j] = DVg[CONF(32) ? p * 32 : swz(p, pi)];
           }
         XSTAMP(8);
-        if (l > 0) {   // image pieces w, w+4, ... (36 of 1 KiB)
+        if (l > 0) {   // image pieces w, w+4, ... (30 of 1 KiB)
 #pragma unroll
-          for (int i = 0; i < (BIMG_F / 256 + 3) / 4; ++i) {
+          for (int i = 0; i < 8; ++i) {
             const int pc = w + 4 * i;
             if (pc < BIMG_F / 256 && !CONF(1024)) dma16(isrc + pc * 256, IMG + pc * 256);
           }
@@ -2363,16 +2247,6 @@ constexpr int cb16_lds() { return BIMG_F + 3 * 16 * NW * 32 + 4 * 16 * NW * XS +
 static_assert(cb16_lds<8>() * 4 + 16 <= 160 * 1024, "chain bwd16 LDS");
 static_assert(8 * 1280 <= 3 * 128 * 32, "bwd16: the partial scratch must fit in Xp | Xc | ZT");
 
-// Σ over the 16 lanes of a DPP row (lanes 16k .. 16k+15): quad xor 1, xor 2, half-row mirror, row
-// mirror; every lane of the row ends with the row total (a fixed tree: deterministic)
-LBWN_DEV float row16_sum(float v) {
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, true));
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, true));
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, true));
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, true));
-  return v;
-}
-
 // GC rows of a wave whose 16 positions are not one voice: dv column sums per run of equal ids,
 // one atomic per run and column (as gc_scatter_x3, 16 positions)
 LBWN_DEV void gc_scatter16(float* gtab, long ld, const float* DVs, const float* DVg, int w, int lane, int Cd,
@@ -2393,8 +2267,7 @@ LBWN_DEV void gc_scatter16(float* gtab, long ld, const float* DVs, const float* 
   }
 }
 
-// GR: out_c0 rows cross tiles as tagged granules (no sc1 rows, drain-before-flag or flag)
-template <int NW, bool TR, bool GR>
+template <int NW, bool TR>
 __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
   constexpr int TP = 16 * NW, NT = 64 * NW, NH = NW / 4, PH = TP / NH;   // PH: positions per half
   constexpr int NR = TP * 8 / NT;                                        // float4 per thread of a tile (2)
@@ -2416,7 +2289,6 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
   const int r = 16 * w + i16;
   const int tps = (a.T + TP - 1) / TP, ntiles = a.B * tps;
   const int oc_bytes = (int)std::min<long>(a.ocls * 4, 0x7fffffffL);
-  const unsigned ep1024 = GR ? lbwn_chain_epoch * 1024u : 0u;
   if (tid == 0) s_fail = 0;
   for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
     const int tile = ntiles - 1 - it;
@@ -2463,58 +2335,21 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
       // 1. G = dx_{l+1} rows: out_c0_{l+1}[t + dn] (own OC / the producer's published rows) + out_a
       if (dn) {
         const int ptt = tt + max(1, dn / TP);
-        if (!GR && ptt < tps) {
+        if (ptt < tps) {
           if (tid == 0 && !s_fail) {
             if (!wait_flag_ge(a.flags + (long)b * tps + ptt, (unsigned)(a.L - l - 1), a.status, 2u)) s_fail = 1;
           }
           __syncthreads();
         }
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)(l + 1) * a.ocls, (short)0, oc_bytes, BUF_DW3);
         floatx4 gl[NR], go[NR];
-        if (GR) {
-          // rows of the producer tile (sr >= TP, inside T): poll their granules until layer l+1's tag
-          const unsigned tag = ep1024 + 512u + (unsigned)(l + 1);
-          const unsigned long long* src = a.hogb + ((long)(l + 1) * ntiles + (long)b * tps + min(ptt, tps - 1)) * TP * 32;
 #pragma unroll
-          for (int i = 0; i < NR; ++i) {
-            const int e = tid + NT * i, row = e >> 3, c4 = (e & 7) * 4, sr = row + dn;
-            go[i] = *(const floatx4*)(OC + min(sr, TP - 1) * XS + c4);
-            gl[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-            if (sr >= TP && t0 + sr < a.T) {
-              const int srow = t0 + sr - ptt * TP;
-              long long t_start = 0;
-              for (unsigned spins = 1;; ++spins) {
-                bool ok = true;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                  const unsigned long long x =
-                      __hip_atomic_load(src + srow * 32 + c4 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                  gl[i][j] = __uint_as_float((unsigned)x);
-                  ok &= (unsigned)(x >> 32) == tag;
-                }
-                if (ok) break;
-                if ((spins & 15) == 0) {
-                  const long long now = wall_clock64();
-                  if (t_start == 0) t_start = now;
-                  else if (now - t_start > SPIN_TIMEOUT || s_fail) {
-                    __hip_atomic_fetch_or((gu32*)a.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    s_fail = 1;
-                    break;
-                  }
-                }
-                __builtin_amdgcn_s_sleep(1);
-              }
-            }
-          }
-        } else {
-          const __amdgpu_buffer_rsrc_t rs =
-              __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)(l + 1) * a.ocls, (short)0, oc_bytes, BUF_DW3);
-#pragma unroll
-          for (int i = 0; i < NR; ++i) {
-            const int e = tid + NT * i, row = e >> 3, c4 = (e & 7) * 4, sr = row + dn;
-            const int ts = min(t0 + sr, a.T - 1);
-            gl[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
-            go[i] = *(const floatx4*)(OC + min(sr, TP - 1) * XS + c4);
-          }
+        for (int i = 0; i < NR; ++i) {
+          const int e = tid + NT * i, row = e >> 3, c4 = (e & 7) * 4, sr = row + dn;
+          const int ts = min(t0 + sr, a.T - 1);
+          gl[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
+          go[i] = *(const floatx4*)(OC + min(sr, TP - 1) * XS + c4);
         }
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
@@ -2549,25 +2384,27 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         gv[xb] = v;
         *(floatx4*)gp = v;
       }
-      // 2. dz = dZ + RES·g on 16x16x32 splits: B = the lane's g values (k = 8g + e, RSX's k order),
-      //    A = RSX rows ch16(b, i16); the x / z row DMA pieces go out between the two blocks
+      // 2. dz = dZ + RES·g  (f32 MFMA 16x16x4: k = g's channel 16xb + 4g + rr)
       floatx4 dz[2];
       {
-        const unsigned short* RX = (const unsigned short*)IMG + RSX_OFF;
-        bf16x8 gb[3];
+        floatx4 rx[2][2];
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+          for (int xb = 0; xb < 2; ++xb) rx[bb][xb] = *(const floatx4*)(Rs + ch16(bb, i16) * XS + 16 * xb + 4 * g);
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) dz[bb] = valid ? dzr[bb] : floatx4{0.f, 0.f, 0.f, 0.f};
-        split8(gv[0], gv[1], gb);
 #pragma unroll
-        for (int bb = 0; bb < 2; ++bb) {
-          bf16x8 af[3];
+        for (int xb = 0; xb < 2; ++xb) {
 #pragma unroll
-          for (int p = 0; p < 3; ++p) af[p] = *(const bf16x8*)(RX + ch16(bb, i16) * XR_ROW + 32 * p + 8 * g);
-          dz[bb] = mfma16x3(af, gb, dz[bb]);
+          for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb)
+              dz[bb] = __builtin_amdgcn_mfma_f32_16x16x4f32(rx[bb][xb][rr], gv[xb][rr], dz[bb], 0, 0, 0);
           // x / z rows of this layer: pieces k = w, w + NW, ... (3·TP/8 rows of 8 over the block)
 #pragma unroll
           for (int k2 = 0; k2 < TP / 8 / NW / 2 + 1; ++k2) {
-            const int k = w + NW * (2 * k2 + bb);
+            const int k = w + NW * (2 * k2 + xb);
             if (k < TP / 8) dma_rows3(k);
           }
         }
@@ -2593,30 +2430,6 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
           if (dvo) {
             *(floatx4*)(dvo + c) = dvs[bb];
             *(floatx4*)(dvo + 32 + c) = dvg[bb];
-          }
-        }
-      }
-      // bias partials: column sums of dv (sig, gate) and g over this wave's 16 positions from the
-      // lanes' own registers (DPP row sums across the 16 position lanes), one part per wave, read
-      // after step 8's barrier (waves 0-2 re-reading 128 LDS rows each there, with the others
-      // idle at the barrier, took ~3k cycles per layer)
-      {
-        floatx4 ss[2], sgt[2], sx[2];
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            ss[bb][e] = row16_sum(dvs[bb][e]);
-            sgt[bb][e] = row16_sum(dvg[bb][e]);
-            sx[bb][e] = row16_sum(gv[bb][e]);
-          }
-        if (i16 == 0) {
-          float* pw = part + w * 96;
-#pragma unroll
-          for (int bb = 0; bb < 2; ++bb) {
-            *(floatx4*)(pw + 8 * (q0 + bb) + 4 * h) = ss[bb];
-            *(floatx4*)(pw + 32 + 8 * (q0 + bb) + 4 * h) = sgt[bb];
-            *(floatx4*)(pw + 64 + 16 * bb + 4 * g) = sx[bb];
           }
         }
       }
@@ -2647,18 +2460,10 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         const __amdgpu_buffer_rsrc_t rw =
             __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)l * a.ocls, (short)0, oc_bytes, BUF_DW3);
         const bool pub = l > 0 && valid && r < min(d, TP);
-        unsigned long long* hdst = GR ? a.hogb + ((long)l * ntiles + tile) * TP * 32 + r * 32 : nullptr;
-        const unsigned long long htag = (unsigned long long)(ep1024 + 512u + (unsigned)l) << 32;
 #pragma unroll
         for (int xb = 0; xb < 2; ++xb) {
           *(floatx4*)(OC + r * XS + 16 * xb + 4 * g) = acc_c[xb];
-          if (GR && pub) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              __hip_atomic_store(hdst + 16 * xb + 4 * g + j, htag | __float_as_uint(acc_c[xb][j]), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-          }
-          if (!GR && pub) __builtin_amdgcn_raw_buffer_store_b128(acc_c[xb], rw, (int)((m * 32 + 16 * xb + 4 * g) * 4), 0, 16);
+          if (pub) __builtin_amdgcn_raw_buffer_store_b128(acc_c[xb], rw, (int)((m * 32 + 16 * xb + 4 * g) * 4), 0, 16);
         }
       }
       if (l == 0 && valid) {
@@ -2674,7 +2479,7 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
       // 5. publish out_c0_l (the drain also lands this layer's x / z DMA pieces)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // DV, G, OC, Xp/Xc/ZT complete; the weight image is dead
-      if (!GR && tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
+      if (tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
       if (a.gc_dtab && !tile_uni) gc_scatter16(a.gc_dtab + (long)l * 64, a.gc_ld, DVs, DVg, w, lane, 32, gc_starts, gc_pid);
       XSTAMP(4);
       // 6. dSIG / dGATE tile t4 = w & 3 (2·kind + tap) over this wave's position half:
@@ -2687,72 +2492,67 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         const float* XA = (t4 & 1) ? Xc : Xp;
         const float* DB = (t4 & 2) ? DVg : DVs;
         const int pi = lane & 31, hh = lane >> 5;
-        // k-steps in two groups of PH/32: the first group's operands are read before the DMA issue
-        // (its asm is a compiler barrier for LDS reads), the second group's after (all four up
-        // front held 64 registers and spilled)
-        constexpr int KG = PH / 32;
-        float xa[KG][8], db[KG][8];
-        auto rd = [&](int grp) {
+        float xa[PH / 16][8], db[PH / 16][8];
 #pragma unroll
-          for (int s2 = 0; s2 < KG; ++s2)
+        for (int s2 = 0; s2 < PH / 16; ++s2)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const int p = p0 + 16 * (KG * grp + s2) + 8 * hh + e;
-              xa[s2][e] = XA[p * 32 + pi];
-              db[s2][e] = DB[p * XS + pi];
-            }
-        };
-        auto ks = [&]() {
-#pragma unroll
-          for (int s2 = 0; s2 < KG; ++s2) {
-            bf16x8 fx[3], fd[3];
-            split8(floatx4{xa[s2][0], xa[s2][1], xa[s2][2], xa[s2][3]}, floatx4{xa[s2][4], xa[s2][5], xa[s2][6], xa[s2][7]}, fx);
-            split8(floatx4{db[s2][0], db[s2][1], db[s2][2], db[s2][3]}, floatx4{db[s2][4], db[s2][5], db[s2][6], db[s2][7]}, fd);
-            accT = mfma_x3(fx, fd, accT);
+          for (int e = 0; e < 8; ++e) {
+            const int p = p0 + 16 * s2 + 8 * hh + e;
+            xa[s2][e] = XA[p * 32 + pi];
+            db[s2][e] = DB[p * XS + pi];
           }
-        };
-        rd(0);
         XSTAMP(8);
         if (l > 0) {   // the next layer's image and rows, behind this layer's operand reads
           dma_image(l - 1);
           load_regs(l - 1);
         }
         XSTAMP(9);
-        ks();
-        XSTAMP(10);
-        rd(1);
-        ks();
+#pragma unroll
+        for (int s2 = 0; s2 < PH / 16; ++s2) {
+          bf16x8 fx[3], fd[3];
+          split8(floatx4{xa[s2][0], xa[s2][1], xa[s2][2], xa[s2][3]}, floatx4{xa[s2][4], xa[s2][5], xa[s2][6], xa[s2][7]}, fx);
+          split8(floatx4{db[s2][0], db[s2][1], db[s2][2], db[s2][3]}, floatx4{db[s2][4], db[s2][5], db[s2][6], db[s2][7]}, fd);
+          accT = mfma_x3(fx, fd, accT);
+          if (s2 == 0) XSTAMP(10);
+        }
       }
       XSTAMP(5);
       // 7. dRES quarter t4 (16x16: z channels 16(t4>>1).., res out 16(t4&1)..) over the same
-      //    positions on 16x16x32 splits (k = 32 positions): A[i=c][k=pos] = z[pos][c], B[k=pos][j=o] =
-      //    g[pos][o], each lane's 8 positions 8g..8g+7 of the k-step
+      //    positions on v_mfma_f32_16x16x4_f32: A[i=c][k=pos] = z[pos][c], B[k=pos][j=o] = g[pos][o]
       floatx4 accR = {0.f, 0.f, 0.f, 0.f};
       {
         const int cz = 16 * (t4 >> 1) + i16, og = 16 * (t4 & 1) + i16;
 #pragma unroll
         for (int c8 = 0; c8 < PH / 32; ++c8) {
-          floatx4 za[2], ga[2];
+          float za[8], ga[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const int p = p0 + 32 * c8 + 8 * g + e;
-            za[e >> 2][e & 3] = ZT[p * 32 + cz];
-            ga[e >> 2][e & 3] = G[p * XS + og];
+            const int p = p0 + 32 * c8 + 4 * e + g;
+            za[e] = ZT[p * 32 + cz];
+            ga[e] = G[p * XS + og];
           }
-          bf16x8 fz[3], fg[3];
-          split8(za[0], za[1], fz);
-          split8(ga[0], ga[1], fg);
-          accR = mfma16x3(fz, fg, accR);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) accR = __builtin_amdgcn_mfma_f32_16x16x4f32(za[e], ga[e], accR, 0, 0, 0);
         }
       }
       XSTAMP(11);
-      // 8. bias partials: the per-wave column sums were parked in part (step 3)
+      // 8. bias partials (column sums of DVs, DVg, G: waves 0-2; lane = (row class pc, 4-column
+      //    group c4), rows pc + 8p)
       float* slab = a.slab + ((long)l * ntiles + tile) * SLAB;
+      if (w < 3) {
+        const int c4 = (lane & 7) * 4, pc = lane >> 3;
+        const float* pl = w == 0 ? DVs : w == 1 ? DVg : G;
+        floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < TP / 8; ++p) s4 += *(const floatx4*)(pl + (pc + 8 * p) * XS + c4);
+        *(floatx4*)(part + pc * 96 + 32 * w + c4) = s4;
+      }
       __syncthreads();   // every read of Xp/Xc/ZT/DV/G of this layer is done; part complete
       if (tid < 96) {
         float s1 = 0.f;
 #pragma unroll
-        for (int pw = 0; pw < NW; ++pw) s1 += part[pw * 96 + tid];
+        for (int pc = 0; pc < 8; ++pc) s1 += part[pc * 96 + tid];
         slab[5120 + tid] = s1;
       }
       XSTAMP(12);
@@ -3197,20 +2997,15 @@ static void fwd_launch(bool traced, void (*plain)(ChainFK), void (*traced_k)(Cha
 }
 
 // the 16-position-wave forward chain of NW waves (64·NW threads), by LC / conditioning mode
-template <int NW, bool GR>
-static void launch_fwd16_g(bool tr, bool lc, int cm, int grid, const ChainFK& k, hipStream_t st) {
-  void (*f)(ChainFK);
-  if (lc) f = cm == 0 ? (tr ? chain_fwd16_kernel<NW, true, 0, true, GR> : chain_fwd16_kernel<NW, true, 0, false, GR>)
-                      : (tr ? chain_fwd16_kernel<NW, true, 1, true, GR> : chain_fwd16_kernel<NW, true, 1, false, GR>);
-  else if (cm == 0) f = tr ? chain_fwd16_kernel<NW, false, 0, true, GR> : chain_fwd16_kernel<NW, false, 0, false, GR>;
-  else if (cm == 1) f = tr ? chain_fwd16_kernel<NW, false, 1, true, GR> : chain_fwd16_kernel<NW, false, 1, false, GR>;
-  else f = tr ? chain_fwd16_kernel<NW, false, 2, true, GR> : chain_fwd16_kernel<NW, false, 2, false, GR>;
-  hipLaunchKernelGGL(f, dim3(grid), dim3(64 * NW), 0, st, k);
-}
 template <int NW>
 static void launch_fwd16(bool tr, bool lc, int cm, int grid, const ChainFK& k, hipStream_t st) {
-  if (k.hog) launch_fwd16_g<NW, true>(tr, lc, cm, grid, k, st);
-  else launch_fwd16_g<NW, false>(tr, lc, cm, grid, k, st);
+  void (*f)(ChainFK);
+  if (lc) f = cm == 0 ? (tr ? chain_fwd16_kernel<NW, true, 0, true> : chain_fwd16_kernel<NW, true, 0, false>)
+                      : (tr ? chain_fwd16_kernel<NW, true, 1, true> : chain_fwd16_kernel<NW, true, 1, false>);
+  else if (cm == 0) f = tr ? chain_fwd16_kernel<NW, false, 0, true> : chain_fwd16_kernel<NW, false, 0, false>;
+  else if (cm == 1) f = tr ? chain_fwd16_kernel<NW, false, 1, true> : chain_fwd16_kernel<NW, false, 1, false>;
+  else f = tr ? chain_fwd16_kernel<NW, false, 2, true> : chain_fwd16_kernel<NW, false, 2, false>;
+  hipLaunchKernelGGL(f, dim3(grid), dim3(64 * NW), 0, st, k);
 }
 
 int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
@@ -3226,9 +3021,7 @@ int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   k.ximg = c.wpack_x3;
   k.SG = c.SG; k.sgls = c.sgls;
   k.lcact = c.lcact; k.lcimg = c.lcimg; k.Lo = c.Lo;
-  k.hog = c.fwd_nw ? c.hog : nullptr;
   LBWN_REQUIRE(!c.wpack_x3 || (((uintptr_t)c.wpack_x3) & 15) == 0, "chain fwd: split images not 16-B aligned");
-  LBWN_REQUIRE(!k.hog || c.L < 1024, "chain fwd: granule hand-off tags need L < 1024");
   const bool lc = c.lcimg != nullptr;
   if (lc)
     LBWN_REQUIRE(c.wpack_x3 && c.lcact && !c.cond && c.Lo > 16 * (LC_K - 1) && c.Lo <= LC_KP && c.Lo % 4 == 0 &&
@@ -3287,23 +3080,12 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
     if (int e = lbwn_zero_launch(c.flags, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st)) return e;
   }
   LBWN_REQUIRE(x3 == (c.dzls > 0), "chain bwd: the bf16-split chain reads dZ in chain order (dzls), the f32 chain in rows");
-  k.hogb = c.bwd_nw ? c.hogb : nullptr;
   if (c.bwd_nw == 8) {
-    if (k.hogb) {
-      if (k.trace) chain_bwd16_kernel<8, true, true><<<c.grid, 512, 0, st>>>(k);
-      else chain_bwd16_kernel<8, false, true><<<c.grid, 512, 0, st>>>(k);
-    } else {
-      if (k.trace) chain_bwd16_kernel<8, true, false><<<c.grid, 512, 0, st>>>(k);
-      else chain_bwd16_kernel<8, false, false><<<c.grid, 512, 0, st>>>(k);
-    }
+    if (k.trace) chain_bwd16_kernel<8, true><<<c.grid, 512, 0, st>>>(k);
+    else chain_bwd16_kernel<8, false><<<c.grid, 512, 0, st>>>(k);
   } else if (c.bwd_nw == 4) {
-    if (k.hogb) {
-      if (k.trace) chain_bwd16_kernel<4, true, true><<<c.grid, 256, 0, st>>>(k);
-      else chain_bwd16_kernel<4, false, true><<<c.grid, 256, 0, st>>>(k);
-    } else {
-      if (k.trace) chain_bwd16_kernel<4, true, false><<<c.grid, 256, 0, st>>>(k);
-      else chain_bwd16_kernel<4, false, false><<<c.grid, 256, 0, st>>>(k);
-    }
+    if (k.trace) chain_bwd16_kernel<4, true><<<c.grid, 256, 0, st>>>(k);
+    else chain_bwd16_kernel<4, false><<<c.grid, 256, 0, st>>>(k);
   } else if (x3 && k.trace) chain_bwd_x3_kernel<true><<<c.grid, 256, 0, st>>>(k);
   else if (x3) chain_bwd_x3_kernel<false><<<c.grid, 256, 0, st>>>(k);
   else chain_bwd_kernel<<<c.grid, 256, 0, st>>>(k);
@@ -3324,23 +3106,6 @@ int lbwn_layer_reduce_all_launch(const lbwn_layer_red_args& r, int L, long slab_
 }
 
 int lbwn_slab_floats() { return SLAB; }
-
-namespace {
-__global__ void step_begin_kernel(unsigned* p, long n) {
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) p[e] = 0u;
-  if (blockIdx.x == 0 && threadIdx.x == 0) lbwn_chain_epoch = lbwn_chain_epoch + 1u;
-}
-}  // namespace
-
-// The training step's first launch: zero the status word and the chains' flag blocks (n_bytes) and
-// advance the granule hand-offs' epoch (one kernel: the step's launch gaps cost ~2 us each)
-int lbwn_step_begin_launch(void* words, size_t n_bytes, hipStream_t st) {
-  LBWN_REQUIRE(n_bytes % 4 == 0, "step begin: byte count must be a multiple of 4");
-  const long n = (long)(n_bytes / 4);
-  step_begin_kernel<<<(int)std::max<long>(1, std::min<long>((n + 255) / 256, 1024)), 256, 0, st>>>((unsigned*)words, n);
-  LBWN_CHECK_LAUNCH();
-  return 0;
-}
 
 namespace {
 // gtab[id][l·64 + c] += Σ over tiles with tile_gid == id (in tile order) of the tile's dv column

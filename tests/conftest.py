@@ -30,16 +30,11 @@ def lib():
     return _lib.load()
 
 
-@pytest.fixture(params=['w32', '128', '64', '128:w32', '128+gran'])
+@pytest.fixture(params=['w32', '128', '64', '128:w32'])
 def chain_tile(request, monkeypatch):
     """The chains' form (LBWN_CHAIN_TILE = <fwd>[:<bwd>], read at plan creation): 'w32' =
     32-position waves on 128-position tiles (chain_fwd_kernel / chain_bwd_x3_kernel), '128' /
     '64' = 16-position waves on 128- / 64-position tiles (chain_fwd16_kernel / chain_bwd16_kernel
-    with 8 / 4 waves) -- the C4 tile axis; '128:w32' mixes the forms; '+gran' switches the
-    16-position chains' cross-tile hand-offs to tagged granules (LBWN_FWD_HANDOFF /
-    LBWN_BWD_HANDOFF=gran)."""
-    tile, _, handoff = request.param.partition('+')
-    monkeypatch.setenv('LBWN_CHAIN_TILE', tile)
-    monkeypatch.setenv('LBWN_FWD_HANDOFF', handoff or 'flag')
-    monkeypatch.setenv('LBWN_BWD_HANDOFF', handoff or 'flag')
+    with 8 / 4 waves) -- the C4 tile axis; '128:w32' mixes the forms."""
+    monkeypatch.setenv('LBWN_CHAIN_TILE', request.param)
     return request.param
