@@ -171,6 +171,7 @@ int lbwn_head_xent(float* logits, const int* wav_q, const int* ids, int B, int T
   lbwn_head_args h;
   h.logits = logits; h.q = wav_q; h.ids = ids; h.B = B; h.T = T; h.Q = Q; h.partial = partial_ws;
   h.write_grad = write_grad;
+  h.colpart = nullptr;
   int nb = 0;
   hipStream_t st = (hipStream_t)stream;
   if (int e = lbwn_head_launch(h, &nb, st)) return e;

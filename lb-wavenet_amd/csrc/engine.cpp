@@ -15,6 +15,7 @@
 #include "kernels.h"
 
 struct lbwn_plan {
+  int head_colparts = 0;   // post2-bias column partial rows the last forward's head wrote (0: none)
   lbwn_arch a;
   int B, T, L, nbl, H, Cr, Cd, Cs, Cp, Q;
   int Ge, ncat1, Li, Lo, nup, hop, up[8];   // conditioning (Ge = 0: no GC, Lo = 0: no LC)
@@ -712,7 +713,9 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   P = &Ppad;
   // the sticky status word (chain spin timeouts OR their codes in) lives for one step:
   // zeroed here, read by the host after the step (lbwn_plan_tensor "status")
-  if ((e = lbwn_zero_launch(at<char>(ws, p->oSTATUS), 16 + 2 * p->nflag_bytes, st))) return e;
+  // (in the fused prologue below when the bf16-split chains run)
+  const bool fused_pro = lbwn_gemm_mode() == 1 && p->chain;
+  if (!fused_pro && (e = lbwn_zero_launch(at<char>(ws, p->oSTATUS), 16 + 2 * p->nflag_bytes, st))) return e;
   p->bwd_flags_fresh = true;
   // the fused LC upsample depends only on the mel input and the upsample filters: it runs on
   // aux2 beside the weight packs, embedding, GC table and D-sep prepend, joined before the chain
@@ -750,34 +753,46 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   // per-layer images of the forward chain
   // ... and the backward chain's split images (dx weights + f32 residual image), one launch
   const bool lcx = lc_in_chain(p);
-  if (x3 && p->chain &&
-      (e = lbwn_pack_layers_fb_x3_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b,
-                                         at<unsigned short>(ws, p->oWPKX), at<float>(ws, p->oWPKB), L, Cr, Cd,
-                                         P->skip_b, p->Cs, bsum, P->lc_sig, P->lc_gate, p->Lo,
-                                         lcx ? at<unsigned short>(ws, p->oLCX) : nullptr, pst, p->fwd_nw != 0)))
-    return e;
-  const bool bsum_done = x3 && p->chain && P->skip_b;   // summed by the pack launch above
+  const bool bsum_done = x3 && p->chain && P->skip_b;   // summed by the pack (or prologue) launch
+  lbwn_prologue_args pa;
+  memset(&pa, 0, sizeof(pa));
   if (x3) {
     const float* wsrc[6] = {P->skip, P->post1, P->post2, P->post2, P->post1, P->skip};
-    const float* jw[6];
-    long jld[6];
-    int jr[6], jk[6], jt[6], nj = 0;
-    unsigned short* jo[6];
     for (int i = 0; i < 6; ++i) {
       if (!p->oW3[i]) continue;
       const W3Shape w = w3_shape(p, i);
-      jw[nj] = wsrc[i]; jld[nj] = w.ldw; jr[nj] = w.rows; jk[nj] = w.K; jt[nj] = w.trans;
-      jo[nj] = at<unsigned short>(ws, p->oW3[i]);
-      ++nj;
+      const int j = pa.njobs++;
+      pa.W[j] = wsrc[i]; pa.ldw[j] = w.ldw; pa.rows[j] = w.rows; pa.K[j] = w.K; pa.trans[j] = w.trans;
+      pa.out[j] = at<unsigned short>(ws, p->oW3[i]);
     }
-    if (nj && (e = lbwn_split_planes_launch(nj, jw, jld, jr, jk, jt, jo, pst))) return e;
   }
-  // one-hot·PRE + PRE_BIAS == row gather (tmodel.py:53-66, :86-102)
-  if ((e = lbwn_embed_launch(wav_q, P->pre, P->pre_b, X, B, T, H, Cr, p->Q, st))) return e;
+  if (fused_pro) {
+    // status word + flags, weight planes, both chains' images, embedding and D-sep prepend: one launch
+    pa.sig = P->sig; pa.gate = P->gate; pa.sig_b = P->sig_b; pa.gate_b = P->gate_b; pa.res = P->res; pa.res_b = P->res_b;
+    pa.fout = at<unsigned short>(ws, p->oWPKX); pa.bout = at<float>(ws, p->oWPKB);
+    pa.L = L; pa.Cr = Cr; pa.Cd = Cd; pa.skip_b = P->skip_b; pa.Cs = p->Cs; pa.bsum = bsum;
+    pa.lc_sig = P->lc_sig; pa.lc_gate = P->lc_gate; pa.Lo = p->Lo;
+    pa.lcout = lcx ? at<unsigned short>(ws, p->oLCX) : nullptr; pa.lc16 = p->fwd_nw != 0;
+    pa.q = wav_q; pa.pre = P->pre; pa.pre_b = P->pre_b; pa.X = X; pa.xls = p->x_layer_stride; pa.save = save;
+    pa.nbl = p->nbl; pa.B = B; pa.T = T; pa.H = H; pa.Q = p->Q;
+    pa.zero = at<char>(ws, p->oSTATUS); pa.zero_bytes = 16 + 2 * p->nflag_bytes;
+    if ((e = lbwn_step_prologue_launch(pa, st))) return e;
+  } else {
+    if (x3 && p->chain &&
+        (e = lbwn_pack_layers_fb_x3_launch(P->sig, P->gate, P->sig_b, P->gate_b, P->res, P->res_b,
+                                           at<unsigned short>(ws, p->oWPKX), at<float>(ws, p->oWPKB), L, Cr, Cd,
+                                           P->skip_b, p->Cs, bsum, P->lc_sig, P->lc_gate, p->Lo,
+                                           lcx ? at<unsigned short>(ws, p->oLCX) : nullptr, pst, p->fwd_nw != 0)))
+      return e;
+    if (pa.njobs && (e = lbwn_split_planes_launch(pa.njobs, pa.W, pa.ldw, pa.rows, pa.K, pa.trans, pa.out, pst)))
+      return e;
+    // one-hot·PRE + PRE_BIAS == row gather (tmodel.py:53-66, :86-102)
+    if ((e = lbwn_embed_launch(wav_q, P->pre, P->pre_b, X, B, T, H, Cr, p->Q, st))) return e;
+  }
   Cond cd;
   if ((e = cond_forward(p, P, ws, mel, cd, st))) return e;
   // D-separation prepend for every layer (tmodel.py:122-127)
-  if ((e = lbwn_dsep_prepend_launch(X, p->x_layer_stride, save, L, p->nbl, B, T, H, Cr, st))) return e;
+  if (!fused_pro && (e = lbwn_dsep_prepend_launch(X, p->x_layer_stride, save, L, p->nbl, B, T, H, Cr, st))) return e;
   if (p->chain) {
     // all layers in one persistent launch (tmodel.py:313-325)
     lbwn_chain_args c;
@@ -844,6 +859,10 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   lbwn_head_args h;
   h.logits = LOG; h.q = wav_q; h.ids = ids; h.B = B; h.T = T; h.Q = p->Q;
   h.partial = at<float>(ws, p->oHEADP); h.write_grad = 1;
+  // the post2 bias gradient's column partials from the head itself (bf16-split form, Q <= 512),
+  // summed in the backward by colsum_final: no colsum pass over dlogits
+  h.colpart = (lbwn_gemm_mode() == 1 && p->Q <= 512) ? at<float>(ws, p->oCOLS) : nullptr;
+  p->head_colparts = h.colpart ? lbwn_head_nblocks(M, true) : 0;
   int nb = 0;
   Probe(p, st, "head");
   if ((e = lbwn_head_launch(h, &nb, st))) return e;
@@ -930,19 +949,20 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
       float* fp[3];
       float* fo[3];
       int fn[3], fa[3] = {0, 0, 0}, np[3], nf = 0;
+      int rp[3] = {1, 1, 1};
       if (G->post2_b) {
-        int n0 = 0;
-        if ((e = lbwn_colsum_partial_launch(LOG, Q, (int)M, Q, COLS, &n0, st))) return e;
+        int n0 = p->head_colparts;   // written by this step's head
+        if (!n0 && (e = lbwn_colsum_partial_launch(LOG, Q, (int)M, Q, COLS, &n0, st))) return e;
         fp[nf] = COLS; fn[nf] = Q; fo[nf] = G->post2_b; np[nf] = n0; ++nf;
       }
       if (G->post1_b) { fp[nf] = CPART; fn[nf] = Cp; fo[nf] = G->post1_b; np[nf] = lbwn_colpart_parts(M); ++nf; }
-      if (G->skip_b) {
+      if (G->skip_b) {   // every layer's SKIP_BIAS row gets the same sum: L copies
         fp[nf] = CPART + (long)lbwn_colpart_parts(M) * Cp; fn[nf] = Cs; fo[nf] = G->skip_b;
-        np[nf] = lbwn_colpart_parts(M); ++nf;
+        np[nf] = lbwn_colpart_parts(M); rp[nf] = L; ++nf;
       }
-      if (nf && (e = lbwn_colsum_final_launch(nf, fp, fn, fo, fa, np, st))) return e;
+      if (nf && (e = lbwn_colsum_final_launch(nf, fp, fn, fo, fa, np, st, rp))) return e;
     }
-    if (G->skip_b && (e = lbwn_bcast_rows_launch(G->skip_b, L, Cs, st))) return e;
+    if (!fcols && G->skip_b && (e = lbwn_bcast_rows_launch(G->skip_b, L, Cs, st))) return e;
   }
   // weight gradients of the head GEMMs (dPOST2, dPOST1) on the main stream BEFORE the chain at
   // full rate: a chain block takes a whole CU's LDS, so nothing runs beside it, and side-stream

@@ -17,6 +17,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "prologue.h"
 
 namespace {
 
@@ -966,39 +967,9 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
   }
 }
 
-// Pre-split planes of weights W (f32, row stride ldw): out[r][kc][plane][32] = split of
-// W[r][32·kc + j] (k-contiguous, trans = 0) or W[32·kc + j][r] (trans = 1); k ≥ K is zero.
-// Up to 6 weights per launch (blockIdx.y = job).
-struct SplitJobs {
-  const float* W[6];
-  long ldw[6];
-  int rows[6], K[6], trans[6];
-  unsigned short* out[6];
-};
-__global__ void split_planes_kernel(SplitJobs jb) {
-  const int jj = blockIdx.y;
-  const float* __restrict__ W = jb.W[jj];
-  const long ldw = jb.ldw[jj];
-  const int rows = jb.rows[jj], K = jb.K[jj], trans = jb.trans[jj];
-  unsigned short* __restrict__ out = jb.out[jj];
-  const int kch = (K + X3_BK - 1) / X3_BK;
-  const long total = (long)rows * kch * (X3_BK / 2);   // pairs
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int j2 = (int)(e % (X3_BK / 2)) * 2;
-    const long rc = e / (X3_BK / 2);
-    const int kc = (int)(rc % kch), r = (int)(rc / kch);
-    const int k = kc * X3_BK + j2;
-    floatx2 x;
-    x[0] = k < K ? (trans ? W[(long)k * ldw + r] : W[(long)r * ldw + k]) : 0.f;
-    x[1] = k + 1 < K ? (trans ? W[(long)(k + 1) * ldw + r] : W[(long)r * ldw + k + 1]) : 0.f;
-    unsigned h, m, l;
-    split2(x, h, m, l);
-    unsigned* o = (unsigned*)(out + rc * (3 * X3_BK) + j2);
-    o[0] = h;
-    o[X3_BK / 2] = m;
-    o[X3_BK] = l;
-  }
-}
+// Pre-split planes of the weights (body and SplitJobs in prologue.h; blockIdx.y = job)
+static_assert(PLANE_BK == X3_BK, "pre-split chunk = GEMM k-step");
+__global__ void split_planes_kernel(SplitJobs jb) { split_planes_body(jb, blockIdx.y, blockIdx.x, gridDim.x); }
 
 }  // namespace
 

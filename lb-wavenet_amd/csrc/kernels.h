@@ -82,6 +82,36 @@ int lbwn_layer_image_x3_elems();
 // lbwn_pack_layers_x3_launch + lbwn_pack_layers_bx3_launch in one launch, plus (skip_b, bsum
 // non-null) bsum[n] = Σ_l skip_b[l·Cs + n] (lbwn_sum_bias_launch)
 // ... and (lcout non-null) the L split LC images of the in-chain LC term (lbwn_lc_image_x3_elems each)
+// The training step's start-of-step work in one launch (layer.hip step_prologue_kernel): the
+// arguments of lbwn_pack_layers_fb_x3_launch, lbwn_split_planes_launch (njobs 0..6),
+// lbwn_embed_launch, lbwn_dsep_prepend_launch and lbwn_zero_launch (zero_bytes may be 0).
+struct lbwn_prologue_args {
+  const float *sig, *gate, *sig_b, *gate_b, *res, *res_b;
+  unsigned short* fout;
+  float* bout;
+  int L, Cr, Cd;
+  const float* skip_b;
+  int Cs;
+  float* bsum;
+  const float *lc_sig, *lc_gate;
+  int Lo;
+  unsigned short* lcout;
+  int lc16;
+  int njobs;
+  const float* W[6];
+  long ldw[6];
+  int rows[6], K[6], trans[6];
+  unsigned short* out[6];
+  const int* q;
+  const float *pre, *pre_b;
+  float* X;
+  long xls;
+  const float* save;
+  int nbl, B, T, H, Q;
+  void* zero;
+  size_t zero_bytes;
+};
+int lbwn_step_prologue_launch(const lbwn_prologue_args& a, hipStream_t st);
 int lbwn_pack_layers_fb_x3_launch(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
                                   const float* res, const float* res_b, unsigned short* fout, float* bout, int L,
                                   int Cr, int Cd, const float* skip_b, int Cs, float* bsum, const float* lc_sig,
@@ -164,7 +194,9 @@ struct lbwn_head_args {
   int B, T, Q;
   float* partial;           // [nblocks][3] (sum_xent, n_valid, sum |argmax diff|)
   int write_grad;
+  float* colpart;           // nullable: [nblocks][Q] column sums of the dlogits written (Q <= 512)
 };
+int lbwn_head_nblocks(long M, bool colpart);
 int lbwn_head_launch(const lbwn_head_args& a, int* nblocks_out, hipStream_t st);
 int lbwn_stats_reduce_launch(const float* partial, int nparts, float* stats, hipStream_t st);
 
@@ -178,7 +210,8 @@ int lbwn_colsum_ws_floats(int M, int N);
 // N floats), and the second over any partials (first-pass ones or a GEMM epilogue's colpart)
 int lbwn_colsum_partial_launch(const float* X, long ldx, int M, int N, float* ws, int* nparts, hipStream_t st);
 int lbwn_colsum_final_launch(int njobs, float* const* parts, const int* N, float* const* out, const int* accumulate,
-                             const int* nparts, hipStream_t st);
+                             const int* nparts, hipStream_t st,
+                             const int* reps = nullptr);
 int lbwn_sum_bias_launch(const float* b, int L, int N, float* out, hipStream_t st);
 int lbwn_fill_launch(float* p, float v, long n, hipStream_t st);
 

@@ -12,8 +12,11 @@
 //   zᵀ = tanh(v_sig)·σ(v_gate);  x_{l+1}ᵀ = x_lᵀ + RESᵀ·zᵀ + b_res
 // Weights arrive pre-packed per layer in the exact padded LDS image (lbwn_pack_layers), so
 // staging is a straight 16-B copy.  Channel counts up to 32 are supported (zero-padded).
+#include <string.h>
+
 #include "common.h"
 #include "kernels.h"
+#include "prologue.h"
 
 namespace {
 
@@ -1802,12 +1805,10 @@ __global__ void pack_layers_bx3_kernel(const float* sig, const float* gate, cons
 }
 // both chains' images in one launch (blocks [0, L): forward, [L, 2L): backward), and in the
 // blocks after them (if skip_b) the skip GEMM's bias Σ_l skip_b[l] (l in order)
-__global__ void pack_layers_fb_x3_kernel(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
-                                         const float* res, const float* res_b, unsigned short* fout, float* bout,
-                                         int L, int Cr, int Cd, const float* skip_b, int Cs, float* bsum,
-                                         const float* lc_sig, const float* lc_gate, int Lo, unsigned short* lcout,
-                                         int lc16) {
-  const int l = blockIdx.x;
+LBWN_DEV void pack_fb_x3_block(int l, const float* sig, const float* gate, const float* sig_b, const float* gate_b,
+                               const float* res, const float* res_b, unsigned short* fout, float* bout, int L, int Cr,
+                               int Cd, const float* skip_b, int Cs, float* bsum, const float* lc_sig,
+                               const float* lc_gate, int Lo, unsigned short* lcout, int lc16) {
   const int nlc = lcout ? L : 0;
   if (l < L) {
     pack_x3_body(l, sig, gate, sig_b, gate_b, res, res_b, fout, Cr, Cd);
@@ -1817,7 +1818,7 @@ __global__ void pack_layers_fb_x3_kernel(const float* sig, const float* gate, co
     if (lc16) pack_lc16_body(l - 2 * L, lc_sig, lc_gate, lcout, Lo, Cd);
     else pack_lc_x3_body(l - 2 * L, lc_sig, lc_gate, lcout, Lo, Cd);
   } else {
-    const int n = (l - 2 * L - nlc) * blockDim.x + threadIdx.x;
+    const int n = (l - 2 * L - nlc) * 256 + threadIdx.x;
     if (n < Cs) {
       float s = 0.f;
 #pragma unroll 10
@@ -1825,6 +1826,53 @@ __global__ void pack_layers_fb_x3_kernel(const float* sig, const float* gate, co
       bsum[n] = s;
     }
   }
+}
+__global__ __launch_bounds__(256) void pack_layers_fb_x3_kernel(const float* sig, const float* gate,
+                                                                const float* sig_b, const float* gate_b,
+                                                                const float* res, const float* res_b,
+                                                                unsigned short* fout, float* bout, int L, int Cr,
+                                                                int Cd, const float* skip_b, int Cs, float* bsum,
+                                                                const float* lc_sig, const float* lc_gate, int Lo,
+                                                                unsigned short* lcout, int lc16) {
+  pack_fb_x3_block(blockIdx.x, sig, gate, sig_b, gate_b, res, res_b, fout, bout, L, Cr, Cd, skip_b, Cs, bsum, lc_sig,
+                   lc_gate, Lo, lcout, lc16);
+}
+
+// The step's start-of-step work in ONE launch (lbwn_step_prologue_launch): zero the status word and
+// hand-off flags, pre-split the skip/head weight planes, gather the PRE embedding, prepend the
+// D-sep state, and pack both chains' images -- five independent jobs that ran as five dependent
+// launches of 7-12 us each (profiles/r04_v1_step_timeline.txt).  Block ranges, heavy jobs first.
+struct PrologueK {
+  lbwn_prologue_args a;
+  SplitJobs jb;
+  int nz, ns, ne, nd, np;   // blocks: zero, split (per job), embed, D-sep (per layer), pack
+};
+__global__ __launch_bounds__(256) void step_prologue_kernel(PrologueK k) {
+  const lbwn_prologue_args& a = k.a;
+  long b = blockIdx.x;
+  if (b < (long)k.ns * a.njobs) {
+    split_planes_body(k.jb, (int)(b / k.ns), b % k.ns, k.ns);
+    return;
+  }
+  b -= (long)k.ns * a.njobs;
+  if (b < k.ne) {
+    embed_body(b, k.ne, a.q, a.pre, a.pre_b, a.X, a.B, a.T, a.H, a.Cr, a.Q);
+    return;
+  }
+  b -= k.ne;
+  if (b < (long)k.nd * a.L) {
+    dsep_body<true>((int)(b / k.nd), b % k.nd, k.nd, a.X, a.xls, const_cast<float*>(a.save), a.nbl, a.B, a.T, a.H,
+                    a.Cr);
+    return;
+  }
+  b -= (long)k.nd * a.L;
+  if (b < k.nz) {
+    zero_body(b, k.nz, (unsigned*)a.zero, (long)(a.zero_bytes / 4));
+    return;
+  }
+  b -= k.nz;
+  pack_fb_x3_block((int)b, a.sig, a.gate, a.sig_b, a.gate_b, a.res, a.res_b, a.fout, a.bout, a.L, a.Cr, a.Cd,
+                   a.skip_b, a.Cs, a.bsum, a.lc_sig, a.lc_gate, a.Lo, a.lcout, a.lc16);
 }
 
 // element (p, c) of a 32-float-row tile with the 4-float groups XOR-permuted: bit 4 of the column
@@ -2931,6 +2979,34 @@ int lbwn_pack_layers_fb_x3_launch(const float* sig, const float* gate, const flo
   pack_layers_fb_x3_kernel<<<2 * L + nlc + nsum, 256, 0, st>>>(sig, gate, sig_b, gate_b, res, res_b, fout, bout, L, Cr,
                                                                Cd, skip_b, Cs, bsum, lc_sig, lc_gate, Lo, lcout,
                                                                lc16);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+int lbwn_step_prologue_launch(const lbwn_prologue_args& a, hipStream_t st) {
+  LBWN_REQUIRE(a.Cr <= 32 && a.Cd <= 32 && (((uintptr_t)a.fout) & 15) == 0 && (((uintptr_t)a.bout) & 15) == 0,
+               "step_prologue: bad pack arguments");
+  LBWN_REQUIRE(!a.lcout || (a.lc_sig && a.lc_gate && a.Lo >= 1 && a.Lo <= LC_KP && (((uintptr_t)a.lcout) & 15) == 0),
+               "step_prologue: bad LC image arguments");
+  LBWN_REQUIRE(a.njobs >= 0 && a.njobs <= 6 && a.zero_bytes % 4 == 0 && a.q && a.pre && a.X && a.save,
+               "step_prologue: bad arguments");
+  PrologueK k;
+  memset(&k, 0, sizeof(k));
+  k.a = a;
+  long most = 0;
+  for (int j = 0; j < a.njobs; ++j) {
+    LBWN_REQUIRE(a.W[j] && a.out[j] && a.rows[j] > 0 && a.K[j] > 0, "step_prologue: bad split job");
+    k.jb.W[j] = a.W[j]; k.jb.ldw[j] = a.ldw[j]; k.jb.rows[j] = a.rows[j]; k.jb.K[j] = a.K[j];
+    k.jb.trans[j] = a.trans[j]; k.jb.out[j] = a.out[j];
+    most = std::max(most, (long)a.rows[j] * ((a.K[j] + PLANE_BK - 1) / PLANE_BK) * (PLANE_BK / 2));
+  }
+  auto blocks = [](long n, long per, long cap) { return (int)std::max(1L, std::min(cap, (n + per - 1) / per)); };
+  k.ns = blocks(most, 1024, 256);                                        // 4 pairs per thread
+  k.ne = blocks((long)a.B * a.T * a.Cr, 1024, 2048);
+  k.nd = blocks((long)a.B * (1L << (a.nbl - 1)) * a.Cr, 1024, 64);       // per layer, sized by the deepest d
+  k.nz = a.zero_bytes ? blocks((long)(a.zero_bytes / 4), 1024, 256) : 0;
+  k.np = 2 * a.L + (a.lcout ? a.L : 0) + ((a.skip_b && a.bsum) ? (a.Cs + 255) / 256 : 0);
+  const long grid = (long)k.ns * a.njobs + k.ne + (long)k.nd * a.L + k.nz + k.np;
+  step_prologue_kernel<<<(unsigned)grid, 256, 0, st>>>(k);
   LBWN_CHECK_LAUNCH();
   return 0;
 }

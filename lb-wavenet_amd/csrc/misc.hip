@@ -12,53 +12,19 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "prologue.h"
 
 namespace {
 
-// ---- D-separation state ----------------------------------------------------------------
-// SAVE for layer l (dilation d_l = 2^(l % nbl)) is [B][d_l][Cr], layers packed in order.
-// x buffers: xall + l*xlayer_stride, per stream [H+T][Cr]; SAVE_l occupies rows [H-d, H).
-
-LBWN_DEV long save_offset(int l, int nbl, int B, int Cr) {
-  // Σ_{l'<l} d_{l'} = (l / nbl)·(2^nbl - 1) + (2^(l % nbl) - 1)
-  const long s = (long)(l / nbl) * ((1L << nbl) - 1) + ((1L << (l % nbl)) - 1);
-  return s * B * Cr;
-}
-
+// ---- D-separation state and embedding: bodies in prologue.h ---------------------------------
 template <bool TO_X>
 __global__ void dsep_kernel(float* xall, long xls, float* save, int nbl, int B, int T, int H, int Cr) {
-  const int l = blockIdx.y;
-  const int d = 1 << (l % nbl);
-  const long n = (long)B * d * Cr;
-  float* sv = save + save_offset(l, nbl, B, Cr);
-  float* xl = xall + l * xls;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(e % Cr);
-    const long r = e / Cr;
-    const int i = (int)(r % d), b = (int)(r / d);
-    if (TO_X) {
-      xl[((long)b * (H + T) + (H - d + i)) * Cr + c] = sv[e];              // prepend
-    } else {
-      sv[e] = xl[((long)b * (H + T) + (H + T - d + i)) * Cr + c];          // save: last d rows of [SAVE ++ x]
-    }
-  }
+  dsep_body<TO_X>(blockIdx.y, blockIdx.x, gridDim.x, xall, xls, save, nbl, B, T, H, Cr);
 }
-
-// ---- embedding -------------------------------------------------------------------------
 
 __global__ void embed_kernel(const int* __restrict__ q, const float* __restrict__ pre, const float* pre_b,
                              float* x0, int B, int T, int H, int Cr, int Q) {
-  const long n = (long)B * T * Cr;
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(e % Cr);
-    const long m = e / Cr;
-    const int b = (int)(m / T), t = (int)(m % T);
-    int code = q[m];
-    code = code < 0 ? 0 : (code >= Q ? Q - 1 : code);
-    float v = pre[(long)code * Cr + c];
-    if (pre_b) v += pre_b[c];
-    x0[((long)b * (H + T) + H + t) * Cr + c] = v;
-  }
+  embed_body(blockIdx.x, gridDim.x, q, pre, pre_b, x0, B, T, H, Cr, Q);
 }
 
 // out[m] = a[m] + (t+gd < T ? c0[m+gd] : 0)   (dx of a layer input from (g + dcur, dprev))
@@ -238,13 +204,19 @@ __global__ __launch_bounds__(256) void head_kernel(lbwn_head_args a) {
 // the gradient written from registers (the generic kernel above re-reads the row three times and
 // evaluates exp twice).  Lane c-order (c = lane + 64·j) and the first-max tie-break are kept, so
 // argmax (avg_diff) is identical; Σe is summed per lane, then across the wave.
+// With a.colpart, the block's column sums of the dlogits it wrote go to colpart[block][Q] (the
+// post2 bias gradient's partials, summed by colsum_final: no second pass over the [M][Q] matrix).
 template <int QV>
 __global__ __launch_bounds__(256) void head_reg_kernel(lbwn_head_args a) {
   __shared__ float part[4][3];
+  __shared__ float cpart[4][64 * QV];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const long M = (long)a.B * a.T;
   const int Q = a.Q;
   float s_xent = 0.f, s_valid = 0.f, s_diff = 0.f;
+  float cs[QV];
+#pragma unroll
+  for (int j = 0; j < QV; ++j) cs[j] = 0.f;
   for (long m = (long)blockIdx.x * 4 + w; m < M; m += (long)gridDim.x * 4) {
     float* row = a.logits + m * Q;
     const int t = (int)(m % a.T);
@@ -286,7 +258,9 @@ __global__ __launch_bounds__(256) void head_reg_kernel(lbwn_head_args a) {
 #pragma unroll
       for (int j = 0; j < QV; ++j) {
         const int c = lane + 64 * j;
-        if (c < Q) row[c] = valid ? e[j] * inv - (c == tgt ? 1.f : 0.f) : 0.f;
+        const float g = valid ? e[j] * inv - (c == tgt ? 1.f : 0.f) : 0.f;
+        if (c < Q) row[c] = g;
+        cs[j] += g;
       }
     }
     if (lane == 0 && valid) {
@@ -300,11 +274,18 @@ __global__ __launch_bounds__(256) void head_reg_kernel(lbwn_head_args a) {
     part[w][1] = s_valid;
     part[w][2] = s_diff;
   }
+  if (a.colpart) {
+#pragma unroll
+    for (int j = 0; j < QV; ++j) cpart[w][lane + 64 * j] = cs[j];
+  }
   __syncthreads();
   if (threadIdx.x < 3) {
     const int k = threadIdx.x;
     a.partial[blockIdx.x * 3 + k] = ((part[0][k] + part[1][k]) + part[2][k]) + part[3][k];
   }
+  if (a.colpart)
+    for (int c = threadIdx.x; c < Q; c += 256)
+      a.colpart[(long)blockIdx.x * Q + c] = ((cpart[0][c] + cpart[1][c]) + cpart[2][c]) + cpart[3][c];
 }
 
 // stats[0] = Σxent, [1] = n_valid, [2] = Σ|diff|, [3] = 1/n_valid (0 if none)
@@ -342,6 +323,7 @@ struct ColsumJobs {
   int accumulate[4];
   float* ws[4];
   int nparts[4];   // partial rows per job (colsum_final_kernel)
+  int reps[4];     // copies of the result row written (out + r·N), colsum_final_kernel
 };
 __global__ __launch_bounds__(256) void colsum_partial_kernel(ColsumJobs jb, int M) {
   __shared__ floatx4 red[256];
@@ -385,7 +367,10 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(ColsumJobs jb) {
   if (threadIdx.x < 64 && c < N) {
     const float tot = ((red[threadIdx.x] + red[64 + threadIdx.x]) + red[128 + threadIdx.x]) + red[192 + threadIdx.x];
     float* out = jb.out[j];
-    out[c] = jb.accumulate[j] ? out[c] + tot : tot;
+    for (int r = 0; r < max(1, jb.reps[j]); ++r) {
+      float* o = out + (long)r * N + c;
+      *o = jb.accumulate[j] ? *o + tot : tot;
+    }
   }
 }
 
@@ -556,7 +541,8 @@ int lbwn_shift_add_launch(float* out, const float* a, const float* c0, int gd, i
 
 int lbwn_head_launch(const lbwn_head_args& a, int* nblocks_out, hipStream_t st) {
   const long M = (long)a.B * a.T;
-  const int nb = (int)std::min<long>((M + 3) / 4, 2048);
+  LBWN_REQUIRE(!a.colpart || a.Q <= 512, "head: column partials need Q <= 512");
+  const int nb = lbwn_head_nblocks(M, a.colpart != nullptr);
   if (a.Q <= 256) head_reg_kernel<4><<<nb, 256, 0, st>>>(a);
   else if (a.Q <= 512) head_reg_kernel<8><<<nb, 256, 0, st>>>(a);
   else head_kernel<<<nb, 256, 0, st>>>(a);
@@ -564,7 +550,10 @@ int lbwn_head_launch(const lbwn_head_args& a, int* nblocks_out, hipStream_t st) 
   if (nblocks_out) *nblocks_out = nb;
   return 0;
 }
-int lbwn_head_nblocks(long M) { return (int)std::min<long>((M + 3) / 4, 2048); }
+// with column partials: at most ceil(M/32) blocks, so colpart fits the colsum workspace
+int lbwn_head_nblocks(long M, bool colpart) {
+  return (int)(colpart ? std::min<long>((M + 31) / 32, 1024) : std::min<long>((M + 3) / 4, 2048));
+}
 
 int lbwn_stats_reduce_launch(const float* partial, int nparts, float* stats, hipStream_t st) {
   stats_reduce_kernel<<<1, 256, 0, st>>>(partial, nparts, stats);
@@ -609,7 +598,7 @@ int lbwn_colsum_partial_launch(const float* X, long ldx, int M, int N, float* ws
 }
 
 int lbwn_colsum_final_launch(int njobs, float* const* parts, const int* N, float* const* out, const int* accumulate,
-                             const int* nparts, hipStream_t st) {
+                             const int* nparts, hipStream_t st, const int* reps) {
   LBWN_REQUIRE(njobs >= 1 && njobs <= 4, "colsum_final: 1..4 jobs");
   ColsumJobs jb;
   memset(&jb, 0, sizeof(jb));
@@ -618,6 +607,7 @@ int lbwn_colsum_final_launch(int njobs, float* const* parts, const int* N, float
     LBWN_REQUIRE(nparts[j] >= 1, "colsum_final: nparts >= 1");
     jb.N[j] = N[j]; jb.out[j] = out[j]; jb.accumulate[j] = accumulate[j]; jb.ws[j] = parts[j];
     jb.nparts[j] = nparts[j];
+    jb.reps[j] = reps ? reps[j] : 1;
     nmax = std::max(nmax, N[j]);
   }
   colsum_final_kernel<<<dim3((nmax + 63) / 64, njobs), 256, 0, st>>>(jb);
@@ -682,9 +672,7 @@ __global__ void bcast_rows_kernel(float* dst, int L, int N) {
 }  // namespace
 
 namespace {
-__global__ void zero_words_kernel(unsigned* p, long n) {
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) p[e] = 0u;
-}
+__global__ void zero_words_kernel(unsigned* p, long n) { zero_body(blockIdx.x, gridDim.x, p, n); }
 }  // namespace
 
 // Zero n_bytes (a multiple of 4) on the stream: an ordinary kernel in the step's launch sequence.
