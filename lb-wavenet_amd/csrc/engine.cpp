@@ -15,6 +15,7 @@
 #include "kernels.h"
 
 struct lbwn_plan {
+  int chain_xcd = 1;       // chain_first's XCD-grouped walk
   int head_colparts = 0;   // post2-bias column partial rows the last forward's head wrote (0: none)
   lbwn_arch a;
   int B, T, L, nbl, H, Cr, Cd, Cs, Cp, Q;
@@ -305,6 +306,10 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   LBWN_REQUIRE(p, "plan: out of host memory");
   p->fwd_nw = fwd_nw;
   p->bwd_nw = bwd_nw;
+  {  // XCD-grouped chain tile walk (layer.hip chain_first); LBWN_CHAIN_XCD=0: tile = block index
+    const char* xv = getenv("LBWN_CHAIN_XCD");
+    p->chain_xcd = !(xv && !strcmp(xv, "0"));
+  }
   p->a = *a;
   p->B = B;
   p->T = T;
@@ -807,6 +812,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     }
     c.flags = at<unsigned>(ws, p->oFLAGS); c.status = at<unsigned>(ws, p->oSTATUS);
     c.flags_zeroed = 1;   // zeroed with the status word at the step start
+    c.xcd = p->chain_xcd;
     if (p->ctrace_blk >= 0) { c.trace = at<long long>(ws, p->oCTRACE); c.trace_blk = p->ctrace_blk; }
     c.B = B; c.T = T; c.H = H; c.L = L; c.nbl = p->nbl; c.Cr = Cr; c.Cd = Cd; c.grid = p->chain_grid;
     if (c.SG && p->fwd_nw) { c.fwd_nw = p->fwd_nw; c.grid = p->fwd_grid; }
@@ -1040,6 +1046,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     c.gc_dtab = cd.gc_dtab; c.dv_out = cd.dv_out; c.lddv = cd.ldcond;
     c.dx0_a = at<float>(ws, p->oGA[0]); c.dx0_c = at<float>(ws, p->oGC0[0]);
     c.flags = at<unsigned>(ws, p->oFLAGS + p->nflag_bytes); c.status = at<unsigned>(ws, p->oSTATUS);
+    c.xcd = p->chain_xcd;
     c.flags_zeroed = p->bwd_flags_fresh ? 1 : 0;   // zeroed at the step start unless already used
     p->bwd_flags_fresh = false;
     if (p->ctrace_blk >= 0) { c.trace = at<long long>(ws, p->oCTRACE); c.trace_blk = p->ctrace_blk; }

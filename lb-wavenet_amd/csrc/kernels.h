@@ -170,6 +170,7 @@ struct lbwn_chain_args {
   const float* lcact = nullptr; const unsigned short* lcimg = nullptr; int Lo = 0;
   int fwd_nw = 0;              // forward form (lbwn_chain_fwd_tile); lcimg in the matching layout
   int bwd_nw = 0;              // backward form: 0 = chain_bwd_x3_kernel (128), 4 / 8 = chain_bwd16_kernel
+  int xcd = 0;                 // XCD-grouped tile walk (layer.hip chain_first)
 };
 int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st);
 int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st);

@@ -432,7 +432,18 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 constexpr long long SPIN_TIMEOUT = 400000000LL;  // wall_clock64 ticks (100 MHz) = 4 s
 constexpr int BUF_DW3 = 0x00020000;
 
+// First tile of this block in the chains' tile walk (tile += gridDim.x after it).  xcd: blocks
+// b and b + 8 share an XCD under round-robin dispatch (MI355X_MICROARCH.md, placement: speed only,
+// never correctness), so with gridDim.x % 8 == 0 block b takes tile (b % 8)·(G/8) + b / 8 of each
+// round: consecutive tiles -- a stream's hand-off neighbours -- run on one XCD (32 tiles = one
+// 4096-sample stream at C2).  A bijection of each round's tiles: the rounds are unchanged.
+LBWN_DEV int chain_first(int xcd) {
+  const int bx = blockIdx.x, G = gridDim.x;
+  return (xcd && (G & 7) == 0) ? (bx & 7) * (G >> 3) + (bx >> 3) : bx;
+}
+
 struct ChainFK {
+  int xcd;                     // chain_first: XCD-grouped tile walk
   float* X; long xls;        // x_l for all layers: layer stride (floats); each [B][H+T][32]
   float* Z; long ldz;
   const float* wpack;        // L packed images
@@ -654,7 +665,8 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
   const int r = 32 * w + pi;  // this lane's row of the tile
   const int tps = (a.T + LP - 1) / LP, ntiles = a.B * tps;
   if (tid == 0) s_fail = 0;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  const int first = chain_first(a.xcd);
+  for (int tile = first; tile < ntiles; tile += gridDim.x) {
     const int b = tile / tps, tt = tile % tps, t0 = tt * LP;
     const int t = t0 + r;
     const bool valid = t < a.T;
@@ -709,7 +721,7 @@ __global__ __launch_bounds__(256) void chain_fwd_kernel(ChainFK a) {
         dma_lc_image(a.lcimg, 1, LCI, w, lane);   // lands with layer 0's halo loads
       }
     }
-    const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && tile == (int)blockIdx.x;
+    const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && tile == first;
 #define FSTAMP(i) if (TR && trc) a.trace[16 * l + (i)] = clock64()
     auto store_zs = [&](int ll, const floatx16& zz, const floatx16& ss) {
       if (valid) store_rows16(a.Z + m * a.ldz + (long)ll * a.Cd, zz, a.Cd, h);
@@ -1065,7 +1077,8 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
   const int r = 16 * w + i16;  // this lane's row of the tile
   const int tps = (a.T + TP - 1) / TP, ntiles = a.B * tps;
   if (tid == 0) s_fail = 0;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  const int first = chain_first(a.xcd);
+  for (int tile = first; tile < ntiles; tile += gridDim.x) {
     const int b = tile / tps, tt = tile % tps, t0 = tt * TP;
     const int t = t0 + r;
     const bool valid = t < a.T;
@@ -1130,7 +1143,7 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
         dma_lc16_image<NW>(a.lcimg, 1, LCI, w, lane);   // lands with layer 0's halo loads
       }
     }
-    const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && tile == (int)blockIdx.x;
+    const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && tile == first;
 #define FSTAMP(i) if (TR && trc) a.trace[16 * l + (i)] = clock64()
     for (int l = 0; l < a.L; ++l) {
       FSTAMP(0);
@@ -1332,6 +1345,7 @@ LBWN_DEV void slab_group_prefetch(const RedK& a, int grp, float (&pre)[RED_PARTS
 // after the publish, so the cross-tile critical path per layer is G-build → dz → dx.
 // Weight-gradient partials go to slab[l][tile] (summed by layer_reduce_all_kernel).
 struct ChainBK {
+  int xcd;                     // chain_first: XCD-grouped tile walk
   const float* X; long xls;
   const float* DZ; long lddz; long dzls;   // dzls > 0: DZ in chain order (sg_off blocks per layer)
   const float* wpack;
@@ -1440,7 +1454,8 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
   const int tps = (a.T + LP - 1) / LP, ntiles = a.B * tps;
   const int oc_bytes = (int)std::min<long>(a.ocls * 4, 0x7fffffffL);
   if (tid == 0) s_fail = 0;
-  for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
+  const int first = chain_first(a.xcd);
+  for (int it = first; it < ntiles; it += gridDim.x) {
     const int tile = ntiles - 1 - it;
     const int b = tile / tps, tt = tile % tps, t0 = tt * LP;
     const int t = t0 + r;
@@ -1459,7 +1474,7 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
     floatx16 oa;  // out_a of layer l+1, own row
 #pragma unroll
     for (int q = 0; q < 16; ++q) oa[q] = 0.f;
-    const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && it == (int)blockIdx.x;
+    const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && it == first;
 #define CSTAMP(i) if (trc) a.trace[16 * l + (i)] = clock64()
     for (int l = a.L - 1; l >= 0; --l) {
       CSTAMP(0);
@@ -1939,7 +1954,8 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
   const int tps = (a.T + LP - 1) / LP, ntiles = a.B * tps;
   const int oc_bytes = (int)std::min<long>(a.ocls * 4, 0x7fffffffL);
   if (tid == 0) s_fail = 0;
-  for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
+  const int first = chain_first(a.xcd);
+  for (int it = first; it < ntiles; it += gridDim.x) {
     const int tile = ntiles - 1 - it;
     const int b = tile / tps, tt = tile % tps, t0 = tt * LP;
     const int t = t0 + r;
@@ -1983,7 +1999,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
     floatx16 oa;  // out_a of layer l+1, own row
 #pragma unroll
     for (int q = 0; q < 16; ++q) oa[q] = 0.f;
-    const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && it == (int)blockIdx.x;
+    const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && it == first;
 #define XSTAMP(i) if (TR && trc) a.trace[16 * l + (i)] = clock64()
     for (int l = a.L - 1; l >= 0; --l) {
       XSTAMP(0);
@@ -2338,7 +2354,8 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
   const int tps = (a.T + TP - 1) / TP, ntiles = a.B * tps;
   const int oc_bytes = (int)std::min<long>(a.ocls * 4, 0x7fffffffL);
   if (tid == 0) s_fail = 0;
-  for (int it = blockIdx.x; it < ntiles; it += gridDim.x) {
+  const int first = chain_first(a.xcd);
+  for (int it = first; it < ntiles; it += gridDim.x) {
     const int tile = ntiles - 1 - it;
     const int b = tile / tps, tt = tile % tps, t0 = tt * TP;
     const int t = t0 + r;
@@ -2374,7 +2391,7 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
     __syncthreads();
     floatx4 oa[2];  // out_a of layer l+1, own row (N layout)
     oa[0] = oa[1] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && it == (int)blockIdx.x;
+    const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && it == first;
 #define XSTAMP(i) if (TR && trc) a.trace[16 * l + (i)] = clock64()
     for (int l = a.L - 1; l >= 0; --l) {
       XSTAMP(0);
@@ -3095,6 +3112,7 @@ int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   k.B = c.B; k.T = c.T; k.H = c.H; k.L = c.L; k.nbl = c.nbl; k.Cd = c.Cd;
   k.trace = c.trace; k.trace_blk = c.trace_blk;
   k.ximg = c.wpack_x3;
+  k.xcd = c.xcd;
   k.SG = c.SG; k.sgls = c.sgls;
   k.lcact = c.lcact; k.lcimg = c.lcimg; k.Lo = c.Lo;
   LBWN_REQUIRE(!c.wpack_x3 || (((uintptr_t)c.wpack_x3) & 15) == 0, "chain fwd: split images not 16-B aligned");
@@ -3143,6 +3161,7 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   k.flags = c.flags; k.status = c.status;
   k.B = c.B; k.T = c.T; k.H = c.H; k.L = c.L; k.nbl = c.nbl; k.Cd = c.Cd;
   k.trace = c.trace ? c.trace + 16L * c.L : nullptr; k.trace_blk = c.trace_blk;
+  k.xcd = c.xcd;
   k.Zf = c.Z; k.SG = c.SG; k.sgls = c.sgls; k.bimg = c.bimg;
   const bool x3 = c.bimg && c.SG && c.Z;
   if (x3) LBWN_REQUIRE((((uintptr_t)c.bimg) & 15) == 0 && (((uintptr_t)c.SG) & 15) == 0 && (c.ldz & 3) == 0,

@@ -1,15 +1,21 @@
 #!/bin/bash
-# A/B one library under two environments: bench (headline, no gen) + kernel stats + one step's
-# timeline per arm.  Usage: bash tools/ab_env.sh TAG "VAR=a" "VAR=b"
+# Same-box A/B of environment settings on the training step, two interleaved rounds.
+# Usage: bash tools/ab_env.sh "LBWN_CHAIN_XCD=0" "LBWN_CHAIN_XCD=1" ...   ("-" = no setting)
+# CONFIGS (default "arch3:8 arch5:8"): arch:batch list.
 set -o pipefail
-TAG=$1; A=$2; B=$3
-export TMPDIR=/tmp
-for arm in a b; do
-  E=$A; [ $arm = b ] && E=$B
-  env $E timeout -k 10 120 python bench.py --no-cpu-baseline --no-extras --no-gen > gpurun_out/abe_${TAG}_$arm.json 2>/dev/null || { echo "bench $arm failed"; exit 1; }
+mkdir -p gpurun_out
+CONFIGS=${CONFIGS:-"arch3:8 arch5:8"}
+for round in 1 2; do
+  k=0
+  for v in "$@"; do
+    k=$((k + 1))
+    for cfg in $CONFIGS; do
+      arch=${cfg%%:*}; b=${cfg#*:}
+      steps=40; [ "$b" -gt 8 ] && steps=12
+      envs=(); [ "$v" != "-" ] && envs=($v)
+      env "${envs[@]}" timeout -k 10 240 python bench.py --arch par/$arch.json --batch $b --no-cpu-baseline --no-extras --no-gen \
+        --steps $steps > gpurun_out/abe_${k}_$arch$b.json 2> gpurun_out/abe_${k}_$arch$b.err || { echo "bench [$v] $cfg failed"; tail -5 gpurun_out/abe_${k}_$arch$b.err; exit 1; }
+      python -c "import json; d=json.load(open('gpurun_out/abe_${k}_$arch$b.json')); print('round $round [$v] $cfg', round(d['ms_per_step'],4), 'fwd', round(d['roofline_dilconv']['avg_launch_us'],1), 'bwd', round(d['roofline']['avg_launch_us'],1))"
+    done
+  done
 done
-for arm in a b; do
-  E=$A; [ $arm = b ] && E=$B
-  env $E timeout -k 10 120 python bench.py --no-cpu-baseline --no-extras --no-gen > gpurun_out/abe_${TAG}_${arm}2.json 2>/dev/null || { echo "bench $arm failed"; exit 1; }
-done
-echo abe ok
