@@ -98,6 +98,18 @@ LBWN_DEV int xcd_remap(int bid, int nwg) {
 LBWN_DEV int gemm_work() { return xcd_remap(blockIdx.x + gridDim.x * blockIdx.z, gridDim.x * gridDim.z); }
 LBWN_DEV int gemm_tile() { return gemm_work() % gridDim.x; }
 LBWN_DEV int gemm_split() { return gemm_work() / gridDim.x; }
+// 2-D blocking of a tm × tn tile grid over the 8 XCDs (no split-K): XCD x (= block % 8 under
+// round-robin dispatch; placement is speed only) takes column half x & 1 and row quarter x >> 1,
+// row-panel-major, so its L2 holds one half of the pre-split B (dZ: 2.45 of 4.9 MB) for the whole
+// launch while A row panels stream through once per column half: A read twice and B eight halves,
+// instead of B re-fetched per wave of row panels on every XCD (dZ 2.06x its algorithmic bytes,
+// profiles/r04_pmc_read_requests.json)
+LBWN_DEV int xcd2d_tile(int tm, int tn) {
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  if ((nwg & 7) || (tm & 3) || (tn & 1) || gridDim.z != 1 || nwg != tm * tn) return gemm_tile();
+  const int x = bid & 7, j = bid >> 3, hn = tn >> 1, qm = tm >> 2;
+  return ((x >> 1) * qm + j / hn) * tn + (x & 1) * hn + j % hn;
+}
 
 // Block tile BMT × BNT, 4 waves as 2 × 2, each wave (BMT/2) × (BNT/2) = MI × NI MFMA tiles.
 // 128×128 tiles: four blocks (16 waves) per CU, i.e. at most 128 VGPRs; every register
@@ -808,7 +820,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
   const int tiles_n = (g.N + BN - 1) / BN;
   if (g.step_advance && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && tid == 0)   // no-return atomic
     __hip_atomic_fetch_add(g.step_advance, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int t = gemm_tile();
+  const int t = (NB == 10 && g.xcd2d) ? xcd2d_tile((g.M + BM - 1) / BM, tiles_n) : gemm_tile();
   const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
   const int kz0 = gemm_split() * g.k_per_split;
   const int kz1 = min(g.K, kz0 + g.k_per_split);
@@ -1059,6 +1071,8 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
       // C2 = 1280 = 5 rounds) instead of 128-column ones (13 column tiles, the last half empty:
       // 1664 = 6.5 rounds)
       grid.x = (unsigned)(((a.M + 255) / 256) * (a.N / 160));
+      static const int x2 = [] { const char* e = getenv("LBWN_DZ_XCD"); return (e && e[0] == '0') ? 0 : 1; }();
+      g.xcd2d = x2;   // LBWN_DZ_XCD=0: the 1-D remap (same-box A/B switch)
       gemm_x3q_kernel<10><<<grid, 512, 0, st>>>(g);
     } else if (X3Q) {
       gemm_x3q_kernel<8><<<grid, 512, 0, st>>>(g);

@@ -25,6 +25,7 @@ struct lbwn_gemm_args {
   long c_chain_ls;
   int k_per_split;     // set by the launcher
   long split_stride;   // set by the launcher
+  int xcd2d;           // set by the launcher: gemm_x3q_kernel<10>'s 2-D XCD blocking (xcd2d_tile)
 };
 int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                      hipStream_t st);
