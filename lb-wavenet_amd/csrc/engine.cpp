@@ -16,6 +16,7 @@
 
 struct lbwn_plan {
   int chain_xcd = 1;       // chain_first's XCD-grouped walk
+  bool dv_blk = false;     // the last backward exported DV k-blocked ([2L][m32(M)][32])
   int head_colparts = 0;   // post2-bias column partial rows the last forward's head wrote (0: none)
   lbwn_arch a;
   int B, T, L, nbl, H, Cr, Cd, Cs, Cp, Q;
@@ -417,7 +418,7 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     p->oCOND = p->Lo ? carve(cur, f * (size_t)M * ncond) : 0;
     p->up_fused = p->Lo > 0 && lbwn_lc_up_fused_ok(p->nup, p->up, p->Li, p->Lo);
     if (p->up_fused) p->oUPPART = carve(cur, f * (size_t)lbwn_lc_up_part_floats(p->nup, p->up, p->Li, p->Lo, (int)(M / hop)));
-    p->oDVALL = p->Lo ? carve(cur, f * (size_t)M * ncond) : 0;
+    p->oDVALL = p->Lo ? carve(cur, f * (size_t)m32(M) * ncond) : 0;   // rows or [2L][m32(M)][32]
     p->oLCCAT = p->Lo ? carve(cur, f * (size_t)p->Lo * ncond) : 0;
     if (p->Lo && ncond % 32 == 0)
       p->oLCCAT3 = carve(cur, sizeof(unsigned short) * lbwn_split_planes_elems(p->Lo, (int)ncond));
@@ -632,6 +633,7 @@ int lc_wgrad(lbwn_plan* p, const lbwn_params* G, void* ws, float* spl, hipStream
   const long ncond = 2L * p->L * p->Cd;
   lbwn_gemm_args g = gemm0();
   g.A = at<float>(ws, p->oLCACT[p->nup - 1]); g.lda = p->Lo; g.B = at<float>(ws, p->oDVALL); g.ldb = ncond;
+  if (p->dv_blk) { g.ldb = 32; g.b_gstride = m32(p->M) * 32; }
   g.C = at<float>(ws, p->oDLCCAT); g.ldc = ncond;
   g.M = p->Lo; g.N = (int)ncond; g.K = (int)p->M;
   Probe(p, st, "lc_wgrad");
@@ -649,6 +651,7 @@ int lc_dlc(lbwn_plan* p, const lbwn_params* P, void* ws, float* spl, hipStream_t
     return e;
   lbwn_gemm_args g = gemm0();
   g.A = at<float>(ws, p->oDVALL); g.lda = ncond; g.B = at<float>(ws, p->oLCCAT); g.ldb = ncond;
+  if (p->dv_blk) { g.lda = 32; g.a_kstride = m32(p->M) * 32; }
   g.C = at<float>(ws, p->oDLC[0]); g.ldc = p->Lo;
   g.M = (int)p->M; g.N = p->Lo; g.K = (int)ncond;
   if (p->oLCCAT3 && lbwn_gemm_mode() == 1) {   // pre-split B: the A-in-registers GEMM (96-column tiles)
@@ -1040,7 +1043,9 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
       c.Z = Z; c.SG = at<float>(ws, p->oSG); c.sgls = m32(M) * 32; c.bimg = at<float>(ws, p->oWPKB);
       c.dzls = m32(M) * 32;   // dZ in chain order (the dZ GEMM above)
       if (cd.gc_dtab) c.tile_gid = at<int>(ws, p->oTGID);
+      if (cd.dv_out) c.dvks = m32(M) * 32;   // DV k-blocked: contiguous GEMM k-steps for dlc / dLCcat
     }
+    p->dv_blk = c.dvks != 0;
     c.slab = SLABS; c.ocg = at<float>(ws, p->oOCG); c.ocls = M * 32;
     c.gc_tab = cd.gc_tab; c.gc_ld = cd.gc_ld; c.cond = cd.cond; c.ldcond = cd.ldcond;
     c.gc_dtab = cd.gc_dtab; c.dv_out = cd.dv_out; c.lddv = cd.ldcond;
@@ -1092,6 +1097,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     }
     if (p->aux2) LBWN_HIP(hipEventRecord(p->ev_join2, rst));
   } else {
+    p->dv_blk = false;
       for (int l = L - 1; l >= 0; --l) {
       lbwn_layer_args a = layer_base(p, P, WPK, ids, l);
       cd.apply(a, l);

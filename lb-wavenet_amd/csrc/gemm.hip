@@ -318,19 +318,23 @@ struct X3Stage {
   int kz;               // the split's first k
   unsigned okm[2];      // !KFULL: bit i = k in range (zeroed at store time, not at load)
   LBWN_DEV static bool mine(int tid, int q) { return KC || tid + NTHR * q < 2 * ROWS; }
-  LBWN_DEV void init(const float* __restrict__ P, long ld, int mn0, int MN, int kz0, int tid) {
+  // gs: 0, or for a k-blocked operand (ld = 32, KFULL) the stride of its 32-deep k chunks (KC)
+  // or of its 32-wide mn groups (MN)
+  LBWN_DEV void init(const float* __restrict__ P, long ld, int mn0, int MN, int kz0, int tid, long gs = 0) {
     kq = 4 * (tid & 7);
     kz = kz0;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       if (KC) {
-        p[i] = P + (long)min(mn0 + (tid >> 3) + (NTHR / 8) * i, MN - 1) * ld + kz0 + kq;
+        p[i] = P + (long)min(mn0 + (tid >> 3) + (NTHR / 8) * i, MN - 1) * ld +
+               (gs ? (long)(kz0 / X3_BK) * gs : (long)kz0) + kq;
       } else {
         const int b = (tid + NTHR * (i >> 2)) % (2 * ROWS);
-        p[i] = P + (long)(kz0 + kq + (i & 3)) * ld + min(mn0 + 4 * (b >> 3), MN - 4);
+        const int mn = min(mn0 + 4 * (b >> 3), MN - 4);   // 4-aligned: never crosses a 32-group
+        p[i] = P + (long)(kz0 + kq + (i & 3)) * ld + (gs ? (long)(mn >> 5) * gs + (mn & 31) : (long)mn);
       }
     }
-    step = KC ? X3_BK : X3_BK * ld;
+    step = KC ? (gs ? gs : X3_BK) : X3_BK * ld;
   }
   // k-step t of the split ending at kend (kend read only when !KFULL); a clamped index keeps
   // every load unconditional
@@ -506,9 +510,9 @@ __global__ __launch_bounds__(128 * WM, (WM == 2 && STAGES == 1) ? X3_OCC : 1) vo
   X3Stage<A_KC, KFULL, BM, NTHR> sa;
   X3Stage<B_KC, KFULL, BN, NTHR> sb;
   X3Pre<BN, NTHR> sp;
-  sa.init(g.A, g.lda, m0, g.M, kz0, tid);
+  sa.init(g.A, g.lda, m0, g.M, kz0, tid, A_KC ? g.a_kstride : 0);
   if (BPRE) sp.init(g.b3, g.K / X3_BK, n0, g.N, kz0, tid);
-  else sb.init(g.B, g.ldb, n0, g.N, kz0, tid);
+  else sb.init(g.B, g.ldb, n0, g.N, kz0, tid, B_KC ? 0 : g.b_gstride);
   const bool relu_a = g.relu_a;
   if (ntiles > 0) {
     sa.load(0, kz1);
@@ -834,16 +838,17 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
     for (int b = 0; b < NB; ++b) acc[a][b] = (floatx4){0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  const float* pa0 = g.A + (long)min(m0 + 32 * wave + fr, g.M - 1) * g.lda + kz0 + 8 * fq;
-  const float* pa1 = g.A + (long)min(m0 + 32 * wave + 16 + fr, g.M - 1) * g.lda + kz0 + 8 * fq;
+  const long aks = g.a_kstride ? g.a_kstride : X3_BK;   // floats per 32-deep k-step of A
+  const float* pa0 = g.A + (long)min(m0 + 32 * wave + fr, g.M - 1) * g.lda + (kz0 / X3_BK) * aks + 8 * fq;
+  const float* pa1 = g.A + (long)min(m0 + 32 * wave + 16 + fr, g.M - 1) * g.lda + (kz0 / X3_BK) * aks + 8 * fq;
   const int alo = g.relu_a ? 0 : (int)0x80000000;   // relu as an integer max (x3_store4)
   floatx4 av[2][4];
   auto a_load = [&](auto sset, int kt) {
     constexpr int S = decltype(sset)::value;
-    av[S][0] = *(const floatx4*)(pa0 + kt * X3_BK);
-    av[S][1] = *(const floatx4*)(pa0 + kt * X3_BK + 4);
-    av[S][2] = *(const floatx4*)(pa1 + kt * X3_BK);
-    av[S][3] = *(const floatx4*)(pa1 + kt * X3_BK + 4);
+    av[S][0] = *(const floatx4*)(pa0 + kt * aks);
+    av[S][1] = *(const floatx4*)(pa0 + kt * aks + 4);
+    av[S][2] = *(const floatx4*)(pa1 + kt * aks);
+    av[S][3] = *(const floatx4*)(pa1 + kt * aks + 4);
   };
   auto a_split = [&](auto sset, int mi, bf16x8 (&f)[3]) {
     constexpr int S = decltype(sset)::value;
@@ -998,6 +1003,10 @@ int gemm_setup(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int& split
   LBWN_REQUIRE(a.a_codes == nullptr || !a_kcontig, "gemm: one-hot A must be m-contiguous");
   LBWN_REQUIRE((a.a_codes || (((uintptr_t)a.A) & 15) == 0) && (((uintptr_t)a.B) & 15) == 0,
                "gemm: A/B not 16-B aligned");
+  LBWN_REQUIRE(!a.a_kstride || (a_kcontig && a.lda == 32 && a.K % 32 == 0 && !a.a_codes && lbwn_gemm_mode() == 1),
+               "gemm: k-blocked A needs k-contiguous A, lda = 32, K %% 32 == 0 and the bf16-split form");
+  LBWN_REQUIRE(!a.b_gstride || (!b_kcontig && a.ldb == 32 && !a.b3 && lbwn_gemm_mode() == 1),
+               "gemm: mn-blocked B needs mn-contiguous B, ldb = 32, no pre-split and the bf16-split form");
   if (split_k < 1) split_k = 1;
   g = a;
   int kps = (a.K + split_k - 1) / split_k;

@@ -26,6 +26,11 @@ struct lbwn_gemm_args {
   int k_per_split;     // set by the launcher
   long split_stride;   // set by the launcher
   int xcd2d;           // set by the launcher: gemm_x3q_kernel<10>'s 2-D XCD blocking (xcd2d_tile)
+  // k-blocked operands (the backward chain's DV export, [K/32][Mp][32]): 0 = plain layout.
+  // a_kstride: A k-contiguous with lda = 32, element (m, k) at A[m·32 + (k/32)·a_kstride + k%32]
+  // (gemm_x3q_kernel only); b_gstride: B mn-contiguous with ldb = 32, element (k, n) at
+  // B[k·32 + (n/32)·b_gstride + n%32] (the LDS-staged bf16-split kernel only)
+  long a_kstride, b_gstride;
 };
 int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                      hipStream_t st);
@@ -172,6 +177,7 @@ struct lbwn_chain_args {
   int fwd_nw = 0;              // forward form (lbwn_chain_fwd_tile); lcimg in the matching layout
   int bwd_nw = 0;              // backward form: 0 = chain_bwd_x3_kernel (128), 4 / 8 = chain_bwd16_kernel
   int xcd = 0;                 // XCD-grouped tile walk (layer.hip chain_first)
+  long dvks = 0;               // x3 backward forms: dv_out k-blocked ([L·2][Mp][32], chunk stride dvks)
 };
 int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st);
 int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st);

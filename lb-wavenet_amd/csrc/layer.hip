@@ -1354,6 +1354,7 @@ struct ChainBK {
   float* dx0_a; float* dx0_c;  // layer 0's out_a / out_c0 [B·T][32]
   const float* gc_tab; long gc_ld; const int* ids; const float* cond; long ldcond;
   float* dv_out; long lddv;    // dv export for the LC gradients: [M][L·2Cd] (layer l at column l·2Cd) or null
+  long dvks;                   // x3 forms: 0, or the chunk stride of the k-blocked export [L·2][Mp][32]
   float* gc_dtab;              // GC gradient table, layout of gc_tab, atomics, or null
   unsigned* flags; unsigned* status;
   int B, T, H, L, nbl, Cd;
@@ -2093,7 +2094,10 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
         dvg[q] = dz[q] * zz * (1.f - sg);
       }
       {
-        float* dvo = (a.dv_out && valid) ? a.dv_out + m * a.lddv + (long)l * 64 : nullptr;
+        // DV export: rows (layer l at columns l·64) or k-blocked (a.dvks: [L·2][Mp][32] chunks)
+        float* dvo = (a.dv_out && valid)
+                         ? a.dv_out + (a.dvks ? 2L * l * a.dvks + m * 32 : m * a.lddv + (long)l * 64) : nullptr;
+        const long dgo = a.dvks ? a.dvks : 32;   // gate half
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const floatx4 vs = floatx4{dvs[4 * q], dvs[4 * q + 1], dvs[4 * q + 2], dvs[4 * q + 3]};
@@ -2102,7 +2106,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
           *(floatx4*)(DVg + (CONF(2048) ? 4 * lane + 256 * q + 1024 * w : swz(r, 8 * q + 4 * h))) = vg;
           if (dvo) {
             *(floatx4*)(dvo + 8 * q + 4 * h) = vs;
-            *(floatx4*)(dvo + 32 + 8 * q + 4 * h) = vg;
+            *(floatx4*)(dvo + dgo + 8 * q + 4 * h) = vg;
           }
         }
       }
@@ -2486,7 +2490,10 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
           dvg[bb][e] = dz[bb][e] * zz * (1.f - sg);
         }
       {
-        float* dvo = (a.dv_out && valid) ? a.dv_out + m * a.lddv + (long)l * 64 : nullptr;
+        // DV export: rows (layer l at columns l·64) or k-blocked (a.dvks: [L·2][Mp][32] chunks)
+        float* dvo = (a.dv_out && valid)
+                         ? a.dv_out + (a.dvks ? 2L * l * a.dvks + m * 32 : m * a.lddv + (long)l * 64) : nullptr;
+        const long dgo = a.dvks ? a.dvks : 32;   // gate half
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) {
           const int c = 8 * (q0 + bb) + 4 * h;
@@ -2494,7 +2501,7 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
           *(floatx4*)(DVg + r * XS + c) = dvg[bb];
           if (dvo) {
             *(floatx4*)(dvo + c) = dvs[bb];
-            *(floatx4*)(dvo + 32 + c) = dvg[bb];
+            *(floatx4*)(dvo + dgo + c) = dvg[bb];
           }
         }
       }
@@ -3158,6 +3165,7 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   k.ocg = c.ocg; k.ocls = c.ocls; k.dx0_a = c.dx0_a; k.dx0_c = c.dx0_c;
   k.gc_tab = c.gc_tab; k.gc_ld = c.gc_ld; k.ids = c.ids; k.cond = c.cond; k.ldcond = c.ldcond;
   k.dv_out = c.dv_out; k.lddv = c.lddv; k.gc_dtab = c.gc_dtab; k.tile_gid = c.tile_gid;
+  k.dvks = c.dvks;
   k.flags = c.flags; k.status = c.status;
   k.B = c.B; k.T = c.T; k.H = c.H; k.L = c.L; k.nbl = c.nbl; k.Cd = c.Cd;
   k.trace = c.trace ? c.trace + 16L * c.L : nullptr; k.trace_blk = c.trace_blk;
