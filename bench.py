@@ -437,7 +437,7 @@ class TrainBench:
                'peak': peak / 1e12 if bound == 'mfma' else peak / 1e9,
                'unit': 'TFLOP/s' if bound == 'mfma' else 'GB/s', 'frac': ach / peak,
                'avg_launch_us': avg * 1e6, 'work_per_launch': work,
-               'traffic': traffic_from_profiles(name) if traffic else None}
+               'traffic': traffic_from_profiles(name, traffic if isinstance(traffic, str) else None) if traffic else None}
         if bound == 'mfma':
             out['arith'] = ('bf16-split (6 products) for dx and dSIG/dGATE, f32 MFMA for dz and dRES'
                             if x3 and name == 'layer_bwd' else ('bf16-split' if x3 else 'f32 MFMA'))
@@ -538,7 +538,7 @@ DEFAULT_TILE = '128'    # the library's default chain form (engine.cpp, LBWN_CHA
 CANDS = ['layer_bwd', 'dskip', 'layer_fwd', 'post1_fwd', 'dpost1', 'ds', 'post2_fwd', 'dpost2', 'dh']
 
 
-def sub_bench(arch_file, B, T, dp, steps, warmup, gc=None, backward=True, label=''):
+def sub_bench(arch_file, B, T, dp, steps, warmup, gc=None, backward=True, label='', traffic_tag=None):
     """A secondary configuration (C1 / C4 / C5-per-GPU) in the same run."""
     from lbwn.arch import load_arch
     arch = load_arch(arch_file, num_global_cond=gc)
@@ -548,8 +548,8 @@ def sub_bench(arch_file, B, T, dp, steps, warmup, gc=None, backward=True, label=
            'value': dp.world * B * T / (ms / 1000.0), 'unit': 'audio samples/s', 'ms_per_step': ms,
            'steps': steps, 'warmup': warmup}
     if dom:
-        out['roofline'] = tb.roof(dom, samples[dom], traffic=False)
-        out['roofline_dilconv'] = tb.roof('layer_fwd', samples['layer_fwd'], traffic=False)
+        out['roofline'] = tb.roof(dom, samples[dom], traffic=traffic_tag or False)
+        out['roofline_dilconv'] = tb.roof('layer_fwd', samples['layer_fwd'], traffic=traffic_tag or False)
     tb.close()
     return out
 
@@ -701,13 +701,13 @@ def main(argv=None):
     if world == 1 and not args.no_extras and args.arch is None:
         par = lambda f: os.path.join(ROOT, 'par', f)   # noqa: E731
         out['c4'] = sub_bench(par('arch5.json'), 32, 4096, dp, 10, 3, label='C4: arch5 deep stack, B=32 x T=4096, '
-                              'train fwd+bwd+Adam, 1 GPU')
+                              'train fwd+bwd+Adam, 1 GPU', traffic_tag='c4')
         out['c4']['sweep'] = {'default_tile': os.environ.get('LBWN_CHAIN_TILE') or DEFAULT_TILE,
                               'tiles': [chain_dilation_sweep(par('arch5.json'), 32, 4096, dp, tile=t)
                                         for t in ('128', '64', 'w32')]}
         out['c5_per_gpu'] = sub_bench(par('arch5.json'), 8, 4096, dp, 10, 3,
                                       label='C5 per-GPU share on one GPU: arch5, B=8 x T=4096 (the N>1 runs '
-                                            'default to this per rank: scaling reference)')
+                                            'default to this per rank: scaling reference)', traffic_tag='c5')
         out['c1'] = sub_bench(par('arch1.json'), 2, 512, dp, 20, 5, backward=False,
                               label='C1: arch1 (GC 17/377), B=2 x T=512, forward + masked xent loss')
         if not args.no_cpu_baseline:
@@ -726,11 +726,12 @@ def main(argv=None):
     return 0
 
 
-def traffic_from_profiles(kernel):
-    """HBM bytes per launch from the committed PMC summary (profiles/pmc_traffic.json,
-    written by tools/pmc_traffic.py from separate rocprofv3 --pmc passes, FETCH_SIZE x2
-    gfx950 correction), or None when not collected."""
-    p = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+def traffic_from_profiles(kernel, tag=None):
+    """HBM bytes per launch from the committed PMC summary (profiles/pmc_traffic.json for the
+    headline C2 configuration, profiles/pmc_traffic_<tag>.json for another one, written by
+    tools/pmc_traffic.py from separate rocprofv3 --pmc passes, FETCH_SIZE x2 gfx950
+    correction), or None when not collected."""
+    p = os.path.join(ROOT, 'profiles', 'pmc_traffic%s.json' % ('_' + tag if tag else ''))
     try:
         with open(p) as f:
             d = json.load(f)

@@ -21,6 +21,8 @@ timeout -k 10 120 python tools/gen_trace.py 10 > gpurun_out/gentrace_$TAG.txt 2>
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_gen_$TAG -o run -- python tools/gen_bench.py --batch 10 --steps 4000 > gpurun_out/prof_gen_$TAG.log 2>&1 || exit 1
 S=$(find gpurun_out/prof_gen_$TAG -name '*kernel_stats.csv' | head -1)
 python tools/prof_summary.py "$S" gpurun_out/stats_gen_$TAG.md 10 gen_$TAG
-bash tools/pmc_traffic.sh > gpurun_out/pmc_traffic_$TAG.log 2>&1 || exit 1
+TAG= bash tools/pmc_traffic.sh > gpurun_out/pmc_traffic_$TAG.log 2>&1 || exit 1
+TAG=c4 bash tools/pmc_traffic.sh --arch par/arch5.json --batch 32 > gpurun_out/pmc_traffic_c4_$TAG.log 2>&1 || exit 1
+TAG=c5 bash tools/pmc_traffic.sh --arch par/arch5.json --batch 8 > gpurun_out/pmc_traffic_c5_$TAG.log 2>&1 || exit 1
 bash tools/pmc_req.sh > gpurun_out/pmc_req_$TAG.log 2>&1 || exit 1
 echo full ok
