@@ -5,7 +5,7 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 step = int(sys.argv[2]) if len(sys.argv) > 2 else -3
-starts = [i for i, r in enumerate(rows) if 'pack_layers' in r['Kernel_Name']]
+starts = [i for i, r in enumerate(rows) if 'pack_layers' in r['Kernel_Name'] or 'step_prologue' in r['Kernel_Name']]
 i0 = starts[step]
 i1 = starts[step + 1] if step + 1 < len(starts) and step != -1 else len(rows)
 seg = sorted(rows[i0:i1], key=lambda r: int(r['Start_Timestamp']))
