@@ -385,8 +385,9 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->oCPART = carve(cur, sizeof(float) * (size_t)lbwn_colpart_parts(M) * (p->Cp + p->Cs));
   // [status (16 B) | forward hand-off flags | backward hand-off flags], zeroed by ONE memset per
   // step (each flag block padded to 16 B)
-  // one flag per tile of the finest chain tile (64 positions), so any form fits
-  p->nflag_bytes = (sizeof(unsigned) * (size_t)B * ((T + 63) / 64) + 15) / 16 * 16;
+  // one flag per 16-position wave of a tile (the 16-position chains' per-wave hand-offs; the
+  // 32-position forms use one per 128-position tile), so any form fits: ceil(T/TP)·NW <= T/16 + 8
+  p->nflag_bytes = (sizeof(unsigned) * (size_t)B * ((T + 15) / 16 + 8) + 15) / 16 * 16;
   p->oSTATUS = carve(cur, 16 + 2 * p->nflag_bytes);
   p->oFLAGS = p->oSTATUS + 16;
   {
