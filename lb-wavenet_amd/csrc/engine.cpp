@@ -15,7 +15,7 @@
 #include "kernels.h"
 
 struct lbwn_plan {
-  int chain_xcd = 1;       // chain_first's XCD-grouped walk
+  int chain_xcd = 0;       // chain_first's XCD-grouped walk
   bool dv_blk = false;     // the last backward exported DV k-blocked ([2L][m32(M)][32])
   int head_colparts = 0;   // post2-bias column partial rows the last forward's head wrote (0: none)
   lbwn_arch a;
@@ -307,9 +307,11 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   LBWN_REQUIRE(p, "plan: out of host memory");
   p->fwd_nw = fwd_nw;
   p->bwd_nw = bwd_nw;
-  {  // XCD-grouped chain tile walk (layer.hip chain_first); LBWN_CHAIN_XCD=0: tile = block index
+  {  // XCD-grouped chain tile walk (layer.hip chain_first), off by default: same-box A/B
+     // (profiles/r04_ab_handoff_xcd.txt) forward chain 234-235 us with tile = block index, 243 grouped;
+     // backward unchanged.  LBWN_CHAIN_XCD=1 turns it on.
     const char* xv = getenv("LBWN_CHAIN_XCD");
-    p->chain_xcd = !(xv && !strcmp(xv, "0"));
+    p->chain_xcd = xv && !strcmp(xv, "1");
   }
   p->a = *a;
   p->B = B;

@@ -934,6 +934,42 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
   const bool raw = g.split_stride != 0;
   const int rbase = m0 + 32 * wave;
   float cs[NB];
+  if (g.c_chain_ls && !raw) {
+    // dZ in the chain's order (no bias / mask / accumulate): a 4x4 transpose among lanes fr&3
+    // (two xor exchanges) gives each lane one row x 4 consecutive columns = one 16-B run of the
+    // destination; stored write-through (sc1): the 210-MB output streams past the L2 instead of
+    // evicting the B half it holds (xcd2d_tile)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      cs[nb] = 0.f;
+      const int col0 = n0 + nb * 16;
+      if (col0 >= g.N) continue;   // wave-uniform
+      const long chunk = g.c_chain_ls * 4;
+      const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+          C + (long)(col0 >> 5) * g.c_chain_ls, (short)0, (int)(chunk < 0x7fffffffL ? chunk : 0x7fffffffL), 0x00020000);
+      const int c = fr & 3, colq = col0 + 4 * (fr >> 2);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        float a0 = acc[mi][nb][0], a1 = acc[mi][nb][1], a2 = acc[mi][nb][2], a3 = acc[mi][nb][3];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (rbase + 16 * mi + 4 * fq + e < g.M) cs[nb] += acc[mi][nb][e];
+        const bool odd = c & 1, hi = c & 2;
+        {
+          const float r0 = __shfl_xor(odd ? a0 : a1, 1), r1 = __shfl_xor(odd ? a2 : a3, 1);
+          if (odd) { a0 = r0; a2 = r1; } else { a1 = r0; a3 = r1; }
+        }
+        {
+          const float q0 = __shfl_xor(hi ? a0 : a2, 2), q1 = __shfl_xor(hi ? a1 : a3, 2);
+          if (hi) { a0 = q0; a1 = q1; } else { a2 = q0; a3 = q1; }
+        }
+        const int row = rbase + 16 * mi + 4 * fq + c;
+        const int off = row < g.M ? (int)(((((long)(row >> 5) * 4 + ((colq >> 3) & 3)) * 32 + (row & 31)) * 8 + (colq & 7)) * 4)
+                                  : 0x7ffffff0;   // past the record: dropped
+        __builtin_amdgcn_raw_buffer_store_b128((floatx4){a0, a1, a2, a3}, rc, off, 0, 16);
+      }
+    }
+  } else
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     cs[nb] = 0.f;

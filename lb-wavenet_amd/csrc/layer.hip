@@ -556,26 +556,6 @@ LBWN_DEV void publish_flag(unsigned* f, unsigned v) {
   __hip_atomic_store((gu32*)f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Per-wave hand-off wait (the 16-position chains): every lane polls the producer flag of the row
-// it will load (the 16 rows of a wave come from at most two producer waves: one or two distinct
-// words, one request), relaxed agent-scope loads; lanes with need = false pass.  The wave loads its
-// rows itself once its poll has matched (MI355X_MICROARCH.md, valid forms: the polling wave loads
-// after its match, no barrier).  Bounded; a timeout ORs code into the status word and returns
-// false (the caller then skips every later wait).
-LBWN_DEV bool wave_wait_flag_ge(unsigned* f, bool need, unsigned want, unsigned* status, unsigned code) {
-  const long long t0 = wall_clock64();
-  for (;;) {
-    const unsigned v = __hip_atomic_load((gu32*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (__all(!need || v >= want)) return true;
-    if (wall_clock64() - t0 > SPIN_TIMEOUT) {
-      if ((threadIdx.x & 63) == 0)
-        __hip_atomic_fetch_or((gu32*)status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
 // bias + conditioning into the accumulators (acc layout rows = out channel)
 LBWN_DEV void conv_init(const float* bs, const floatx4 (&cv)[8], int h, floatx16& acc_s, floatx16& acc_g) {
 #pragma unroll
@@ -1029,7 +1009,8 @@ LBWN_DEV void conv16_init(const float* bs, const floatx4 (&cv)[4], int q0, int h
 // of the NP parts (4 / NP accumulator blocks) are read before its MFMAs (NP = 2 halves the live
 // fragments for the register-tight LC form)
 template <int NP = 1>
-LBWN_DEV void conv16_tap_v(floatx4 x0, floatx4 x1, const unsigned short* Wt, int i16, int g, floatx4 (&acc)[4]) {
+LBWN_DEV void conv16_tap(const float* xrow, const unsigned short* Wt, int i16, int g, floatx4 (&acc)[4]) {
+  const floatx4 x0 = *(const floatx4*)(xrow + 8 * g), x1 = *(const floatx4*)(xrow + 8 * g + 4);
   bf16x8 xb[3];
 #pragma unroll
   for (int part = 0; part < NP; ++part) {
@@ -1046,10 +1027,6 @@ LBWN_DEV void conv16_tap_v(floatx4 x0, floatx4 x1, const unsigned short* Wt, int
 #pragma unroll
     for (int ii = 0; ii < NB; ++ii) acc[part * NB + ii] = mfma16x3(wf[ii], xb, acc[part * NB + ii]);
   }
-}
-template <int NP = 1>
-LBWN_DEV void conv16_tap(const float* xrow, const unsigned short* Wt, int i16, int g, floatx4 (&acc)[4]) {
-  conv16_tap_v<NP>(*(const floatx4*)(xrow + 8 * g), *(const floatx4*)(xrow + 8 * g + 4), Wt, i16, g, acc);
 }
 
 // lc·[LC_SIGNAL_l | LC_GATE_l] onto the accumulators: A = LC16 image rows, B = the lane's LC input
@@ -1178,34 +1155,37 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
       const float* br = bias_of(Wl) + 64;
       floatx4 pf[PF];
       FSTAMP(1);
-      if (!DMAIMG) {   // the image of layer l+2 into registers (written after this layer's barrier)
-        const floatx4* src = (const floatx4*)(wsrc + (long)min(l + 2, a.L - 1) * IMGF);
-#pragma unroll
-        for (int i = 0; i < PF; ++i) pf[i] = src[min(tid + NT * i, IMGF / 4 - 1)];
-      }
-      // The dilated tap's operand x_l[t-d] (channels 8g..8g+7 of this lane's row): rows r >= d from
-      // this tile (LDS, written before the previous layer's barrier); rows r < d from earlier tiles of
-      // the stream -- or the D-sep prepend -- by sc1 loads into registers, once the producer WAVES of
-      // those rows have published layer l.  No block barrier, no LDS staging: for d < 16 only wave 0
-      // waits for another tile.
-      floatx4 g0 = floatx4{0.f, 0.f, 0.f, 0.f}, g1 = g0;
-      if (16 * w < d) {   // wave-uniform
-        const int p = t - d;
-        if (l > 0 && !s_fail) {   // layer 0 reads the embedding (written before the launch)
-          const int pp = max(p, 0), pt = pp / TP, pw = (pp % TP) >> 4;
-          if (!wave_wait_flag_ge(a.flags + ((long)b * tps + pt) * NW + pw, r < d && p >= 0, (unsigned)l, a.status, 1u) &&
-              lane == 0)
-            s_fail = 1;
+      // wait for the producer of the halo rows
+      const int ptt = tt - max(1, d / TP);
+      if (l > 0 && ptt >= 0) {
+        if (tid == 0 && !s_fail) {
+          if (!wait_flag_ge(a.flags + (long)b * tps + ptt, (unsigned)l, a.status, 1u)) s_fail = 1;
         }
-        FSTAMP(2);
+        __syncthreads();
+      }
+      FSTAMP(2);
+      {  // halo rows [0, min(d,TP)): sc1 loads (clamped rows), then the image of layer l+2 behind them
+        const int nh = min(d, TP);
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc(xl, (short)0, (int)((long)(a.H + a.T) * 32 * 4), BUF_DW3);
-        // rows r >= d come from LDS: their loads get an offset past the buffer (no memory access,
-        // the value is 0 and unused)
-        const int off = r < d ? ((a.H + p) * 32 + 8 * g) * 4 : 0x7ffffff0;
-        g0 = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
-        g1 = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 16);
+        floatx4 hv[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int e = min(tid + NT * i, nh * 8 - 1), row = e >> 3, c4 = (e & 7) * 4;
+          hv[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((a.H + t0 + row - d) * 32 + c4) * 4, 0, 16);
+        }
+        if (!DMAIMG) {
+          const floatx4* src = (const floatx4*)(wsrc + (long)min(l + 2, a.L - 1) * IMGF);
+#pragma unroll
+          for (int i = 0; i < PF; ++i) pf[i] = src[min(tid + NT * i, IMGF / 4 - 1)];
+        }
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int e = tid + NT * i;
+          *(floatx4*)(HALO + (e >> 3) * XS + (e & 7) * 4) = hv[i];
+        }
       }
+      __syncthreads();
       FSTAMP(3);
       // residual weights (RT rows 16rb + i16, k group g) read now
       bf16x8 rf[2][3];
@@ -1218,15 +1198,8 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
       }
       __builtin_amdgcn_sched_barrier(0);
       // dilated tap W0·x[t-d], gate
-      {
-        const float* lrow = cur + max(r - d, 0) * XS + 8 * g;
-        floatx4 xd0 = *(const floatx4*)lrow, xd1 = *(const floatx4*)(lrow + 4);
-        if (r < d) {
-          xd0 = g0;
-          xd1 = g1;
-        }
-        conv16_tap_v<LC ? 2 : 1>(xd0, xd1, (const unsigned short*)Wl, i16, g, acc);
-      }
+      const float* xp = (r >= d) ? cur + (r - d) * XS : HALO + r * XS;
+      conv16_tap<LC ? 2 : 1>(xp, (const unsigned short*)Wl, i16, g, acc);
       floatx4 z[2], sg[2];
 #pragma unroll
       for (int bb = 0; bb < 2; ++bb)
@@ -1237,13 +1210,6 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
           sg[bb][j] = sq;
         }
       FSTAMP(4);
-      // LC form: the images this layer's next-layer own tap reads (split image of l+1, LC image of
-      // l+1) came by LDS-DMA after the previous layer's barrier -- landed and visible to every wave
-      // only behind every issuing wave's vmcnt wait and a barrier
-      if (DMAIMG) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-      }
       if (l + 1 < a.L) {
         // residual: x_{l+1} = x_l + br + RES·z → LDS (next layer's rows) and HBM (sc1 for halo rows)
         floatx4 accr[2];
@@ -1279,14 +1245,12 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
         if (LC) lc16_terms(LCIu, lcv, i16, g, acc);
       }
       FSTAMP(5);
-      // every wave's rows of x_{l+1} are in LDS and every read of this layer's image is done: the
-      // next layer reads other waves' rows, and the image slot of layer l is refilled below
-      __syncthreads();
-      FSTAMP(9);
-      // publish x_{l+1} per wave: each wave drains its own stores, then its lane 0 signals for it
+      // publish x_{l+1}: every wave drains its stores, barrier, one lane signals
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0 && l + 1 < a.L) publish_flag(a.flags + (long)tile * NW + w, (unsigned)(l + 1));
+      FSTAMP(9);
+      __syncthreads();
       FSTAMP(10);
+      if (tid == 0 && l + 1 < a.L) publish_flag(a.flags + tile, (unsigned)(l + 1));
       if (LC && l + 2 < a.L) dma_lc16_image<NW>(a.lcimg, l + 2, LCI, w, lane);
       if (DMAIMG && l + 2 < a.L) {
         const float* src = wsrc + (long)(l + 2) * IMGF + lane * 4;
