@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 second pass: PMC traffic for C4 / C5 (sub-benchmark rooflines), dZ read-request split,
-# and same-box A/Bs of the chains' XCD-grouped tile walk and dZ's 2-D XCD blocking.
+# and dZ's 2-D XCD blocking (time A/B and traffic without it).
 # Usage: bash tools/gpu_r4_pass2.sh TAG
 set -o pipefail
 mkdir -p gpurun_out
@@ -9,5 +9,6 @@ TAG=${1:-r4}
 TAG=c4 bash tools/pmc_traffic.sh --arch par/arch5.json --batch 32 > gpurun_out/pmc_traffic_c4_$TAG.log 2>&1 || exit 1
 TAG=c5 bash tools/pmc_traffic.sh --arch par/arch5.json --batch 8 > gpurun_out/pmc_traffic_c5_$TAG.log 2>&1 || exit 1
 bash tools/pmc_req.sh > gpurun_out/pmc_req_$TAG.log 2>&1 || exit 1
-CONFIGS="arch3:8 arch5:8" bash tools/ab_env.sh "LBWN_CHAIN_XCD=0 LBWN_DZ_XCD=0" "LBWN_CHAIN_XCD=1 LBWN_DZ_XCD=0" "LBWN_CHAIN_XCD=1 LBWN_DZ_XCD=1" > gpurun_out/ab_xcd_$TAG.txt 2>&1 || exit 1
+CONFIGS="arch3:8" bash tools/ab_env.sh "-" "LBWN_DZ_XCD=0" > gpurun_out/ab_dzxcd_$TAG.txt 2>&1 || exit 1
+TAG=dz0 LBWN_DZ_XCD=0 bash tools/pmc_traffic.sh > gpurun_out/pmc_traffic_dz0_$TAG.log 2>&1 || exit 1
 echo pass2 ok
