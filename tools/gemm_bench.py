@@ -18,7 +18,9 @@ SHAPES = [('skip_fwd', M, 512, 1600, 1, 0, 1), ('dz', M, 1600, 512, 1, 1, 1), ('
           # dLCCAT = lcᵀ·DV (K = 80 channels, or padded to 96)
           ('lc_cond', M, 3200, 80, 1, 0, 1), ('lc_cond96', M, 3200, 96, 1, 0, 1),
           ('lc_dlc', M, 80, 3200, 1, 1, 1), ('lc_dlc96', M, 96, 3200, 1, 1, 1),
-          ('lc_dcat', 80, 3200, M, 0, 0, 8), ('lc_dcat96', 96, 3200, M, 0, 0, 8)]
+          ('lc_dcat', 80, 3200, M, 0, 0, 8), ('lc_dcat96', 96, 3200, M, 0, 0, 8),
+          # C4 (arch5 B = 32): dlc over M = 131072
+          ('lc_dlc_c4', 4 * M, 80, 3200, 1, 1, 1), ('lc_dlc_c4_128', 4 * M, 128, 3200, 1, 1, 1)]
 
 
 def timeit(fn, reps=20):
