@@ -70,8 +70,6 @@ struct lbwn_plan {
   hipEvent_t ev_chain = nullptr, ev_join2 = nullptr;
   hipEvent_t ev_fwd_fork = nullptr, ev_fwd_up = nullptr;   // forward: LC upsample on aux2
   hipEvent_t ev_upb = nullptr;   // backward: the upsample's per-frame pass done (main) -> its sum (aux2)
-  hipEvent_t ev_dlc = nullptr;   // backward (lc_tail): dlc done (main) -> dLCcat (aux2)
-  int lc_tail = 1;               // LBWN_LC_TAIL=0: dLCcat beside dlc (the round-3 order)
   bool up_forked = false;        // this forward launched the fused upsample on aux2
   bool bwd_chain_event = false;  // the last backward recorded ev_chain (lbwn_plan_stream_wait)
   bool wpk_valid = false;        // the f32 layer images were packed this step
@@ -86,7 +84,6 @@ struct lbwn_plan {
     if (ev_fwd_fork) (void)hipEventDestroy(ev_fwd_fork);
     if (ev_fwd_up) (void)hipEventDestroy(ev_fwd_up);
     if (ev_upb) (void)hipEventDestroy(ev_upb);
-    if (ev_dlc) (void)hipEventDestroy(ev_dlc);
     if (ev_join2) (void)hipEventDestroy(ev_join2);
   }
   // one-shot event probe
@@ -315,8 +312,6 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
      // backward unchanged.  LBWN_CHAIN_XCD=1 turns it on.
     const char* xv = getenv("LBWN_CHAIN_XCD");
     p->chain_xcd = xv && !strcmp(xv, "1");
-    const char* lv = getenv("LBWN_LC_TAIL");
-    p->lc_tail = !(lv && !strcmp(lv, "0"));
   }
   p->a = *a;
   p->B = B;
@@ -358,10 +353,6 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     // so 512 blocks measured slower: C5 per GPU 3.11 -> 3.06 ms at 256 blocks, same box)
     const long dtiles = (M + 255) / 256 * ((p->Lo + 127) / 128);
     p->split_dlcx = (int)std::max<long>(1, std::min<long>(256 / std::max<long>(1, dtiles), (2L * L * p->Cd) / 256));
-    if (const char* sv = getenv("LBWN_DLC_SPLIT")) {   // same-box A/B switch
-      const int v = atoi(sv);
-      if (v >= 1 && v <= 16) p->split_dlcx = v;
-    }
     p->split_floats = std::max(p->split_floats, (long)p->split_dlcx * M * p->Lo);
     long rows = (long)B * (T / hop);
     for (int i = 0; i < p->nup; ++i) {
@@ -518,7 +509,6 @@ int ensure_device(lbwn_plan* p) {
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_fwd_fork, hipEventDisableTiming));
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_fwd_up, hipEventDisableTiming));
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_upb, hipEventDisableTiming));
-    LBWN_HIP(hipEventCreateWithFlags(&p->ev_dlc, hipEventDisableTiming));
   }
   return 0;
 }
@@ -1091,11 +1081,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     // and the LC upsample backward once dlc (main stream) is done: small latency-bound GEMMs that
     // fill the room dSKIP leaves.
     float* SPLA = p->oSPLIT_AUX ? at<float>(ws, p->oSPLIT_AUX) : SPL;
-    // LC tail (p->lc_tail): dLCcat waits for dlc instead of running beside it -- both stream the
-    // DV export (1.68 GB at C4) from HBM, and side by side dlc took 1.13 ms against 0.46 alone
-    // (tools/gemm_bench.py lc_dlc_c4); dLCcat then runs beside the upsample backward and dSKIP
-    const bool lc_after = p->Lo > 0 && p->lc_tail && p->aux2;
-    if (p->Lo > 0 && !lc_after && (e = lc_wgrad(p, G, ws, SPLA, rst))) return e;
+    if (p->Lo > 0 && (e = lc_wgrad(p, G, ws, SPLA, rst))) return e;
     if ((e = lbwn_pre_grad_launch(wav_q, at<float>(ws, p->oGA[0]), at<float>(ws, p->oGC0[0]), 1, B, T, Cr, Q, G->pre,
                                   G->pre_b, at<float>(ws, p->oSPLIT2), rst)))
       return e;
@@ -1110,11 +1096,6 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     // behind dLCcat on the side stream the upsample backward was the last thing to finish)
     if (p->Lo > 0) {
       if ((e = lc_dlc(p, P, ws, SPL, st))) return e;
-      if (lc_after) {
-        LBWN_HIP(hipEventRecord(p->ev_dlc, st));
-        LBWN_HIP(hipStreamWaitEvent(rst, p->ev_dlc, 0));
-        if ((e = lc_wgrad(p, G, ws, SPLA, rst))) return e;
-      }
       if ((e = lc_upsample_bwd(p, P, G, ws, mel, SPL, st, rst))) return e;   // its frame sum on the side
     }
     if (p->aux2) LBWN_HIP(hipEventRecord(p->ev_join2, rst));
