@@ -217,8 +217,33 @@ __global__ __launch_bounds__(256) void head_reg_kernel(lbwn_head_args a) {
   float cs[QV];
 #pragma unroll
   for (int j = 0; j < QV; ++j) cs[j] = 0.f;
-  for (long m = (long)blockIdx.x * 4 + w; m < M; m += (long)gridDim.x * 4) {
+  // the next row's logits and target are loaded while this row is processed (one row of HBM
+  // latency in flight per wave instead of none)
+  const long stride = (long)gridDim.x * 4;
+  long m = (long)blockIdx.x * 4 + w;
+  float vn[QV];
+  int tn = 0, idn = 0;
+  {
+    const long mc = min(m, M - 1), mq = min(mc + 1, M - 1);
+#pragma unroll
+    for (int j = 0; j < QV; ++j) vn[j] = a.logits[mc * Q + min(lane + 64 * j, Q - 1)];
+    tn = a.q[mq];
+    idn = a.ids[mq];
+  }
+  for (; m < M; m += stride) {
     float* row = a.logits + m * Q;
+    float v[QV];
+#pragma unroll
+    for (int j = 0; j < QV; ++j) v[j] = (lane + 64 * j < Q) ? vn[j] : -INFINITY;
+    const int tgt = tn;
+    const bool valid = idn != 0;   // tmodel.py:232
+    {
+      const long mc = min(m + stride, M - 1), mq = min(mc + 1, M - 1);
+#pragma unroll
+      for (int j = 0; j < QV; ++j) vn[j] = a.logits[mc * Q + min(lane + 64 * j, Q - 1)];
+      tn = a.q[mq];
+      idn = a.ids[mq];
+    }
     const int t = (int)(m % a.T);
     if (t == a.T - 1) {  // logits_out[:, :-1] (tmodel.py:231): the last position has no target
       if (a.write_grad)
@@ -227,11 +252,6 @@ __global__ __launch_bounds__(256) void head_reg_kernel(lbwn_head_args a) {
           if (lane + 64 * j < Q) row[lane + 64 * j] = 0.f;
       continue;
     }
-    const int tgt = a.q[m + 1];
-    const bool valid = a.ids[m + 1] != 0;   // tmodel.py:232
-    float v[QV];
-#pragma unroll
-    for (int j = 0; j < QV; ++j) v[j] = (lane + 64 * j < Q) ? row[lane + 64 * j] : -INFINITY;
     float mx = -INFINITY;
     int am = 0x7fffffff;
 #pragma unroll
@@ -349,23 +369,27 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(ColsumJobs jb, int 
     *(floatx4*)(part + (long)blockIdx.x * N + 4 * t) = tot;
   }
 }
-// 256 threads (4 part lanes × 64 columns): a 1024-thread block needs 16 free wave slots on one
-// CU, which beside a resident layer chain and the aux-stream GEMMs it waited ~430 µs for
+// 256 threads = 16 part lanes × 16 columns per block (grid: N/16 column blocks × jobs): each lane
+// sums every 16th partial row in order, then the 16 lane sums are added in order (deterministic).
+// (4 part lanes × 64 columns left 256-deep serial sums per thread once the head wrote 1024
+// partial rows: 21 µs for the three bias sums)
 __global__ __launch_bounds__(256) void colsum_final_kernel(ColsumJobs jb) {
-  __shared__ float red[256];
+  __shared__ float red[16][17];
   const int j = blockIdx.y, N = jb.N[j], nparts = jb.nparts[j];
   const float* part = jb.ws[j];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), lane = threadIdx.x >> 6;  // 4 part lanes
-  if (blockIdx.x * 64 >= N) return;   // block-uniform
+  const int cl = threadIdx.x & 15, lane = threadIdx.x >> 4, c = blockIdx.x * 16 + cl;
+  if (blockIdx.x * 16 >= N) return;   // block-uniform
   float s = 0.f;
   if (c < N) {
 #pragma unroll 8
-    for (int p = lane; p < nparts; p += 4) s += part[(long)p * N + c];
+    for (int p = lane; p < nparts; p += 16) s += part[(long)p * N + c];
   }
-  red[threadIdx.x] = s;
+  red[lane][cl] = s;
   __syncthreads();
-  if (threadIdx.x < 64 && c < N) {
-    const float tot = ((red[threadIdx.x] + red[64 + threadIdx.x]) + red[128 + threadIdx.x]) + red[192 + threadIdx.x];
+  if (threadIdx.x < 16 && c < N) {
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) tot += red[k][cl];
     float* out = jb.out[j];
     for (int r = 0; r < max(1, jb.reps[j]); ++r) {
       float* o = out + (long)r * N + c;
@@ -580,7 +604,7 @@ int lbwn_colsum_multi_launch(int njobs, const float* const* X, const long* ldx, 
     nmax = std::max(nmax, N[j]);
   }
   colsum_partial_kernel<<<dim3(np, njobs), 256, 0, st>>>(jb, M);
-  colsum_final_kernel<<<dim3((nmax + 63) / 64, njobs), 256, 0, st>>>(jb);
+  colsum_final_kernel<<<dim3((nmax + 15) / 16, njobs), 256, 0, st>>>(jb);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
@@ -610,7 +634,7 @@ int lbwn_colsum_final_launch(int njobs, float* const* parts, const int* N, float
     jb.reps[j] = reps ? reps[j] : 1;
     nmax = std::max(nmax, N[j]);
   }
-  colsum_final_kernel<<<dim3((nmax + 63) / 64, njobs), 256, 0, st>>>(jb);
+  colsum_final_kernel<<<dim3((nmax + 15) / 16, njobs), 256, 0, st>>>(jb);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
