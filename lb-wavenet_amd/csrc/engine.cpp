@@ -47,6 +47,7 @@ struct lbwn_plan {
   int split_dlc, split_dlcx, split_up[8];
   size_t oSPLIT_AUX = 0;         // split-K workspace of the aux2 stream (LC / GC grads beside dSKIP)
   bool up_fused = false;         // LC upsample as one fused launch per direction (cond.hip)
+  bool up_fused_bwd = false;     // ... for the backward (LBWN_LC_UP=bwdgemm: per-stage GEMMs there)
   size_t oUPPART = 0;            // its per-frame filter-gradient partials
   size_t total;
   long x_layer_stride;  // floats
@@ -420,6 +421,16 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     }
     p->oCOND = p->Lo ? carve(cur, f * (size_t)M * ncond) : 0;
     p->up_fused = p->Lo > 0 && lbwn_lc_up_fused_ok(p->nup, p->up, p->Li, p->Lo);
+    {  // The fused backward runs one block per mel frame at one block per CU: past one round of
+       // frames the per-stage GEMMs win (same box, profiles/r04_ab_lc_upsample.txt: arch5 B=8, 128
+       // frames, fused 2.817-2.829 ms vs GEMMs 2.955-2.957; B=32, 512 frames, fused 10.67-10.68 vs
+       // 10.56-10.57).  LBWN_LC_UP=fused / gemm / bwdgemm overrides (same-box A/B switch).
+      const char* uv = getenv("LBWN_LC_UP");
+      const long frames = M / hop;
+      if (uv && !strcmp(uv, "gemm")) p->up_fused = false;
+      p->up_fused_bwd = p->up_fused && (uv && !strcmp(uv, "fused") ? true
+                                        : uv && !strcmp(uv, "bwdgemm") ? false : frames <= 256);
+    }
     if (p->up_fused) p->oUPPART = carve(cur, f * (size_t)lbwn_lc_up_part_floats(p->nup, p->up, p->Li, p->Lo, (int)(M / hop)));
     p->oDVALL = p->Lo ? carve(cur, f * (size_t)m32(M) * ncond) : 0;   // rows or [2L][m32(M)][32]
     p->oLCCAT = p->Lo ? carve(cur, f * (size_t)p->Lo * ncond) : 0;
@@ -675,7 +686,7 @@ int lc_upsample_bwd(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G, vo
                     hipStream_t st, hipStream_t st_sum = nullptr) {
   int e;
   const float* dout = at<float>(ws, p->oDLC[0]);
-  if (p->up_fused) {
+  if (p->up_fused_bwd) {
     const float* F[8];
     float* act[8];
     for (int i = 0; i < p->nup; ++i) { F[i] = P->lc_up[i]; act[i] = at<float>(ws, p->oLCACT[i]); }
