@@ -1116,8 +1116,8 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
       // C2 = 1280 = 5 rounds) instead of 128-column ones (13 column tiles, the last half empty:
       // 1664 = 6.5 rounds)
       grid.x = (unsigned)(((a.M + 255) / 256) * (a.N / 160));
-      static const int x2 = [] { const char* e = getenv("LBWN_DZ_XCD"); return (e && e[0] == '0') ? 0 : 1; }();
-      g.xcd2d = x2;   // LBWN_DZ_XCD=0: the 1-D remap (same-box A/B switch)
+      const char* xe = getenv("LBWN_DZ_XCD");
+      g.xcd2d = (xe && xe[0] == '0') ? 0 : 1;   // LBWN_DZ_XCD=0: the 1-D remap (same-box A/B switch)
       gemm_x3q_kernel<10><<<grid, 512, 0, st>>>(g);
     } else if (X3Q) {
       gemm_x3q_kernel<8><<<grid, 512, 0, st>>>(g);

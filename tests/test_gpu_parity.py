@@ -496,3 +496,31 @@ def test_adam_kernel_ragged(lib, n, nw):
     np.testing.assert_allclose(m.cpu().numpy(), md, rtol=1e-6, atol=1e-7)
     np.testing.assert_allclose(v.cpu().numpy(), vd, rtol=1e-6, atol=1e-7)
     np.testing.assert_allclose(p.cpu().numpy(), pd, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize('env', [{'LBWN_CHAIN_XCD': '1'}, {'LBWN_DZ_XCD': '0'}])
+def test_placement_switches_bitwise(monkeypatch, env):
+    """The placement-only switches change which block (and so which XCD) computes a tile, never
+    the arithmetic of a tile: the XCD-grouped chain walk (layer.hip chain_first) and dZ's 1-D
+    tile remap instead of the 2-D XCD blocking (gemm.hip xcd2d_tile) give the default plan's
+    outputs and gradients bit for bit (arch3, 128 tiles per chain)."""
+    arch = arch3()
+    B, T = 4, 4096
+    q, ids = rand_batch(arch, B, T)
+    out = []
+    for use in (False, True):
+        for k, v in env.items():
+            if use:
+                monkeypatch.setenv(k, v)
+            else:
+                monkeypatch.delenv(k, raising=False)
+        net = make_net(arch, B)
+        net.forward(q, None, ids, backward=True)
+        torch.cuda.synchronize()
+        assert int(net.plan_tensor(T, 'status').view(torch.int32)[0]) == 0
+        out.append((net.stats[:3].cpu().numpy(), net.save_flat.cpu().numpy(),
+                    {n: g.cpu().numpy() for n, g in net.grads.items()}))
+    (s0, v0, g0), (s1, v1, g1) = out
+    assert np.array_equal(s0, s1) and np.array_equal(v0, v1)
+    for n in g0:
+        assert np.array_equal(g0[n], g1[n]), n
