@@ -806,12 +806,22 @@ __global__ __launch_bounds__(512, 1) void gemm_x3r_kernel(lbwn_gemm_args g) {
 // four lanes cover its 128-B line) and B[8q + j][16ni + r]; the k-step runs as two halves of 4
 // column blocks.
 // LBWN_GEMM_WIDE=0 keeps dZ on 128-column tiles (same-box A/B switch)
+// LBWN_GEMM_AMN=0 keeps the mn-contiguous weight-gradient products on the LDS-staged kernel
+static bool lbwn_gemm_amn() {
+  const char* e = getenv("LBWN_GEMM_AMN");
+  return !(e && e[0] == '0');
+}
 static bool lbwn_gemm_wide_tiles() {
   static const int v = [] { const char* e = getenv("LBWN_GEMM_WIDE"); return (e && e[0] == '0') ? 0 : 1; }();
   return v != 0;
 }
 
-template <int NB>   // 16-column blocks: 8 (128 columns), 10 (160: dZ's N = 1600) or 6 (96: N <= 96, arch5's dlc)
+// AMN: the weight-gradient form (dSKIP, dPOST1, dPOST2: A and B both mn-contiguous, K = the
+// positions): each lane loads its A fragment values as scalars -- per k row one 64-B run of 16
+// consecutive rows i, the same bytes as the k-contiguous form's two 32-B runs -- and splits them in
+// registers as above (A never passes through the LDS); B is staged like the LDS-staged kernel's
+// mn-contiguous operand (4(k) x 4(n) blocks transposed in registers, split, written as planes).
+template <int NB, bool AMN = false>   // 16-column blocks: 8 (128 columns), 10 (160: dZ's N = 1600) or 6 (96: N <= 96, arch5's dlc)
 __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
   // the k-step's column blocks run in NP parts of NH (B fragments live for one part: NB = 10 in
   // two parts of 5 spilled 32 VGPRs)
@@ -828,7 +838,7 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
   const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
   const int kz0 = gemm_split() * g.k_per_split;
   const int kz1 = min(g.K, kz0 + g.k_per_split);
-  const int ntiles = (kz1 - kz0) / X3_BK;   // K % 32 == 0 (pre-split B)
+  const int ntiles = (kz1 - kz0) / X3_BK;   // K % 32 == 0 (pre-split B; AMN: checked by the launcher)
   const int last = max(ntiles - 1, 0);
 
   floatx4 acc[2][NB];
@@ -839,16 +849,27 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
 
   const int fr = lane & 15, fq = lane >> 4;
   const long aks = g.a_kstride ? g.a_kstride : X3_BK;   // floats per 32-deep k-step of A
-  const float* pa0 = g.A + (long)min(m0 + 32 * wave + fr, g.M - 1) * g.lda + (kz0 / X3_BK) * aks + 8 * fq;
-  const float* pa1 = g.A + (long)min(m0 + 32 * wave + 16 + fr, g.M - 1) * g.lda + (kz0 / X3_BK) * aks + 8 * fq;
+  const float* pa0 = AMN ? g.A + min(m0 + 32 * wave + fr, g.M - 1) + (long)(kz0 + 8 * fq) * g.lda
+                         : g.A + (long)min(m0 + 32 * wave + fr, g.M - 1) * g.lda + (kz0 / X3_BK) * aks + 8 * fq;
+  const float* pa1 = AMN ? g.A + min(m0 + 32 * wave + 16 + fr, g.M - 1) + (long)(kz0 + 8 * fq) * g.lda
+                         : g.A + (long)min(m0 + 32 * wave + 16 + fr, g.M - 1) * g.lda + (kz0 / X3_BK) * aks + 8 * fq;
   const int alo = g.relu_a ? 0 : (int)0x80000000;   // relu as an integer max (x3_store4)
   floatx4 av[2][4];
   auto a_load = [&](auto sset, int kt) {
     constexpr int S = decltype(sset)::value;
-    av[S][0] = *(const floatx4*)(pa0 + kt * aks);
-    av[S][1] = *(const floatx4*)(pa0 + kt * aks + 4);
-    av[S][2] = *(const floatx4*)(pa1 + kt * aks);
-    av[S][3] = *(const floatx4*)(pa1 + kt * aks + 4);
+    if (AMN) {   // A[i][k] at A[k·lda + i]: k rows 32kt + 8fq + j
+      const long ko = (long)kt * X3_BK * g.lda;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        av[S][j >> 2][j & 3] = pa0[ko + j * g.lda];
+        av[S][2 + (j >> 2)][j & 3] = pa1[ko + j * g.lda];
+      }
+    } else {
+      av[S][0] = *(const floatx4*)(pa0 + kt * aks);
+      av[S][1] = *(const floatx4*)(pa0 + kt * aks + 4);
+      av[S][2] = *(const floatx4*)(pa1 + kt * aks);
+      av[S][3] = *(const floatx4*)(pa1 + kt * aks + 4);
+    }
   };
   auto a_split = [&](auto sset, int mi, bf16x8 (&f)[3]) {
     constexpr int S = decltype(sset)::value;
@@ -861,15 +882,28 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
     split8(x, y, f);
   };
 
+  // B: pre-split planes copied to LDS, or (AMN) an mn-contiguous f32 operand split on the way
   X3Pre<BN, NTHR> sp;
-  sp.init(g.b3, g.K / X3_BK, n0, g.N, kz0, tid);
+  X3Stage<false, true, BN, NTHR> sm_b;
+  auto b_load = [&](auto sset, int kt) {
+    constexpr int S = decltype(sset)::value;
+    if (AMN) sm_b.template load<S>(kt, 0);
+    else sp.template load<S>(kt);
+  };
+  auto b_store = [&](auto sset, unsigned short* lds) {
+    constexpr int S = decltype(sset)::value;
+    if (AMN) sm_b.template store<S>(lds, tid, false);
+    else sp.template store<S>(lds);
+  };
+  if (AMN) sm_b.init(g.B, g.ldb, n0, g.N, kz0, tid);
+  else sp.init(g.b3, g.K / X3_BK, n0, g.N, kz0, tid);
   if (ntiles > 0) {
-    sp.load(0);
-    sp.store(smem);
+    b_load(std::integral_constant<int, 0>(), 0);
+    b_store(std::integral_constant<int, 0>(), smem);
     a_load(std::integral_constant<int, 0>(), 0);
     a_load(std::integral_constant<int, 1>(), min(1, last));
-    sp.template load<1>(min(1, last));
-    sp.template load<0>(min(2, last));
+    b_load(std::integral_constant<int, 1>(), min(1, last));
+    b_load(std::integral_constant<int, 0>(), min(2, last));
   }
   __syncthreads();
   const int fb_off = fr * X3_ROW + 8 * fq;
@@ -904,8 +938,8 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
     a_split(std::integral_constant<int, S>(), 0, fn[0]);
     a_split(std::integral_constant<int, S>(), 1, fn[1]);
     a_load(std::integral_constant<int, S>(), min(kt + 3, last));
-    sp.template store<S>(nxt);
-    sp.template load<S>(min(kt + 3, last));
+    b_store(std::integral_constant<int, S>(), nxt);
+    b_load(std::integral_constant<int, S>(), min(kt + 3, last));
 #pragma unroll
     for (int part = 1; part < NP; ++part) {
       b_frags(cur, part, fb);
@@ -1106,6 +1140,17 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
   int e = gemm_setup(a, a_kcontig, b_kcontig, split_k, slab_ws, X3_BK, 64 * wm, 128, g, grid);
   if (e) return e;
   const bool kfull = a.K % X3_BK == 0, pre = a.b3 != nullptr;
+  if (X3Q && !a_kcontig && !b_kcontig && kfull && !pre && !a.mask && !a.bias && !a.colpart && !a.c_chain_ls &&
+      !a.b_gstride && a.M >= 256 && a.N % 4 == 0 && ((a.M + 255) / 256) * ((a.N + 127) / 128) >= 8 &&
+      lbwn_gemm_amn()) {
+    // the weight-gradient products with >= 8 output tiles (dSKIP, dPOST1): 256 x 128 tiles with A
+    // in registers (gemm_x3q_kernel AMN).  tools/gemm_bench.py, same box: dSKIP split 9 315 vs
+    // 355 us, dPOST1 split 32 97 vs 107; dPOST2 (4 tiles) 87 vs 77 stays on the 2-per-CU kernel
+    if ((e = gemm_setup(a, a_kcontig, b_kcontig, split_k, slab_ws, X3_BK, 256, 128, g, grid))) return e;
+    gemm_x3q_kernel<8, true><<<grid, 512, 0, st>>>(g);
+    LBWN_CHECK_LAUNCH();
+    return splitk_finish(a, split_k, slab_ws, st);
+  }
   if (wm == 4 && X3R && kfull && pre && a_kcontig) {
     if (a.N <= 96) {   // 96-column tiles: the grid is re-formed for them
       grid.x = (unsigned)(((a.M + 255) / 256) * ((a.N + 95) / 96));
