@@ -2665,11 +2665,13 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
 }
 
 // Sum every layer's slab partials: grid (column groups, L).
-__global__ __launch_bounds__(256) void layer_reduce_all_kernel(RedK a, long slab_layer, long dsig_l, long dres_l,
-                                                               long db_l) {
+// At most 32 VGPRs (22 at this writing, -Rpass-analysis=kernel-resource-usage): it runs on the side stream beside dSKIP's A-in-registers GEMM
+// blocks (2 waves of 240 VGPRs per SIMD leave 32), so it must fit in what they leave free or it
+// waits for them.  Parts p8, p8 + 8, ... in order (the order of slab_group_prefetch/finish).
+__global__ __launch_bounds__(256) void layer_reduce_all_kernel(
+    RedK a, long slab_layer, long dsig_l, long dres_l, long db_l) {
   __shared__ float scratch[256];
-  float pre[RED_PARTS];
-  const int l = blockIdx.y;
+  const int l = blockIdx.y, tid = threadIdx.x;
   RedK k = a;
   k.slab = a.slab + l * slab_layer;
   k.dsig = a.dsig + l * dsig_l;
@@ -2678,8 +2680,25 @@ __global__ __launch_bounds__(256) void layer_reduce_all_kernel(RedK a, long slab
   k.dbsig = a.dbsig ? a.dbsig + l * db_l : nullptr;
   k.dbgate = a.dbgate ? a.dbgate + l * db_l : nullptr;
   k.dbres = a.dbres ? a.dbres + l * (long)a.Cr : nullptr;
-  slab_group_prefetch(k, blockIdx.x, pre, threadIdx.x);
-  slab_group_finish(k, blockIdx.x, pre, scratch, threadIdx.x);
+  const int c = blockIdx.x * 32 + (tid & 31), p8 = tid >> 5, cc = min(c, SLAB - 1);
+  float s = 0.f;
+  const float* col = k.slab + cc;
+  const int st = (int)k.stride;
+  for (int p0 = p8; p0 < k.nparts; p0 += 32) {
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = col[min(p0 + 8 * i, k.nparts - 1) * st];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s += (p0 + 8 * i < k.nparts) ? v[i] : 0.f;
+  }
+  scratch[tid] = s;
+  __syncthreads();
+  if (tid < 32 && c < SLAB) {
+    float tot = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tot += scratch[j * 32 + tid];
+    slab_store(k, c, tot);
+  }
 }
 
 // ---- backward ----------------------------------------------------------------------------

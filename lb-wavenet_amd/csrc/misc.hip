@@ -53,9 +53,11 @@ __global__ void shift_add_kernel(float* out, const float* a, const float* c0, in
 // each, so they find room beside dSKIP's GEMM blocks; 128 x 1 and 256 x 2 measured slower).
 constexpr int PG_BLOCKS = 256;
 constexpr int PG_WAVES = 2;
-constexpr int PG_BATCH = 32;
+constexpr int PG_BATCH = 4;    // small: <= 32 VGPRs so the blocks fit beside dSKIP's (see below)
 
-__global__ __launch_bounds__(64 * PG_WAVES) void pre_grad_part_kernel(const int* __restrict__ q,
+// At most 32 VGPRs (27 / 25 for the reduce at this writing): it runs beside dSKIP's A-in-registers GEMM (2 waves of 240 VGPRs per SIMD)
+__global__ __launch_bounds__(64 * PG_WAVES) void pre_grad_part_kernel(
+    const int* __restrict__ q,
                                                                       const float* __restrict__ g,
                                                                       const float* __restrict__ dprev, int gd, int B,
                                                                       int T, int Cr, int Q, float* part, float* bpart) {
@@ -71,22 +73,25 @@ __global__ __launch_bounds__(64 * PG_WAVES) void pre_grad_part_kernel(const int*
   const long chunk = (M + gridDim.x - 1) / gridDim.x, b0 = blockIdx.x * chunk, b1 = min(M, b0 + chunk);
   const long sub = (chunk + nw - 1) / nw, m0 = b0 + wv * sub, m1 = min(b1, m0 + sub);
   float bsum = 0.f;
-  for (long mb = m0 + h; mb < m1; mb += 2 * PG_BATCH) {
+  // 32-bit position arithmetic (M·Cr < 2^31, checked by the launcher): the kernel must stay within
+  // the 32 VGPRs dSKIP's blocks leave per SIMD
+  const int Mi = (int)M, m1i = (int)m1;
+  for (int mb = (int)m0 + h; mb < m1i; mb += 2 * PG_BATCH) {
     int cd[PG_BATCH];
     float v[PG_BATCH], w[PG_BATCH];
 #pragma unroll
     for (int i = 0; i < PG_BATCH; ++i) {   // loads first (clamped indices: no branch per load)
-      const long m = min(mb + 2 * i, m1 - 1);
-      const long ms = min(m + gd, M - 1);
+      const int m = min(mb + 2 * i, m1i - 1);
+      const int ms = min(m + gd, Mi - 1);
       cd[i] = q[m];
       v[i] = g[m * Cr + cc];
       w[i] = dprev[ms * Cr + cc];
     }
 #pragma unroll
     for (int i = 0; i < PG_BATCH; ++i) {
-      const long m = mb + 2 * i;
-      if (m >= m1 || c >= Cr) continue;
-      const float x = v[i] + ((int)(m % T) + gd < T ? w[i] : 0.f);
+      const int m = mb + 2 * i;
+      if (m >= m1i || c >= Cr) continue;
+      const float x = v[i] + (m % T + gd < T ? w[i] : 0.f);
       bsum += x;
       if (cd[i] >= 0 && cd[i] < Q)
         __hip_atomic_fetch_add(hist + cd[i] * 32 + c, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -109,23 +114,39 @@ __global__ __launch_bounds__(64 * PG_WAVES) void pre_grad_part_kernel(const int*
   }
 }
 
-__global__ __launch_bounds__(256) void pre_grad_reduce_kernel(const float* part, const float* bpart, int nparts,
+// 256 threads = 16 part lanes x 16 columns per block: lane pl sums partials pl, pl + 16, ... in
+// order, then the 16 lane sums are added in order (deterministic).  (One thread per column
+// walking all 256 partials ran 50 us beside dSKIP.)
+__global__ __launch_bounds__(256) void pre_grad_reduce_kernel(
+    const float* part, const float* bpart, int nparts,
                                                               int Q, int Cr, float* dpre, float* dpre_b) {
-  const int e = blockIdx.x * 256 + threadIdx.x, n = Q * Cr;
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x & 15, pl = threadIdx.x >> 4;
+  const int e = blockIdx.x * 16 + cl, n = Q * Cr;
   const bool bias = e >= n;
-  if (bias && (dpre_b == nullptr || e - n >= Cr)) return;
-  const float* p = bias ? bpart + (e - n) : part + e;
+  const bool live = bias ? (dpre_b != nullptr && e - n < Cr) : true;
+  const float* p = bias ? bpart + min(e - n, Cr - 1) : part + e;
   const long stride = bias ? Cr : n;
   float s = 0.f;
-  for (int q0 = 0; q0 < nparts; q0 += 32) {
-    float v[32];
+  if (live) {
+    const int sti = (int)stride;
+    for (int q0 = pl; q0 < nparts; q0 += 64) {
+      float v[4];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) v[i] = p[(long)min(q0 + i, nparts - 1) * stride];
+      for (int i = 0; i < 4; ++i) v[i] = p[min(q0 + 16 * i, nparts - 1) * sti];
 #pragma unroll
-    for (int i = 0; i < 32; ++i) s += (q0 + i < nparts) ? v[i] : 0.f;
+      for (int i = 0; i < 4; ++i) s += (q0 + 16 * i < nparts) ? v[i] : 0.f;
+    }
   }
-  if (bias) dpre_b[e - n] = s;
-  else dpre[e] = s;
+  red[pl][cl] = s;
+  __syncthreads();
+  if (threadIdx.x < 16 && live) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    if (bias) dpre_b[e - n] = t;
+    else dpre[e] = t;
+  }
 }
 
 // ---- softmax cross-entropy head ------------------------------------------------------------
@@ -545,13 +566,14 @@ int lbwn_pre_grad_ws_floats(int Q, int Cr) { return PG_BLOCKS * (Q * Cr + Cr); }
 int lbwn_pre_grad_launch(const int* q, const float* g, const float* dprev, int gd, int B, int T, int Cr, int Q,
                          float* dpre, float* dpre_b, float* ws, hipStream_t st) {
   LBWN_REQUIRE(Cr >= 1 && Cr <= 32 && Q >= 1 && Q * 32 * 4 <= 65536, "pre_grad: Cr <= 32 and Q <= 512 required");
+  LBWN_REQUIRE((long)B * T * Cr < (1L << 31), "pre_grad: B*T*Cr must be < 2^31");
   const int nb = PG_BLOCKS, nw = 1;   // one-wave blocks (two-wave blocks wait for LDS)
   float* part = ws;
   float* bpart = ws + (long)PG_BLOCKS * Q * Cr;
   pre_grad_part_kernel<<<nb, 64 * nw, nw * Q * 32 * 4, st>>>(q, g, dprev, gd, B, T, Cr, Q, part, bpart);
   LBWN_CHECK_LAUNCH();
   const int n = Q * Cr + Cr;
-  pre_grad_reduce_kernel<<<(n + 255) / 256, 256, 0, st>>>(part, bpart, nb, Q, Cr, dpre, dpre_b);
+  pre_grad_reduce_kernel<<<(n + 15) / 16, 256, 0, st>>>(part, bpart, nb, Q, Cr, dpre, dpre_b);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
