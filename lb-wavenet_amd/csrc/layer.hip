@@ -2682,14 +2682,18 @@ __global__ __launch_bounds__(256) void layer_reduce_all_kernel(
   k.dbres = a.dbres ? a.dbres + l * (long)a.Cr : nullptr;
   const int c = blockIdx.x * 32 + (tid & 31), p8 = tid >> 5, cc = min(c, SLAB - 1);
   float s = 0.f;
-  const float* col = k.slab + cc;
+  // buffer loads: one 32-bit offset per load instead of a 64-bit address (the VGPR budget above);
+  // parts past nparts read past the record (0, and the zero is never added: nparts bounds it)
   const int st = (int)k.stride;
-  for (int p0 = p8; p0 < k.nparts; p0 += 32) {
-    float v[4];
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(k.slab), (short)0, (int)std::min<long>((long)k.nparts * st * 4, 0x7fffffffL), 0x00020000);
+  for (int p0 = p8; p0 < k.nparts; p0 += 64) {
+    float v[8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = col[min(p0 + 8 * i, k.nparts - 1) * st];
+    for (int i = 0; i < 8; ++i)
+      v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, ((p0 + 8 * i) * st + cc) * 4, 0, 0));
 #pragma unroll
-    for (int i = 0; i < 4; ++i) s += (p0 + 8 * i < k.nparts) ? v[i] : 0.f;
+    for (int i = 0; i < 8; ++i) s += (p0 + 8 * i < k.nparts) ? v[i] : 0.f;
   }
   scratch[tid] = s;
   __syncthreads();
