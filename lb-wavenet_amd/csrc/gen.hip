@@ -882,18 +882,23 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* step
   if (b % a.Bg == 0 && threadIdx.x == 0) *stepc = t0 + n;   // the group's blocks read it at their start
 }
 
+// the head's LDS carve (below) within the kernel's static allocation, at the largest Q (256)
+static_assert(2 * P_LA * 528 + P_MAXB * 516 + 32 * 256 + 272 + 16 * 516 + 16 * 256 <= G_LDS, "head LDS");
+
 LBWN_DEV void persist_head(const PersistK& a, int m, float* sm, int b0, int B, long long* stepc, long long* trace) {
   // B: this group's streams b0 .. b0+B-1 (granule and logit layouts are over all a.B streams)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int L = a.L, Cd = a.Cd, Cs = a.Cs, Cp = a.Cp, Q = a.Q, n = a.n_steps;
   const long long t0 = *stepc;
-  float* ZS = sm;                  // [2][P_LA layers][16 b][32 k] z of a round (double-buffered)
-  float* RS = ZS + 2 * P_LA * 512; // [16 b][512 k] relu(skip + Σb), zero-padded
-  float* HP = RS + P_MAXB * 512;   // [32 kg][16 b][16 c] per-thread partials (skip, then post1)
-  float* HS = HP + 32 * 256;       // [16 b][16 c] h
-  float* P1T = HS + 256;           // [16 c][516] POST1[:, 16m + c] (rows padded: conflict-free b128 reads)
+  // row paddings (33, 516, 17 floats) put the 16 stream rows a 16-lane MFMA operand read touches
+  // on distinct banks (unpadded, the 32- / 512- / 16-float rows were 8- to 16-way conflicts)
+  float* ZS = sm;                  // [2][P_LA layers][16 b][33] z of a round (double-buffered)
+  float* RS = ZS + 2 * P_LA * 528; // [16 b][516] relu(skip + Σb), zero-padded
+  float* HP = RS + P_MAXB * 516;   // [8 waves][64 lanes][4] MFMA partials (skip, then post1)
+  float* HS = HP + 32 * 256;       // [16 b][17] h
+  float* P1T = HS + 272;           // [16 c][516] POST1[:, 16m + c] (rows padded: conflict-free b128 reads)
   float* P2S = P1T + 16 * 516;     // [16 r][Q] POST2[16m + r, :]
-  for (int e = tid; e < P_MAXB * 512; e += 512) RS[e] = 0.f;
+  for (int e = tid; e < P_MAXB * 516; e += 512) RS[e] = 0.f;
   for (int e = tid; e < 16 * 512; e += 512) {   // the head's weight slices stay in LDS for the run
     const int cc = e >> 9, k = e & 511;
     P1T[cc * 516 + k] = (k < Cs && m * 16 + cc < Cp) ? a.post1[(long)k * Cp + m * 16 + cc] : 0.f;
@@ -904,7 +909,7 @@ LBWN_DEV void persist_head(const PersistK& a, int m, float* sm, int b0, int B, l
   }
   // lane roles: c = column within this block's 16, kg = tid >> 4 = 4·wave + (lane >> 4)
   const int c = tid & 15, kg = tid >> 4, kql = lane >> 4;
-  const int scol = m * 16 + c, hcol = m * 16 + c;
+  const int scol = m * 16 + c, hcol = m * 16 + c, scol16 = m * 16;
   // A: wave wv takes layer l0 + wv of each round, lane quarter kql the channels 8kql..8kql+7
   const float* wsrc = a.skipw + (long)(8 * kql) * Cs + min(scol, Cs - 1);
   // C: post1 rows 16kg .. 16kg+15 of column hcol (P1T); post2 rows 16m .. 16m+15 of column tid (P2S)
@@ -915,68 +920,54 @@ LBWN_DEV void persist_head(const PersistK& a, int m, float* sm, int b0, int B, l
   long long* tr = (trace && m == P_NH - 1 && tid == 0) ? trace : nullptr;
   for (int s = 0; s < n; ++s) {
     const unsigned tag = (unsigned)(t0 + s + 1);
-    // A. skip columns, P_LA layers per round: the round's z granules and this lane's 8 weights
-    //    arrive in one round trip; per-thread partials pa[b] (layer wv of each round, channels
-    //    8kql..) are reduced once after the last round
-    float pa[P_MAXB];
-#pragma unroll
-    for (int bb = 0; bb < P_MAXB; ++bb) pa[bb] = 0.f;
+    // A. skip columns, P_LA layers per round: the round's z granules (thread: stream tid >> 5,
+    //    channel tid & 31, every layer of the round) and this lane's 8 weights arrive in one round
+    //    trip; wave wv accumulates layer l0 + wv of each round into a 16x16 (stream x column)
+    //    tile on v_mfma_f32_16x16x4_f32 (8 MFMAs over the layer's 32 channels: A[i = stream][k] =
+    //    z, B[k][j = column] = SKIP), summed over the waves once after the last round.  (Round 3's
+    //    per-thread FMAs re-read every z row for all 16 columns: ~260 KB of LDS per round.)
+    floatx4 pacc = {0.f, 0.f, 0.f, 0.f};
     // rounds are aligned to the END of the stack: the last round is layer L-1 alone, so the
     // round before it finishes while the chains run their last layer and the tail after the
     // chains is one poll + one layer (the first round takes the remainder)
     const int first = (L - 1) % P_LA == 0 ? P_LA : (L - 1) % P_LA;
+    const int i16 = lane & 15, kk = lane >> 4;
     for (int l0 = 0, r = 0; l0 < L; l0 += (l0 == 0 ? first : P_LA), ++r) {
       const int nl = l0 == L - 1 ? 1 : (l0 == 0 ? min(first, L) : P_LA), li = l0 + wv;
-      float wv8[8], zv[P_LA];
+      float w8[8], zv[P_LA];
+      const float* wl = a.skipw + (long)min(li, L - 1) * Cd * Cs + min(scol16 + i16, Cs - 1);
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        wv8[j] = wsrc[((long)min(li, L - 1) * Cd + min(j, Cd - 1 - 8 * kql)) * Cs];
+      for (int s4 = 0; s4 < 8; ++s4) w8[s4] = wl[(long)min(4 * s4 + kk, Cd - 1) * Cs];
       sweep<P_LA>(a.zg, (unsigned)((b0 + (zn0 ? zb0 : 0)) * L + l0) * 32 + (zn0 ? zk : 0), 32u, nl, tag, zv, a.status);
       if (tr && s == n - 1) tr[8 + L + 40 + r] = wall_clock64();
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (li >= L || 8 * kql + j >= Cd || scol >= Cs) wv8[j] = 0.f;
-      float* Z = ZS + (r & 1) * (P_LA * 512);   // the other buffer's readers finished last round
+      for (int s4 = 0; s4 < 8; ++s4)
+        if (li >= L || 4 * s4 + kk >= Cd || scol16 + i16 >= Cs) w8[s4] = 0.f;
+      float* Z = ZS + (r & 1) * (P_LA * 528);   // the other buffer's readers finished last round
 #pragma unroll
-      for (int i = 0; i < P_LA; ++i) Z[i * 512 + tid] = (zn0 && i < nl) ? zv[i] : 0.f;
+      for (int i = 0; i < P_LA; ++i) Z[i * 528 + zb0 * 33 + zk] = (zn0 && i < nl) ? zv[i] : 0.f;
       __syncthreads();
       if (tr && s == n - 1) tr[8 + L + 80 + r] = wall_clock64();
-      const float* zr = Z + wv * 512 + 8 * kql;
+      const float* zr = Z + wv * 528 + i16 * 33 + kk;
+      float za[8];
 #pragma unroll
-      for (int bb = 0; bb < P_MAXB; ++bb) {
-        if ((bb & 3) == 0) __builtin_amdgcn_sched_barrier(0);   // 4 streams' reads in flight at a time
-        if (bb < B) {
-          const floatx4 z0 = *(const floatx4*)(zr + bb * 32), z1 = *(const floatx4*)(zr + bb * 32 + 4);
-          float x = pa[bb];
-          x = fmaf(z0[0], wv8[0], x);
-          x = fmaf(z0[1], wv8[1], x);
-          x = fmaf(z0[2], wv8[2], x);
-          x = fmaf(z0[3], wv8[3], x);
-          x = fmaf(z1[0], wv8[4], x);
-          x = fmaf(z1[1], wv8[5], x);
-          x = fmaf(z1[2], wv8[6], x);
-          x = fmaf(z1[3], wv8[7], x);
-          pa[bb] = x;
-        }
-      }
+      for (int s4 = 0; s4 < 8; ++s4) za[s4] = zr[4 * s4];
+#pragma unroll
+      for (int s4 = 0; s4 < 8; ++s4) pacc = __builtin_amdgcn_mfma_f32_16x16x4f32(za[s4], w8[s4], pacc, 0, 0, 0);
       if (tr && s == n - 1) tr[8 + L + r] = wall_clock64();
     }
-    // reduce the 32 per-thread partials of each (stream, column) through LDS (no shuffles:
-    // their dependent LDS round trips cost ~2 us per phase)
-#pragma unroll
-    for (int bb = 0; bb < P_MAXB; ++bb)
-      if (bb < B) HP[(kg * 16 + bb) * 16 + c] = pa[bb];
+    // the eight waves' tiles summed through LDS in a fixed order; thread (lane l, e): stream
+    // 4(l >> 4) + e, column l & 15
+    *(floatx4*)(HP + (wv * 64 + lane) * 4) = pacc;
     __syncthreads();
-    {
-      const int sb = tid >> 4;   // (column c, stream sb)
-      if (sb < B && scol < Cs) {
-        float v[32], x = 0.f;
+    if (tid < 256) {
+      const int l = tid & 63, e = tid >> 6, sb = 4 * (l >> 4) + e, cc = l & 15;
+      float v[8], x = 0.f;
 #pragma unroll
-        for (int g = 0; g < 32; ++g) v[g] = HP[(g * 16 + sb) * 16 + c];
+      for (int g = 0; g < 8; ++g) v[g] = HP[(g * 64 + l) * 4 + e];
 #pragma unroll
-        for (int g = 0; g < 32; ++g) x += v[g];
-        put_granule(a.sg + (long)(b0 + sb) * Cs + scol, tag, x);   // B. publish this block's skip columns
-      }
+      for (int g = 0; g < 8; ++g) x += v[g];
+      if (sb < B && scol16 + cc < Cs) put_granule(a.sg + (long)(b0 + sb) * Cs + scol16 + cc, tag, x);   // B. publish
     }
     if (tr && s == n - 1) tr[2] = wall_clock64();
     // B. gather the whole skip vector: thread k = tid polls column k of every stream
@@ -986,74 +977,59 @@ LBWN_DEV void persist_head(const PersistK& a, int m, float* sm, int b0, int B, l
       const float bs = a.bsum ? a.bsum[tid] : 0.f;
 #pragma unroll
       for (int bb = 0; bb < P_MAXB; ++bb)
-        if (bb < B) RS[bb * 512 + tid] = fmaxf(v[bb] + bs, 0.f);
+        if (bb < B) RS[bb * 516 + tid] = fmaxf(v[bb] + bs, 0.f);
     }
     __syncthreads();
     if (tr && s == n - 1) tr[3] = wall_clock64();
-    // C. post1 partial over rows 16kg..16kg+15 of column hcol, 4 streams at a time (independent
-    //    chains), the 32 row groups summed through LDS
+    // C. h = relu(relu(skip + Σb)·POST1[:, cols] + b1) for this block's 16 columns and all 16
+    //    stream slots on v_mfma_f32_16x16x4_f32 (exact f32 products): wave wv takes K rows
+    //    64wv .. 64wv+63 (16 MFMAs; A[i = stream][k] = RS, B[k][j = column] = P1T), the eight
+    //    16x16 partials are summed through LDS in a fixed order.  (Round 3's per-thread FMA form
+    //    re-read each RS row for all 16 columns: ~390 KB of LDS reads, ~1.1 us.)
     {
-      floatx4 w4[4];
+      const int i16 = lane & 15, kk = lane >> 4, k0 = 64 * wv;
+      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+      float av[16], bv[16];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) w4[q] = *(const floatx4*)(P1T + c * 516 + 16 * kg + 4 * q);
-      for (int g0 = 0; g0 < B; g0 += 4) {
-        floatx4 x[4][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) x[j][q] = *(const floatx4*)(RS + min(g0 + j, P_MAXB - 1) * 512 + 16 * kg + 4 * q);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float pp = 0.f;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            pp = fmaf(x[j][q][0], w4[q][0], pp);
-            pp = fmaf(x[j][q][1], w4[q][1], pp);
-            pp = fmaf(x[j][q][2], w4[q][2], pp);
-            pp = fmaf(x[j][q][3], w4[q][3], pp);
-          }
-          if (g0 + j < B) HP[(kg * 16 + g0 + j) * 16 + c] = pp;
-        }
+      for (int s4 = 0; s4 < 16; ++s4) {
+        av[s4] = RS[i16 * 516 + k0 + 4 * s4 + kk];
+        bv[s4] = P1T[i16 * 516 + k0 + 4 * s4 + kk];
       }
+#pragma unroll
+      for (int s4 = 0; s4 < 16; ++s4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s4], bv[s4], acc, 0, 0, 0);
+      *(floatx4*)(HP + (wv * 64 + lane) * 4) = acc;   // lane-linear: D[4kk + e][i16]
     }
     if (tr && s == n - 1) tr[8 + L + 120] = wall_clock64();
     __syncthreads();
     if (tr && s == n - 1) tr[8 + L + 121] = wall_clock64();
-    {
-      const int sb = tid >> 4;
-      if (sb < B) {
-        float v[32], h = 0.f;
+    if (tid < 256) {   // (stream 4·(tid>>6... : element (lane l = tid & 63, e = tid >> 6) of every wave's D
+      const int l = tid & 63, e = tid >> 6, sb = 4 * (l >> 4) + e, cc = l & 15;
+      float v[8], hsum = 0.f;
 #pragma unroll
-        for (int g = 0; g < 32; ++g) v[g] = HP[(g * 16 + sb) * 16 + c];
+      for (int g = 0; g < 8; ++g) v[g] = HP[(g * 64 + l) * 4 + e];
 #pragma unroll
-        for (int g = 0; g < 32; ++g) h += v[g];
-        HS[sb * 16 + c] = hcol < Cp ? fmaxf(h + b1, 0.f) : 0.f;
-      }
+      for (int g = 0; g < 8; ++g) hsum += v[g];
+      const float b1c = (m * 16 + cc < Cp && a.post1_b) ? a.post1_b[m * 16 + cc] : 0.f;
+      HS[sb * 17 + cc] = (m * 16 + cc < Cp) ? fmaxf(hsum + b1c, 0.f) : 0.f;
     }
     __syncthreads();
     if (tr && s == n - 1) tr[8 + L + 122] = wall_clock64();
-    // partial logits over this block's 16 h rows: column q = tid, 4 streams at a time
-    if (tid < Q) {
-      float p2[16];
+    // partial logits over this block's 16 h rows: 16 code columns per MFMA block, blocks wv and
+    // wv + 8 of the Q/16: A[i = stream][k = r] = HS, B[k][j = code] = P2S; lane (code, 4 streams)
+    {
+      const int i16 = lane & 15, kk = lane >> 4;
+      float av[4];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) p2[r] = P2S[r * Q + tid];
-      for (int g0 = 0; g0 < B; g0 += 4) {
-        floatx4 hv[4][4];
+      for (int s4 = 0; s4 < 4; ++s4) av[s4] = HS[i16 * 17 + 4 * s4 + kk];
+      for (int qb = wv; qb < (Q + 15) / 16; qb += 8) {
+        const int q = min(16 * qb + i16, Q - 1);
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s4], P2S[(4 * s4 + kk) * Q + q], acc, 0, 0, 0);
+        if (16 * qb + i16 < Q) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) hv[j][q] = *(const floatx4*)(HS + min(g0 + j, P_MAXB - 1) * 16 + 4 * q);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float lp = 0.f;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            lp = fmaf(hv[j][q][0], p2[4 * q], lp);
-            lp = fmaf(hv[j][q][1], p2[4 * q + 1], lp);
-            lp = fmaf(hv[j][q][2], p2[4 * q + 2], lp);
-            lp = fmaf(hv[j][q][3], p2[4 * q + 3], lp);
-          }
-          if (g0 + j < B) put_granule(a.lg + ((long)m * a.B + b0 + g0 + j) * Q + tid, tag, lp);
+          for (int e = 0; e < 4; ++e)
+            if (4 * kk + e < B) put_granule(a.lg + ((long)m * a.B + b0 + 4 * kk + e) * Q + q, tag, acc[e]);
         }
       }
     }
