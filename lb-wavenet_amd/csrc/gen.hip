@@ -789,6 +789,7 @@ LBWN_DEV void persist_chain(const PersistK& a, float* sm, int b, long long* step
       DL[q] = lsum;
       if (tr && s == n) tr[5] = wall_clock64();
       lds_barrier();   // D
+      if (tr && s == n) tr[7] = wall_clock64();
       float lv[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {

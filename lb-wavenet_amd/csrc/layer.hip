@@ -1861,7 +1861,8 @@ __global__ __launch_bounds__(256) void pack_layers_fb_x3_kernel(const float* sig
 struct PrologueK {
   lbwn_prologue_args a;
   SplitJobs jb;
-  int nz, ns, ne, nd, np;   // blocks: zero, split (per job), embed, D-sep (per layer), pack
+  int nz, ns, ne, nd, np;   // blocks: zero, split (per job), embed, D-sep (all layers), pack
+  bool ev4, dv4;            // float4 items: embed, D-sep
 };
 __global__ __launch_bounds__(256) void step_prologue_kernel(PrologueK k) {
   const lbwn_prologue_args& a = k.a;
@@ -1872,16 +1873,15 @@ __global__ __launch_bounds__(256) void step_prologue_kernel(PrologueK k) {
   }
   b -= (long)k.ns * a.njobs;
   if (b < k.ne) {
-    embed_body(b, k.ne, a.q, a.pre, a.pre_b, a.X, a.B, a.T, a.H, a.Cr, a.Q);
+    embed_flat_body(b, k.ne, a.q, a.pre, a.pre_b, a.X, a.B, a.T, a.H, a.Cr, a.Q, k.ev4);
     return;
   }
   b -= k.ne;
-  if (b < (long)k.nd * a.L) {
-    dsep_body<true>((int)(b / k.nd), b % k.nd, k.nd, a.X, a.xls, const_cast<float*>(a.save), a.nbl, a.B, a.T, a.H,
-                    a.Cr);
+  if (b < k.nd) {
+    dsep_flat_body<true>(b, k.nd, a.X, a.xls, const_cast<float*>(a.save), a.L, a.nbl, a.B, a.T, a.H, a.Cr, k.dv4);
     return;
   }
-  b -= (long)k.nd * a.L;
+  b -= k.nd;
   if (b < k.nz) {
     zero_body(b, k.nz, (unsigned*)a.zero, (long)(a.zero_bytes / 4));
     return;
@@ -3048,11 +3048,15 @@ int lbwn_step_prologue_launch(const lbwn_prologue_args& a, hipStream_t st) {
   }
   auto blocks = [](long n, long per, long cap) { return (int)std::max(1L, std::min(cap, (n + per - 1) / per)); };
   k.ns = blocks(most, 1024, 256);                                        // 4 pairs per thread
-  k.ne = blocks((long)a.B * a.T * a.Cr, 1024, 2048);
-  k.nd = blocks((long)a.B * (1L << (a.nbl - 1)) * a.Cr, 1024, 64);       // per layer, sized by the deepest d
+  LBWN_REQUIRE((long)a.B * a.T * a.Cr < (1L << 31) && (long)dsep_rows(a.L, a.nbl, 1) * a.B * a.Cr < (1L << 31),
+               "step_prologue: x / SAVE exceed 32-bit indexing");
+  k.ev4 = embed_v4(a.pre, a.pre_b, a.X, a.Cr);
+  k.dv4 = dsep_v4(a.X, a.xls, a.save, a.Cr);
+  k.ne = blocks((long)a.B * a.T * (k.ev4 ? a.Cr / 4 : a.Cr), 256, 2048);   // one item per thread
+  k.nd = blocks((long)dsep_rows(a.L, a.nbl, a.B) * (k.dv4 ? a.Cr / 4 : a.Cr), 256, 2048);
   k.nz = a.zero_bytes ? blocks((long)(a.zero_bytes / 4), 1024, 256) : 0;
   k.np = 2 * a.L + (a.lcout ? a.L : 0) + ((a.skip_b && a.bsum) ? (a.Cs + 255) / 256 : 0);
-  const long grid = (long)k.ns * a.njobs + k.ne + (long)k.nd * a.L + k.nz + k.np;
+  const long grid = (long)k.ns * a.njobs + k.ne + k.nd + k.nz + k.np;
   step_prologue_kernel<<<(unsigned)grid, 256, 0, st>>>(k);
   LBWN_CHECK_LAUNCH();
   return 0;

@@ -18,13 +18,13 @@ namespace {
 
 // ---- D-separation state and embedding: bodies in prologue.h ---------------------------------
 template <bool TO_X>
-__global__ void dsep_kernel(float* xall, long xls, float* save, int nbl, int B, int T, int H, int Cr) {
-  dsep_body<TO_X>(blockIdx.y, blockIdx.x, gridDim.x, xall, xls, save, nbl, B, T, H, Cr);
+__global__ void dsep_kernel(float* xall, long xls, float* save, int L, int nbl, int B, int T, int H, int Cr, bool v4) {
+  dsep_flat_body<TO_X>(blockIdx.x, gridDim.x, xall, xls, save, L, nbl, B, T, H, Cr, v4);
 }
 
 __global__ void embed_kernel(const int* __restrict__ q, const float* __restrict__ pre, const float* pre_b,
-                             float* x0, int B, int T, int H, int Cr, int Q) {
-  embed_body(blockIdx.x, gridDim.x, q, pre, pre_b, x0, B, T, H, Cr, Q);
+                             float* x0, int B, int T, int H, int Cr, int Q, bool v4) {
+  embed_flat_body(blockIdx.x, gridDim.x, q, pre, pre_b, x0, B, T, H, Cr, Q, v4);
 }
 
 // out[m] = a[m] + (t+gd < T ? c0[m+gd] : 0)   (dx of a layer input from (g + dcur, dprev))
@@ -538,25 +538,35 @@ inline int grid_for(long n, int per = 256, int cap = 8192) {
 
 }  // namespace
 
-int lbwn_dsep_prepend_launch(float* xall, long xls, const float* save, int L, int nbl, int B, int T, int H,
-                             int Cr, hipStream_t st) {
-  dim3 grid(grid_for((long)B * (1 << (nbl - 1)) * Cr, 256, 256), L);
-  dsep_kernel<true><<<grid, 256, 0, st>>>(xall, xls, const_cast<float*>(save), nbl, B, T, H, Cr);
+// one flat launch over every layer's SAVE rows (dsep_flat_body), one item per thread
+static int dsep_launch(bool to_x, float* xall, long xls, float* save, int L, int nbl, int B, int T, int H, int Cr,
+                       hipStream_t st) {
+  LBWN_REQUIRE(L >= 1 && nbl >= 1 && nbl <= 16 && B >= 1 && Cr >= 1, "dsep: bad shape");
+  LBWN_REQUIRE((long)dsep_rows(L, nbl, 1) * B * Cr < (1L << 31), "dsep: SAVE exceeds 32-bit indexing");
+  const bool v4 = dsep_v4(xall, xls, save, Cr);
+  const long n = (long)dsep_rows(L, nbl, B) * (v4 ? Cr / 4 : Cr);
+  const int grid = (int)std::max(1L, std::min(2048L, (n + 255) / 256));
+  if (to_x) dsep_kernel<true><<<grid, 256, 0, st>>>(xall, xls, save, L, nbl, B, T, H, Cr, v4);
+  else dsep_kernel<false><<<grid, 256, 0, st>>>(xall, xls, save, L, nbl, B, T, H, Cr, v4);
   LBWN_CHECK_LAUNCH();
   return 0;
+}
+
+int lbwn_dsep_prepend_launch(float* xall, long xls, const float* save, int L, int nbl, int B, int T, int H,
+                             int Cr, hipStream_t st) {
+  return dsep_launch(true, xall, xls, const_cast<float*>(save), L, nbl, B, T, H, Cr, st);
 }
 
 int lbwn_dsep_save_launch(const float* xall, long xls, float* save, int L, int nbl, int B, int T, int H, int Cr,
                           hipStream_t st) {
-  dim3 grid(grid_for((long)B * (1 << (nbl - 1)) * Cr, 256, 256), L);
-  dsep_kernel<false><<<grid, 256, 0, st>>>(const_cast<float*>(xall), xls, save, nbl, B, T, H, Cr);
-  LBWN_CHECK_LAUNCH();
-  return 0;
+  return dsep_launch(false, const_cast<float*>(xall), xls, save, L, nbl, B, T, H, Cr, st);
 }
 
 int lbwn_embed_launch(const int* q, const float* pre, const float* pre_b, float* x0, int B, int T, int H, int Cr,
                       int Q, hipStream_t st) {
-  embed_kernel<<<grid_for((long)B * T * Cr), 256, 0, st>>>(q, pre, pre_b, x0, B, T, H, Cr, Q);
+  LBWN_REQUIRE((long)B * T * Cr < (1L << 31), "embed: B*T*n_res exceeds 32-bit indexing");
+  const bool v4 = embed_v4(pre, pre_b, x0, Cr);
+  embed_kernel<<<grid_for((long)B * T * (v4 ? Cr / 4 : Cr)), 256, 0, st>>>(q, pre, pre_b, x0, B, T, H, Cr, Q, v4);
   LBWN_CHECK_LAUNCH();
   return 0;
 }

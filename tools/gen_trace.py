@@ -46,7 +46,8 @@ if g.persistent:
     print('  last head: phase A done %.2f, skip gathered %.2f, partial logits published %.2f'
           % (us(tr[2]), us(tr[3]), us(tr[4])))
     print('  last head C: post1 partials %.2f, barrier %.2f, h %.2f' % tuple(us(tr[8 + L + 120:8 + L + 123])))
-    print('  chain 0: logits gathered %.2f, draw done %.2f' % (us(tr[5]), us(tr[6])))
+    print('  chain 0: logits gathered %.2f (heads 0-15, compute waves), barrier D passed %.2f (heads 16-31, '
+          'loader waves), draw done %.2f' % (us(tr[5]), us(tr[7]), us(tr[6])))
     print('  step period ~ %.2f us (draw done - start of the step it drew)' % us(tr[6]))
     sub = tr[8 + L + 128:8 + L + 128 + 48].reshape(8, 6)
     if np.all(sub > 0):
