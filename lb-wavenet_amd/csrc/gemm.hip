@@ -816,6 +816,12 @@ static bool lbwn_gemm_wide_tiles() {
   return v != 0;
 }
 
+// lane l <- lane l ^ 1 (CTRL 0xB1) or l ^ 2 (0x4E) within each quad: DPP quad_perm
+template <int CTRL>
+LBWN_DEV float quad_xor(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+
 // AMN: the weight-gradient form (dSKIP, dPOST1, dPOST2: A and B both mn-contiguous, K = the
 // positions): each lane loads its A fragment values as scalars -- per k row one 64-B run of 16
 // consecutive rows i, the same bytes as the k-contiguous form's two 32-B runs -- and splits them in
@@ -989,12 +995,12 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
         for (int e = 0; e < 4; ++e)
           if (rbase + 16 * mi + 4 * fq + e < g.M) cs[nb] += acc[mi][nb][e];
         const bool odd = c & 1, hi = c & 2;
-        {
-          const float r0 = __shfl_xor(odd ? a0 : a1, 1), r1 = __shfl_xor(odd ? a2 : a3, 1);
+        {   // lane xor 1 / xor 2 within the quad: DPP quad_perm (VALU) instead of ds_bpermute
+          const float r0 = quad_xor<0xB1>(odd ? a0 : a1), r1 = quad_xor<0xB1>(odd ? a2 : a3);
           if (odd) { a0 = r0; a2 = r1; } else { a1 = r0; a3 = r1; }
         }
         {
-          const float q0 = __shfl_xor(hi ? a0 : a2, 2), q1 = __shfl_xor(hi ? a1 : a3, 2);
+          const float q0 = quad_xor<0x4E>(hi ? a0 : a2), q1 = quad_xor<0x4E>(hi ? a1 : a3);
           if (hi) { a0 = q0; a1 = q1; } else { a2 = q0; a3 = q1; }
         }
         const int row = rbase + 16 * mi + 4 * fq + c;
