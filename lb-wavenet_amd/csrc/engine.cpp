@@ -308,12 +308,6 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   LBWN_REQUIRE(p, "plan: out of host memory");
   p->fwd_nw = fwd_nw;
   p->bwd_nw = bwd_nw;
-  {  // XCD-grouped chain tile walk (layer.hip chain_first), off by default: same-box A/B
-     // (profiles/r04_ab_handoff_xcd.txt) forward chain 234-235 us with tile = block index, 243 grouped;
-     // backward unchanged.  LBWN_CHAIN_XCD=1 turns it on.
-    const char* xv = getenv("LBWN_CHAIN_XCD");
-    p->chain_xcd = xv && !strcmp(xv, "1");
-  }
   p->a = *a;
   p->B = B;
   p->T = T;
@@ -331,6 +325,14 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   p->Ge = a->n_gc_embed;
   p->ncat1 = a->n_gc_embed > 0 ? a->n_gc_category + 1 : 0;
   p->Lo = a->n_lc_out;
+  {  // XCD-grouped chain tile walk (layer.hip chain_first): on for LC archs only.  Same box, two
+     // rounds (profiles/r04_ab_chain_xcd_lc.txt): arch5 B=8 2.748-2.761 vs 2.777-2.779 ms (the
+     // LC products read the k-blocked DV export the chain wrote), arch3 B=8 2.101-2.104 vs
+     // 2.082-2.091 (its forward chain 248 vs 239-240 us; profiles/r04_ab_handoff_xcd.txt).
+     // LBWN_CHAIN_XCD=0 / 1 overrides.  Placement only: bitwise the same results.
+    const char* xv = getenv("LBWN_CHAIN_XCD");
+    p->chain_xcd = xv ? (strcmp(xv, "1") == 0) : (p->Lo > 0);
+  }
   p->Li = a->n_lc_in;
   p->nup = a->n_lc_out > 0 ? a->n_lc_upsample : 0;
   p->hop = hop;

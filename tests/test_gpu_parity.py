@@ -498,6 +498,39 @@ def test_adam_kernel_ragged(lib, n, nw):
     np.testing.assert_allclose(p.cpu().numpy(), pd, rtol=1e-6, atol=1e-7)
 
 
+def test_chain_xcd_walk_lc_bitwise(monkeypatch):
+    """LC archs walk the chains' tiles XCD-grouped by default (engine.cpp plan creation); the
+    block-index walk (LBWN_CHAIN_XCD=0) gives the same outputs and gradients bit for bit (arch5 with
+    its LC and GC terms, 64 tiles per chain), except the GC gradients, whose mixed-voice rows are
+    float atomics (to f32 rounding)."""
+    arch = load_arch(os.path.join(ROOT, 'par', 'arch5.json'))
+    B, T = 2, 4096
+    q, ids = rand_batch(arch, B, T)
+    hop = int(np.prod(arch['lc_upsample']))
+    mel = np.random.default_rng(5).standard_normal((B, T // hop, arch['n_lc_in'])).astype(np.float32)
+    gid = np.where(ids != 0, 3, 0).astype(np.int32) if arch['n_gc_category'] else ids
+    out = []
+    for v in (None, '0'):
+        if v is None:
+            monkeypatch.delenv('LBWN_CHAIN_XCD', raising=False)
+        else:
+            monkeypatch.setenv('LBWN_CHAIN_XCD', v)
+        net = make_net(arch, B)
+        net.forward(q, mel, gid, backward=True)
+        torch.cuda.synchronize()
+        assert int(net.plan_tensor(T, 'status').view(torch.int32)[0]) == 0
+        out.append((net.stats[:3].cpu().numpy(), net.save_flat.cpu().numpy(),
+                    {n: g.cpu().numpy() for n, g in net.grads.items()}))
+    (s0, v0, g0), (s1, v1, g1) = out
+    assert np.array_equal(s0, s1) and np.array_equal(v0, v1)
+    for n in g0:
+        if n.startswith('GC_'):   # mixed-voice waves add their GC rows by float atomics (gc_scatter16):
+            # the add order follows which CU ran which tile, so these compare to f32 rounding
+            np.testing.assert_allclose(g0[n], g1[n], rtol=1e-5, atol=1e-6, err_msg=n)
+        else:
+            assert np.array_equal(g0[n], g1[n]), n
+
+
 @pytest.mark.parametrize('env', [{'LBWN_CHAIN_XCD': '1'}, {'LBWN_DZ_XCD': '0'}])
 def test_placement_switches_bitwise(monkeypatch, env):
     """The placement-only switches change which block (and so which XCD) computes a tile, never
