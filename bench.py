@@ -232,6 +232,7 @@ def bench_gen(net, arch, B=10, seconds=3.0, sr=16000, chunk=1000, sweep=(16, 64,
     out['roofline'] = {'bound': 'latency', 'unit': 'us/step', 'achieved': us, 'peak': fl['step_us'],
                        'frac': fl['step_us'] / us, 'floor': fl,
                        'measured_per_layer_us': t_layer,
+                       'mfma_busy': mfma_from_profiles('gen_persist_kernel', 'gen'),
                        'note': 'peak = the dependent chain of one step at MI355X_MICROARCH.md latencies '
                                '(gen_latency_floor); frac = floor / measured step'}
     out['roofline_hbm'] = {'bound': 'hbm', 'bytes_per_step': bps, 'achieved': bps * n / dt / 1e9, 'peak': HBM_PEAK / 1e9,
@@ -437,7 +438,8 @@ class TrainBench:
                'peak': peak / 1e12 if bound == 'mfma' else peak / 1e9,
                'unit': 'TFLOP/s' if bound == 'mfma' else 'GB/s', 'frac': ach / peak,
                'avg_launch_us': avg * 1e6, 'work_per_launch': work,
-               'traffic': traffic_from_profiles(name, traffic if isinstance(traffic, str) else None) if traffic else None}
+               'traffic': traffic_from_profiles(name, traffic if isinstance(traffic, str) else None) if traffic else None,
+               'mfma_busy': mfma_from_profiles(name, traffic if isinstance(traffic, str) else None) if traffic else None}
         if bound == 'mfma':
             out['arith'] = ('bf16-split (6 products) for dx and dSIG/dGATE, f32 MFMA for dz and dRES'
                             if x3 and name == 'layer_bwd' else ('bf16-split' if x3 else 'f32 MFMA'))
@@ -737,6 +739,23 @@ def traffic_from_profiles(kernel, tag=None):
             d = json.load(f)
         v = d.get(kernel)
         return None if v is None else v.get('hbm_bytes_per_launch')
+    except Exception:
+        return None
+
+
+def mfma_from_profiles(kernel, tag=None):
+    """Matrix-pipe utilisation of a launch from the committed PMC summary (profiles/pmc_mfma.json
+    for C2, profiles/pmc_mfma_<tag>.json for c4 / gen; tools/pmc_mfma.py over one counter-only
+    rocprofv3 pass): {'mfma_busy': SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs),
+    'kernel', 'source'}, or None when not collected."""
+    p = os.path.join(ROOT, 'profiles', 'pmc_mfma%s.json' % ('_' + tag if tag else ''))
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        v = d.get(kernel)
+        if v is None or v.get('mfma_busy') is None:
+            return None
+        return {'frac': v['mfma_busy'], 'kernel': v['kernel'], 'source': 'profiles/' + os.path.basename(p)}
     except Exception:
         return None
 

@@ -66,9 +66,11 @@ size_t lbwn_plan_workspace_bytes(const lbwn_plan* plan);
  * "x" [L][B][H+T][n_res] (layer inputs with D-sep halo, H = 2^(n_block_layers-1)),
  * "z" [M][L·n_dil] (gate outputs), "s" [M][n_skip] (skip sum), "r2" [M][n_post],
  * "logits" [M][n_quant] (dlogits after forward), "dh" [M][n_post], "ds" [M][n_skip],
- * "dz" [M][L·n_dil] (backward), "status" (int32: 0, or the code of a chain hand-off that
- * timed out), and for conditioned archs "cond"/"dvall" [M][L·2·n_dil] (LC term, its dv),
- * "gctab"/"gcd" [n_cat+1][L·2·n_dil] (GC table, its gradient).  */
+ * "dz" [M][L·n_dil] (backward; with the bf16-split chains in the chain's 32-row block order
+ * instead of rows), "status" (int32: 0, or the code of a chain hand-off that timed out), and
+ * for conditioned archs "cond" [M][L·2·n_dil] (LC term), "dvall" (its dv: rows [M][L·2·n_dil],
+ * or after a bf16-split chain backward k-blocked [2L][ceil(M/32)·32][32], the size reported
+ * accordingly), "gctab"/"gcd" [n_cat+1][L·2·n_dil] (GC table, its gradient).  */
 int lbwn_plan_tensor(const lbwn_plan* plan, const char* name, size_t* offset, size_t* bytes);
 /* One-shot timing probe: the next lbwn_train_forward/backward on this plan records
  * hipEvent_t ev_start right before and ev_stop right after the named launch(es):

@@ -16,6 +16,8 @@
 
 struct lbwn_plan {
   int chain_xcd = 0;       // chain_first's XCD-grouped walk
+  int dz_xcd2d = 1;        // dZ's tiles blocked 2-D over the XCDs (gemm.hip xcd2d_tile)
+  int fwd_mode = -1;       // GEMM arithmetic (lbwn_gemm_mode) the last forward ran; the backward follows it
   bool dv_blk = false;     // the last backward exported DV k-blocked ([2L][m32(M)][32])
   int head_colparts = 0;   // post2-bias column partial rows the last forward's head wrote (0: none)
   lbwn_arch a;
@@ -47,7 +49,7 @@ struct lbwn_plan {
   int split_dlc, split_dlcx, split_up[8];
   size_t oSPLIT_AUX = 0;         // split-K workspace of the aux2 stream (LC / GC grads beside dSKIP)
   bool up_fused = false;         // LC upsample as one fused launch per direction (cond.hip)
-  bool up_fused_bwd = false;     // ... for the backward (LBWN_LC_UP=bwdgemm: per-stage GEMMs there)
+  bool up_fused_bwd = false;     // ... for the backward (<= 256 mel frames; else per-stage GEMMs)
   size_t oUPPART = 0;            // its per-frame filter-gradient partials
   size_t total;
   long x_layer_stride;  // floats
@@ -332,6 +334,10 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
      // LBWN_CHAIN_XCD=0 / 1 overrides.  Placement only: bitwise the same results.
     const char* xv = getenv("LBWN_CHAIN_XCD");
     p->chain_xcd = xv ? (strcmp(xv, "1") == 0) : (p->Lo > 0);
+    // dZ's 2-D XCD tile blocking (profiles/r04_ab_dz_xcd.txt: time-neutral, 490 -> 460 MB per
+    // launch); LBWN_DZ_XCD=0 keeps the 1-D remap.  Placement only: bitwise the same results.
+    const char* dv = getenv("LBWN_DZ_XCD");
+    p->dz_xcd2d = (dv && dv[0] == '0') ? 0 : 1;
   }
   p->Li = a->n_lc_in;
   p->nup = a->n_lc_out > 0 ? a->n_lc_upsample : 0;
@@ -423,16 +429,11 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     }
     p->oCOND = p->Lo ? carve(cur, f * (size_t)M * ncond) : 0;
     p->up_fused = p->Lo > 0 && lbwn_lc_up_fused_ok(p->nup, p->up, p->Li, p->Lo);
-    {  // The fused backward runs one block per mel frame at one block per CU: past one round of
-       // frames the per-stage GEMMs win (same box, profiles/r04_ab_lc_upsample.txt: arch5 B=8, 128
-       // frames, fused 2.817-2.829 ms vs GEMMs 2.955-2.957; B=32, 512 frames, fused 10.67-10.68 vs
-       // 10.56-10.57).  LBWN_LC_UP=fused / gemm / bwdgemm overrides (same-box A/B switch).
-      const char* uv = getenv("LBWN_LC_UP");
-      const long frames = M / hop;
-      if (uv && !strcmp(uv, "gemm")) p->up_fused = false;
-      p->up_fused_bwd = p->up_fused && (uv && !strcmp(uv, "fused") ? true
-                                        : uv && !strcmp(uv, "bwdgemm") ? false : frames <= 256);
-    }
+    // The fused backward runs one block per mel frame at one block per CU: past one round of
+    // frames the per-stage GEMMs win (same box, profiles/r04_ab_lc_upsample.txt: arch5 B=8, 128
+    // frames, fused 2.817-2.829 ms vs GEMMs 2.955-2.957; B=32, 512 frames, fused 10.67-10.68 vs
+    // 10.56-10.57)
+    p->up_fused_bwd = p->up_fused && M / hop <= 256;
     if (p->up_fused) p->oUPPART = carve(cur, f * (size_t)lbwn_lc_up_part_floats(p->nup, p->up, p->Li, p->Lo, (int)(M / hop)));
     p->oDVALL = p->Lo ? carve(cur, f * (size_t)m32(M) * ncond) : 0;   // rows or [2L][m32(M)][32]
     p->oLCCAT = p->Lo ? carve(cur, f * (size_t)p->Lo * ncond) : 0;
@@ -478,7 +479,10 @@ int lbwn_plan_tensor(const lbwn_plan* p, const char* name, size_t* off, size_t* 
   else if (!strcmp(name, "ds")) { *off = p->oDS; *bytes = f * M * p->Cs; }
   else if (!strcmp(name, "dz")) { *off = p->oDZ; *bytes = f * M * p->L * p->Cd; }
   else if (!strcmp(name, "cond") && p->Lo) { *off = p->oCOND; *bytes = f * M * 2 * p->L * p->Cd; }
-  else if (!strcmp(name, "dvall") && p->Lo) { *off = p->oDVALL; *bytes = f * M * 2 * p->L * p->Cd; }
+  else if (!strcmp(name, "dvall") && p->Lo) {   // rows [M][L·2Cd], or k-blocked [2L][m32(M)][32] (dv_blk)
+    *off = p->oDVALL;
+    *bytes = f * (p->dv_blk ? (size_t)m32(p->M) : M) * 2 * p->L * p->Cd;
+  }
   else if (!strcmp(name, "gctab") && p->Ge) { *off = p->oGCTAB; *bytes = f * p->ncat1 * 2 * p->L * p->Cd; }
   else if (!strcmp(name, "gcd") && p->Ge) { *off = p->oGCD; *bytes = f * p->ncat1 * 2 * p->L * p->Cd; }
   else LBWN_REQUIRE(false, "plan_tensor: unknown tensor '%s'", name);
@@ -735,6 +739,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   lbwn_params Ppad;
   if ((e = head_pad_params(p, P, ws, Ppad, true, st))) return e;
   P = &Ppad;
+  p->fwd_mode = lbwn_gemm_mode();
   // the sticky status word (chain spin timeouts OR their codes in) lives for one step:
   // zeroed here, read by the host after the step (lbwn_plan_tensor "status")
   // (in the fused prologue below when the bf16-split chains run)
@@ -860,6 +865,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     g.A = Z; g.lda = ldz; g.B = P->skip; g.ldb = p->Cs; g.C = S; g.ldc = p->Cs;
     g.M = (int)M; g.N = p->Cs; g.K = (int)ldz; g.bias = P->skip_b ? bsum : nullptr;
     g.b3 = w3(p, ws, W3_SKIP_F);
+    g.row_exact = 1;
     Probe(p, st, "skip_fwd");
     if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
     Probe::end(p, st, "skip_fwd");
@@ -869,6 +875,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   g.A = S; g.lda = p->Cs; g.B = P->post1; g.ldb = p->Cp; g.C = R2; g.ldc = p->Cp;
   g.M = (int)M; g.N = p->Cp; g.K = p->Cs; g.bias = P->post1_b; g.relu_a = 1; g.relu_out = 1;
   g.b3 = w3(p, ws, W3_POST1_F);
+  g.row_exact = 1;
   Probe(p, st, "post1_fwd");
   if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
   Probe::end(p, st, "post1_fwd");
@@ -877,6 +884,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   g.A = R2; g.lda = p->Cp; g.B = P->post2; g.ldb = p->Q; g.C = LOG; g.ldc = p->Q;
   g.M = (int)M; g.N = p->Q; g.K = p->Cp; g.bias = P->post2_b;
   g.b3 = w3(p, ws, W3_POST2_F);
+  g.row_exact = 1;
   Probe(p, st, "post2_fwd");
   if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
   Probe::end(p, st, "post2_fwd");
@@ -905,6 +913,12 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   hipStream_t st = (hipStream_t)stream;
   int e;
   if ((e = ensure_device(p))) return e;
+  // the backward consumes the forward's layout choices (SG rows, the head's column partials, dZ in
+  // chain order), which follow the GEMM arithmetic: a mode switch in between would mix two paths
+  LBWN_REQUIRE(p->fwd_mode >= 0, "train_backward: no forward on this plan");
+  LBWN_REQUIRE(p->fwd_mode == lbwn_gemm_mode(),
+               "train_backward: the GEMM mode changed since the forward (%d -> %d); run the forward again",
+               p->fwd_mode, lbwn_gemm_mode());
   // padded head widths: the forward's padded images, gradients into padded buffers
   const lbwn_params* Gref = G;
   lbwn_params Ppad, Gpad;
@@ -953,6 +967,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   g.A = DS; g.lda = Cs; g.B = P->skip; g.ldb = Cs; g.C = DZ; g.ldc = ldz; g.M = (int)M; g.N = (int)ldz; g.K = Cs;
   g.b3 = w3(p, ws, W3_SKIP_B);
   if (dz_chain) g.c_chain_ls = m32(M) * 32;
+  g.xcd2d = p->dz_xcd2d;
   Probe(p, st, "dz");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
   Probe::end(p, st, "dz");

@@ -805,17 +805,6 @@ __global__ __launch_bounds__(512, 1) void gemm_x3r_kernel(lbwn_gemm_args g) {
 // l = (r = l & 15, q = l >> 4) supplies A[16mi + r][8q + j] (one 32-B run of a row per mi: a row's
 // four lanes cover its 128-B line) and B[8q + j][16ni + r]; the k-step runs as two halves of 4
 // column blocks.
-// LBWN_GEMM_WIDE=0 keeps dZ on 128-column tiles (same-box A/B switch)
-// LBWN_GEMM_AMN=0 keeps the mn-contiguous weight-gradient products on the LDS-staged kernel
-static bool lbwn_gemm_amn() {
-  const char* e = getenv("LBWN_GEMM_AMN");
-  return !(e && e[0] == '0');
-}
-static bool lbwn_gemm_wide_tiles() {
-  static const int v = [] { const char* e = getenv("LBWN_GEMM_WIDE"); return (e && e[0] == '0') ? 0 : 1; }();
-  return v != 0;
-}
-
 // lane l <- lane l ^ 1 (CTRL 0xB1) or l ^ 2 (0x4E) within each quad: DPP quad_perm
 template <int CTRL>
 LBWN_DEV float quad_xor(float v) {
@@ -1140,15 +1129,14 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
   // A/B since the epilogue and split changes); 128-row tiles at 2 blocks per CU for the rest
   // (the mn-contiguous weight gradients: 1.3-1.5x slower on 256-row tiles)
   // (256-row tiles for dSKIP too, with the 2-deep staging: 341 -> 476 us)
-  const int wm = (a.colpart || (a_kcontig && a.N <= 2048 && a.M >= 8192)) ? 4 : 2;
+  const int wm = (a.colpart || (a_kcontig && a.N <= 2048 && (a.M >= 8192 || a.row_exact))) ? 4 : 2;
   lbwn_gemm_args g;
   dim3 grid;
   int e = gemm_setup(a, a_kcontig, b_kcontig, split_k, slab_ws, X3_BK, 64 * wm, 128, g, grid);
   if (e) return e;
   const bool kfull = a.K % X3_BK == 0, pre = a.b3 != nullptr;
   if (X3Q && !a_kcontig && !b_kcontig && kfull && !pre && !a.mask && !a.bias && !a.colpart && !a.c_chain_ls &&
-      !a.b_gstride && a.M >= 256 && a.N % 4 == 0 && ((a.M + 255) / 256) * ((a.N + 127) / 128) >= 8 &&
-      lbwn_gemm_amn()) {
+      !a.b_gstride && a.M >= 256 && a.N % 4 == 0 && ((a.M + 255) / 256) * ((a.N + 127) / 128) >= 8) {
     // the weight-gradient products with >= 8 output tiles (dSKIP, dPOST1): 256 x 128 tiles with A
     // in registers (gemm_x3q_kernel AMN).  tools/gemm_bench.py, same box: dSKIP split 9 315 vs
     // 355 us, dPOST1 split 32 97 vs 107; dPOST2 (4 tiles) 87 vs 77 stays on the 2-per-CU kernel
@@ -1162,13 +1150,12 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
       grid.x = (unsigned)(((a.M + 255) / 256) * ((a.N + 95) / 96));
       if (X3Q) gemm_x3q_kernel<6><<<grid, 512, 0, st>>>(g);
       else gemm_x3r_kernel<3><<<grid, 512, 0, st>>>(g);
-    } else if (X3Q && a.N % 160 == 0 && a.N > 512 && lbwn_gemm_wide_tiles()) {
+    } else if (X3Q && a.N % 160 == 0 && a.N > 512) {
       // N = 1600 (dZ): 160-column tiles, so the grid is whole rounds of 256 blocks (M/256 x 10 at
       // C2 = 1280 = 5 rounds) instead of 128-column ones (13 column tiles, the last half empty:
-      // 1664 = 6.5 rounds)
+      // 1664 = 6.5 rounds; same box 2.296-2.304 vs 2.342-2.353 ms per step).
+      // a.xcd2d (the caller's choice): the 2-D XCD blocking of the tiles (xcd2d_tile)
       grid.x = (unsigned)(((a.M + 255) / 256) * (a.N / 160));
-      const char* xe = getenv("LBWN_DZ_XCD");
-      g.xcd2d = (xe && xe[0] == '0') ? 0 : 1;   // LBWN_DZ_XCD=0: the 1-D remap (same-box A/B switch)
       gemm_x3q_kernel<10><<<grid, 512, 0, st>>>(g);
     } else if (X3Q) {
       gemm_x3q_kernel<8><<<grid, 512, 0, st>>>(g);

@@ -25,12 +25,17 @@ struct lbwn_gemm_args {
   long c_chain_ls;
   int k_per_split;     // set by the launcher
   long split_stride;   // set by the launcher
-  int xcd2d;           // set by the launcher: gemm_x3q_kernel<10>'s 2-D XCD blocking (xcd2d_tile)
+  int xcd2d;           // gemm_x3q_kernel<10> (N % 160 == 0): the 2-D XCD blocking of its tiles (xcd2d_tile)
   // k-blocked operands (the backward chain's DV export, [K/32][Mp][32]): 0 = plain layout.
   // a_kstride: A k-contiguous with lda = 32, element (m, k) at A[m·32 + (k/32)·a_kstride + k%32]
   // (gemm_x3q_kernel only); b_gstride: B mn-contiguous with ldb = 32, element (k, n) at
   // B[k·32 + (n/32)·b_gstride + n%32] (the LDS-staged bf16-split kernel only)
   long a_kstride, b_gstride;
+  // 1: every output row is computed by the same kernel and k order whatever M is (the tall
+  // 256-row form below M = 8192 too), so a row's value depends only on its own A row: the
+  // training forward's head GEMMs, so a slice processed in stages equals one long slice bit for
+  // bit (README.md:6-21)
+  int row_exact;
 };
 int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                      hipStream_t st);
@@ -235,7 +240,6 @@ int lbwn_pre_grad_launch(const int* q, const float* g, const float* dprev, int g
                          float* dpre, float* dpre_b, float* ws, hipStream_t st);
 int lbwn_shift_add_launch(float* out, const float* a, const float* c0, int gd, int B, int T, int C,
                           hipStream_t st);
-int lbwn_head_nblocks(long M);
 
 int lbwn_mulaw_encode_launch(const float* x, int* q, long n, int n_quanta, int tf32, hipStream_t st);
 int lbwn_mulaw_decode_launch(const int* q, float* x, long n, int n_quanta, hipStream_t st);

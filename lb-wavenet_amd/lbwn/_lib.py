@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (must precede the .so: shared HIP runtime)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get('LBWN_LIB') or os.path.join(HERE, 'liblbwn.so')   # LBWN_LIB: timing-variant builds
+LIB_PATH = os.path.join(HERE, 'liblbwn.so')   # the in-tree build only (tools/with_lib.py loads variants)
 ABI_VERSION = 2
 
 c_int, c_int64, c_float, c_void_p, c_size_t = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t

@@ -91,3 +91,38 @@ def test_plan_chain_tile_env(monkeypatch):
         monkeypatch.setenv('LBWN_CHAIN_TILE', v)
         assert lib.lbwn_plan_create(ctypes.byref(a), 8, 4096, ctypes.byref(h)) == 22, v
         assert b'LBWN_CHAIN_TILE' in lib.lbwn_last_error()
+
+
+def test_gemm_mode_env_selects_f32_mfma():
+    """LBWN_GEMM=f32 (read once, at the first GEMM or mode query) selects the f32-MFMA GEMMs
+    (mode 0); unset or anything else keeps the bf16-split form (mode 1).  Fresh processes: the
+    mode is process state."""
+    import subprocess
+    import sys
+    code = ('import sys; sys.path.insert(0, %r); from lbwn import _lib; print(_lib.load().lbwn_gemm_get_mode())'
+            % os.path.join(ROOT, 'lb-wavenet_amd'))
+    for val, want in (('f32', '0'), ('', '1'), ('bf16', '1')):
+        env = dict(os.environ, LBWN_GEMM=val)
+        out = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stderr[-2000:]
+        assert out.stdout.strip().splitlines()[-1] == want, (val, out.stdout)
+
+
+def test_product_loads_only_the_in_tree_library(monkeypatch):
+    """The product path has no library override: lbwn._lib loads lb-wavenet_amd/lbwn/liblbwn.so
+    (variant builds are for tools/with_lib.py A/B runs only)."""
+    from lbwn import _lib
+    assert _lib.LIB_PATH == os.path.join(ROOT, 'lb-wavenet_amd', 'lbwn', 'liblbwn.so')
+    src = open(os.path.join(ROOT, 'lb-wavenet_amd', 'lbwn', '_lib.py')).read()
+    assert 'environ' not in src
+
+
+def test_env_switches_are_all_tested():
+    """Every LBWN_* switch the product library reads is set by some test."""
+    import glob
+    src = ''.join(open(f).read() for f in glob.glob(os.path.join(ROOT, 'lb-wavenet_amd', 'csrc', '*.[hc]*')))
+    read = set(re.findall(r'getenv\("(LBWN_[A-Z0-9_]+)"\)', src))
+    assert read, 'no switches found'
+    tests = ''.join(open(f).read() for f in glob.glob(os.path.join(ROOT, 'tests', 'test_*.py')))
+    untested = sorted(v for v in read if not re.search(r"(['\"]%s['\"]|\b%s=)" % (v, v), tests))
+    assert not untested, 'read by the library but set by no test: %s' % untested

@@ -109,6 +109,13 @@ def test_arch5_deep_stack(chain_tile):
     _check_config(arch, 2, 1024)
 
 
+def test_arch5_one_mel_hop(chain_tile):
+    """arch5 at T = 256 = one mel hop per stream (B=2): every d >= 256 layer (d = 256, 512 in
+    each of the 5 blocks) reads only SAVE through its dilated tap and keeps old SAVE rows
+    (tmodel.py:122-127, :163-166), with the LC term of a single upsampled frame."""
+    _check_config(_arch('arch5'), 2, 256, seed=2)
+
+
 def test_arch5_tile_rounds(chain_tile):
     """arch5 with more 128-position tiles (4 x 66 = 264) than CUs, so the persistent chains
     run in rounds, at T = 8448 = 33 mel hops."""

@@ -181,3 +181,23 @@ def test_gen_arch3_full_ring_depth(B, n, form):
     np.testing.assert_allclose(g.logits().cpu().numpy(), lg[:, -1], rtol=0, atol=1e-4 * np.abs(lg[:, -1]).max())
     if len(bad) == 0:
         np.testing.assert_allclose(wav.cpu().numpy(), w_ref[:, :wav.shape[1]], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize('B', [3, 20])
+def test_gen_trace_build_same_draws(monkeypatch, B):
+    """LBWN_GEN_TRACE=1 (read at gen-plan creation: the persistent kernel's per-phase clock
+    stamps, tools/gen_trace.py and the bench's measured_per_layer_us) is the same computation:
+    the traced instantiation draws exactly the untraced one's samples (B=20: two stream groups)."""
+    arch = small()
+    out = []
+    for tr in (None, '1'):
+        if tr:
+            monkeypatch.setenv('LBWN_GEN_TRACE', tr)
+        else:
+            monkeypatch.delenv('LBWN_GEN_TRACE', raising=False)
+        g, _ = make_gen(arch, B, chunk=64)
+        g.run(200)
+        torch.cuda.synchronize()
+        assert int(g.tensor('status', torch.int32).item()) == 0
+        out.append(g.samples().cpu().numpy()[:, :200].copy())
+    np.testing.assert_array_equal(out[0], out[1])

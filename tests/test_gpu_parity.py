@@ -291,7 +291,24 @@ def test_plan_forward_backward(lib, gemm_mode, which, B, T, mode, chain_tile):
     mode 0: every product on the f32 MFMA.  Same bars for both.  ('arch3', 8, 4096) is the
     benchmarked C2 shape itself: 256 tiles of the persistent chains, every gradient vs float64."""
     gemm_mode(mode)
-    arch = arch3() if which == 'arch3' else small_arch()
+    check_plan(arch3() if which == 'arch3' else small_arch(), B, T)
+
+
+@pytest.mark.parametrize('T', [40, 96, 200, 384])
+def test_plan_slice_shorter_than_dilation(lib, T, chain_tile):
+    """Slices shorter than the dilation (T < d; train.py:43-44 --slice-size is free): the
+    reference's SAVE update keeps "the last d rows of [SAVE ++ x]" (tmodel.py:122-127,
+    :163-166), so for d > T the new SAVE holds old SAVE rows [T, d) and every dilated tap x[t-d]
+    is a SAVE row.  arch3 at B=2: T=96 puts d = 128/256/512 past the slice, T=200 d = 256/512,
+    T=384 d = 512, T=40 also d = 64 (and a tile shorter than one 64-lane wave).  Exercises
+    the SAVE-from-SAVE rows of the flat D-sep copy (prologue.h dsep_flat_body), the chains'
+    halo taps with no producer tile, and the backward's truncation of dprev into the halo
+    (the gradient into SAVE is dropped).  Forward + backward against the float64 oracle:
+    layer-0 SAVE bit-exact, deeper SAVE 1e-5, z on identical inputs 1e-5, gradients 2e-4."""
+    check_plan(arch3(), 2, T)
+
+
+def check_plan(arch, B, T):
     net = make_net(arch, B)
     q, ids = rand_batch(arch, B, T)
     P, S, lg, cache, new_save, st, dlog = _run_oracle(arch, net, q, ids)
@@ -445,6 +462,34 @@ def test_staged_equals_unstaged_bitwise():
     assert torch.equal(b.save_flat, save_full)
 
 
+def test_staged_equals_unstaged_arch3_bitwise(chain_tile):
+    """README.md:6-21 at arch3 through the persistent chains, with stages shorter than the
+    deepest dilations (100 and 300 < 512; the 100-row stage is also shorter than d = 128 and
+    256): the state carried between stages is SAVE alone, rows [T, d) of it old SAVE rows.
+    One 4096-position slice against stages 100 + 300 + 3696: every layer's z, the SAVE state
+    after each stage boundary and the post-net output, bit for bit."""
+    arch = arch3()
+    B, T = 2, 4096
+    L, Cd = R.n_layers(arch), arch['n_dil']
+    q, ids = rand_batch(arch, B, T)
+    a = make_net(arch, B)
+    a.forward(q, None, ids, backward=False)
+    full_z = a.plan_tensor(T, 'z').view(B, T, L * Cd).clone()
+    full_r2 = a.plan_tensor(T, 'r2').view(B, T, -1).clone()
+    save_full = a.save_flat.clone()
+    b = make_net(arch, B)
+    zs, r2s = [], []
+    for lo, hi in ((0, 100), (100, 400), (400, 4096)):
+        b.forward(q[:, lo:hi], None, ids[:, lo:hi], backward=False)
+        assert int(b.plan_tensor(hi - lo, 'status').view(torch.int32)[0]) == 0
+        zs.append(b.plan_tensor(hi - lo, 'z').view(B, hi - lo, L * Cd).clone())
+        r2s.append(b.plan_tensor(hi - lo, 'r2').view(B, hi - lo, -1).clone())
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat(zs, 1), full_z)
+    assert torch.equal(b.save_flat, save_full)
+    assert torch.equal(torch.cat(r2s, 1), full_r2)
+
+
 def test_adam_step_matches_oracle():
     arch = small_arch(nb=1, nbl=3)
     B, T = 2, 128
@@ -557,3 +602,32 @@ def test_placement_switches_bitwise(monkeypatch, env):
     assert np.array_equal(s0, s1) and np.array_equal(v0, v1)
     for n in g0:
         assert np.array_equal(g0[n], g1[n]), n
+
+
+def test_chain_trace_build_bitwise(monkeypatch):
+    """LBWN_CHAIN_TRACE=<block> (read at plan creation: the chains' traced instantiations, whose
+    clock stamps feed tools/chain_trace.py and the bench's C4 dilation sweep) computes exactly what
+    the untraced chains do: stats, SAVE and every gradient bit for bit, and the stamps are written."""
+    arch = arch3()
+    B, T = 2, 4096
+    q, ids = rand_batch(arch, B, T)
+    out = []
+    for tr in (None, '1'):
+        if tr:
+            monkeypatch.setenv('LBWN_CHAIN_TRACE', tr)
+        else:
+            monkeypatch.delenv('LBWN_CHAIN_TRACE', raising=False)
+        net = make_net(arch, B)
+        net.forward(q, None, ids, backward=True)
+        torch.cuda.synchronize()
+        assert int(net.plan_tensor(T, 'status').view(torch.int32)[0]) == 0
+        out.append((net.stats[:3].cpu().numpy(), net.save_flat.cpu().numpy(),
+                    {n: g.cpu().numpy() for n, g in net.grads.items()},
+                    net.plan_tensor(T, 'ctrace').view(torch.int64).cpu().numpy().copy()))
+    (s0, v0, g0, _), (s1, v1, g1, tr1) = out
+    assert np.array_equal(s0, s1) and np.array_equal(v0, v1)
+    for n in g0:
+        assert np.array_equal(g0[n], g1[n]), n
+    L = R.n_layers(arch)
+    st = tr1.reshape(2, L, 16)[:, :, 0]
+    assert np.all(st != 0), 'chain stamps missing'

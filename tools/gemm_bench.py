@@ -1,5 +1,5 @@
 """Time lbwn_gemm_f32 on the training step's GEMM shapes (arch3, M = 32768) next to
-torch.matmul fp32 (the vendor BLAS) on the same operands.  Usage: python tools/gemm_bench.py [LBWN_LIB]"""
+torch.matmul fp32 (the vendor BLAS) on the same operands.  Usage: python tools/gemm_bench.py (a variant build: python tools/with_lib.py VARIANT.so tools/gemm_bench.py)"""
 import os
 import sys
 

@@ -1,6 +1,6 @@
 #!/usr/bin/env python
 """Per-kernel timing of the training plan via the plan's HIP-event probes (arch3 B=8 T=4096
-by default).  LBWN_LIB selects an alternative liblbwn.so (tools/ablate.sh variants)."""
+by default).  Variant builds: python tools/with_lib.py VARIANT.so tools/kbench.py ..."""
 import argparse
 import json
 import os
@@ -23,7 +23,7 @@ def main():
     ap.add_argument('--slice', type=int, default=4096)
     ap.add_argument('--iters', type=int, default=4)
     ap.add_argument('--probes', default='layer_fwd@25,layer_bwd@25,layer_fwd@9,layer_bwd@9,layer_bwd@0')
-    ap.add_argument('--tag', default=os.environ.get('LBWN_LIB', 'default'))
+    ap.add_argument('--tag', default='default')
     args = ap.parse_args()
     arch = load_arch(args.arch)
     net = WaveNetTrain(**arch, batch_sz=args.batch, l2_factor=1e-3, print_interval=0)

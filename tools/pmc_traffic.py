@@ -2,9 +2,10 @@
 dispatch).  gfx950: FETCH_SIZE counts ½ of the bytes of wide coalesced reads, so
 hbm_bytes = (2·FETCH_SIZE + WRITE_SIZE)·1024 (MI355X_MICROARCH.md § HBM).  Dispatches are
 split into training steps at the step-prologue (or weight-pack) kernel and named in launch order: the chain
-kernels by name, the GEMMs by their position in engine.cpp's fixed enqueue sequence (arch
-without LC or GC -- for LC/GC archs only the named kernels are meaningful: skip_fwd, post1_fwd, post2_fwd, then dh, ds, dz, dpost2, dpost1 before the
-backward chain and dskip after it, all on the main stream; dispatch ids follow enqueue order)."""
+kernels by name, the GEMMs by their position in engine.cpp's fixed enqueue sequence (skip_fwd,
+post1_fwd, post2_fwd, then dh, ds, dz, dpost2, dpost1 before the backward chain and dskip after
+it; an LC arch's dLCcat, dlc and upsample GEMMs in between, gemm_key; dispatch ids follow
+enqueue order)."""
 import csv
 import glob
 import json
@@ -43,12 +44,33 @@ def per_name(rows, skip_steps=8):
             for k, n in NAMED.items():
                 if k in name:
                     key = n
-            if any(g in name for g in ('gemm_f32_kernel', 'gemm_x3_kernel', 'gemm_x3r_kernel', 'gemm_x3q_kernel')):
-                key = GEMM_ORDER[gi] if gi < len(GEMM_ORDER) else 'gemm%d' % gi
+            if is_gemm(name):
+                key = gemm_key(gi, name)
                 gi += 1
             if key:
                 out.setdefault(key, []).append(v)
     return {k: sum(v) / len(v) for k, v in out.items()}
+
+
+def is_gemm(name):
+    return any(g in name for g in ('gemm_f32_kernel', 'gemm_x3_kernel', 'gemm_x3r_kernel', 'gemm_x3q_kernel'))
+
+
+def gemm_key(gi, name):
+    """The gi-th GEMM dispatch of a step.  The first eight are the fixed head sequence; after the
+    backward chain an LC arch enqueues dLCcat (side stream), dlc (96-column tiles) and the
+    upsample's per-stage GEMMs before dSKIP (engine.cpp lbwn_train_backward), so those are named
+    by their kernel form."""
+    if gi < 8:
+        return GEMM_ORDER[gi]
+    if 'gemm_x3q_kernel<8, true>' in name:
+        return 'dskip'
+    if gi == 8:
+        return 'lc_wgrad'
+    if 'gemm_x3q_kernel<6' in name or 'gemm_x3r_kernel<3' in name:
+        return 'lc_dlc'
+    return 'lc_up_bwd_gemm'
+
 
 
 def main(fdir, wdir, out_path):
