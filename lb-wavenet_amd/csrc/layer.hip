@@ -2375,13 +2375,19 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
     const int gc_prev = __shfl(gc_pid, max(lane - 1, 0) & 15);
     const unsigned gc_starts = (unsigned)(__ballot(g == 0 && (i16 == 0 || gc_pid != gc_prev)) & 0xffffull);
     // per-layer rows of this lane's position (Zl channels): dZ, z, σ, issued a layer ahead
+    // (buffer loads: a per-layer scalar base and one 32-bit lane offset per array, instead of three
+    // 64-bit lane addresses held across the layer loop; the launcher checks the byte ranges)
     floatx4 dzr[2], zr[2], sgr[2];
+    const int o_sg = (int)(sg_off(mc, q0, h) * 4), o_z = (int)((mc * a.lddz + 8 * q0 + 4 * h) * 4);
     auto load_regs = [&](int l) {
+      const __amdgpu_buffer_rsrc_t rdz = __builtin_amdgcn_make_buffer_rsrc((void*)(a.DZ + l * a.dzls), (short)0, 0x7fffffff, BUF_DW3);
+      const __amdgpu_buffer_rsrc_t rsg = __builtin_amdgcn_make_buffer_rsrc((void*)(a.SG + (long)l * a.sgls), (short)0, 0x7fffffff, BUF_DW3);
+      const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void*)(a.Zf + (long)l * 32), (short)0, 0x7fffffff, BUF_DW3);
 #pragma unroll
-      for (int bb = 0; bb < 2; ++bb) {
-        dzr[bb] = *(const floatx4*)(a.DZ + l * a.dzls + sg_off(mc, q0 + bb, h));
-        zr[bb] = *(const floatx4*)(a.Zf + mc * a.lddz + (long)l * 32 + 8 * (q0 + bb) + 4 * h);
-        sgr[bb] = *(const floatx4*)(a.SG + (long)l * a.sgls + sg_off(mc, q0 + bb, h));
+      for (int bb = 0; bb < 2; ++bb) {   // q0 + 1: the next 8-channel group (sg_off + 256 floats, z + 8)
+        dzr[bb] = __builtin_amdgcn_raw_buffer_load_b128(rdz, o_sg + 1024 * bb, 0, 0);
+        zr[bb] = __builtin_amdgcn_raw_buffer_load_b128(rz, o_z + 32 * bb, 0, 0);
+        sgr[bb] = __builtin_amdgcn_raw_buffer_load_b128(rsg, o_sg + 1024 * bb, 0, 0);
       }
     };
     auto dma_image = [&](int l) {
@@ -2397,27 +2403,21 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
     oa[0] = oa[1] = floatx4{0.f, 0.f, 0.f, 0.f};
     const bool trc = a.trace && (int)blockIdx.x == a.trace_blk && tid == 0 && it == first;
 #define XSTAMP(i) if (TR && trc) a.trace[16 * l + (i)] = clock64()
+    // the producer's out_c0 rows for the next layer's G build, loaded in this layer's tail (after
+    // the weight-gradient products, when the producer published long ago): its flag wait and
+    // load latency overlap the bias sums and slab stores instead of opening the next layer
+    floatx4 gl[NR];
     for (int l = a.L - 1; l >= 0; --l) {
       XSTAMP(0);
       const int d = 1 << (l % a.nbl);
       const int dn = (l + 1 < a.L) ? 1 << ((l + 1) % a.nbl) : 0;
-      // 1. G = dx_{l+1} rows: out_c0_{l+1}[t + dn] (own OC / the producer's published rows) + out_a
+      // 1. G = dx_{l+1} rows: out_c0_{l+1}[t + dn] (own OC / the producer's rows, gl) + out_a
       if (dn) {
-        const int ptt = tt + max(1, dn / TP);
-        if (ptt < tps) {
-          if (tid == 0 && !s_fail) {
-            if (!wait_flag_ge(a.flags + (long)b * tps + ptt, (unsigned)(a.L - l - 1), a.status, 2u)) s_fail = 1;
-          }
-          __syncthreads();
-        }
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)(l + 1) * a.ocls, (short)0, oc_bytes, BUF_DW3);
-        floatx4 gl[NR], go[NR];
+        XSTAMP(7);
+        floatx4 go[NR];
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
-          const int e = tid + NT * i, row = e >> 3, c4 = (e & 7) * 4, sr = row + dn;
-          const int ts = min(t0 + sr, a.T - 1);
-          gl[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
+          const int e = tid + NT * i, sr = (e >> 3) + dn, c4 = (e & 7) * 4;
           go[i] = *(const floatx4*)(OC + min(sr, TP - 1) * XS + c4);
         }
 #pragma unroll
@@ -2427,9 +2427,11 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
           if (ts >= a.T) v = floatx4{0.f, 0.f, 0.f, 0.f};
           *(floatx4*)(G + row * XS + c4) = v;
         }
+        XSTAMP(14);
         // lands this wave's part of the weight image (DMA'd during the last layer) and the
         // prefetched rows; the barrier then covers every wave's part
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        XSTAMP(15);
         __syncthreads();
       }
 #pragma unroll
@@ -2620,7 +2622,23 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         for (int p = 0; p < TP / 8; ++p) s4 += *(const floatx4*)(pl + (pc + 8 * p) * XS + c4);
         *(floatx4*)(part + pc * 96 + 32 * w + c4) = s4;
       }
-      __syncthreads();   // every read of Xp/Xc/ZT/DV/G of this layer is done; part complete
+      // the next layer's producer: its flag (published after its dx of this layer, half a layer
+      // ago) and then its out_c0 rows, loaded after the barrier below
+      const int pn = tt + max(1, d / TP);
+      if (l > 0 && pn < tps && tid == 0 && !s_fail) {
+        if (!wait_flag_ge(a.flags + (long)b * tps + pn, (unsigned)(a.L - l), a.status, 2u)) s_fail = 1;
+      }
+      __syncthreads();   // every read of Xp/Xc/ZT/DV/G of this layer is done; part complete; the flag seen
+      {
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)l * a.ocls, (short)0, oc_bytes, BUF_DW3);
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {   // (l = 0: a dead load of valid rows)
+          const int e = tid + NT * i, c4 = (e & 7) * 4;
+          const int ts = min(t0 + (e >> 3) + d, a.T - 1);
+          gl[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
+        }
+      }
       if (tid < 96) {
         float s1 = 0.f;
 #pragma unroll
@@ -3210,6 +3228,9 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
     if (int e = lbwn_zero_launch(c.flags, ((size_t)c.B * tps * 4 + 15) / 16 * 16, st)) return e;
   }
   LBWN_REQUIRE(x3 == (c.dzls > 0), "chain bwd: the bf16-split chain reads dZ in chain order (dzls), the f32 chain in rows");
+  if (c.bwd_nw)   // 32-bit byte offsets of the per-lane row loads (chain_bwd16_kernel load_regs)
+    LBWN_REQUIRE(c.dzls * 4 < 0x7fffffffL && c.sgls * 4 < 0x7fffffffL && (long)c.B * c.T * c.ldz * 4 < 0x7fffffffL,
+                 "chain bwd: dZ / SG layer or z rows past 2 GiB");
   if (c.bwd_nw == 8) {
     if (k.trace) chain_bwd16_kernel<8, true><<<c.grid, 512, 0, st>>>(k);
     else chain_bwd16_kernel<8, false><<<c.grid, 512, 0, st>>>(k);

@@ -59,6 +59,10 @@ if net.lib.lbwn_gemm_get_mode() == 1:      # chain_bwd_x3_kernel: XSTAMP(0..6)
                         ('dSIG: k-step 1', 10, 5), ('dRES', 5, 11), ('bias + dRES slab + bar', 11, 12),
                         ('dSIG partials + bar', 12, 13), ('dSIG sum + slab', 13, 6)]:
             print('    %-26s %6d' % (n, np.median(sub[:, j] - sub[:, i])))
+    if np.all(sub[:, 15] > 0):   # sub-stamps of the G build (7 flag barrier, 14 G written, 15 vmcnt drained)
+        for n, i, j in [('G: flag wait + barrier', 0, 7), ('G: loads + LDS writes', 7, 14), ('G: vmcnt(0)', 14, 15),
+                        ('G: barrier', 15, 1)]:
+            print('    %-26s %6d' % (n, np.median(sub[:, j] - sub[:, i])))
     sys.exit(0)
 names = ['stage x/dz + bar', 'gate recompute', 'G wait+build', 'dz,dv,DV', 'dx MFMA+OC', 'publish bar',
          'dSIG MFMA', 'bar+dRES', 'bias+slab+bar', 'image+bar']
