@@ -2625,7 +2625,7 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
       // the next layer's producer: its flag (published after its dx of this layer, half a layer
       // ago) and then its out_c0 rows, loaded after the barrier below
       const int pn = tt + max(1, d / TP);
-      if (l > 0 && pn < tps && tid == 0 && !s_fail) {
+      if (l > 0 && pn < tps && tid == 192 && !s_fail) {   // wave 3: no bias sums, so its poll overlaps waves 0-2's
         if (!wait_flag_ge(a.flags + (long)b * tps + pn, (unsigned)(a.L - l), a.status, 2u)) s_fail = 1;
       }
       __syncthreads();   // every read of Xp/Xc/ZT/DV/G of this layer is done; part complete; the flag seen
