@@ -27,11 +27,13 @@ constexpr int DS = 68;              // dv tile row [pos][64]
 constexpr int WIMG = 64 * WS + 32 * XS + 96;  // packed per-layer image (floats), multiple of 4
 constexpr int SLAB = 2048 + 2048 + 1024 + 96;
 constexpr int RED_PARTS = 32;       // deferred reduction: parts prefetched per thread (8 lanes × 32)
-// Timing-only ablation switches (tools/ablate.sh); 0 in every real build.
+// Timing-only ablation switches (variant builds: make EXTRA=-DLBWN_ABL=<bits> OBJDIR=... OUT=...);
+// 0 in every real build.
 #ifndef LBWN_ABL
 #define LBWN_ABL 0
 #endif
-// LDS bank-conflict attribution (tools/lds_conf.sh), counter-only builds: bit b sends one group of
+// LDS bank-conflict attribution (round 3, counter-only variant builds with EXTRA=-DLBWN_CONF=<bits>,
+// profiles/r03_lds_conf_*.txt): bit b sends one group of
 // chain_bwd_x3_kernel's LDS accesses to a conflict-free address (reads: a wave-uniform broadcast,
 // writes (2048): lane-contiguous 16-B slots); the outputs are wrong, SQ_LDS_BANK_CONFLICT's drop
 // per bit is that group's share.  0 in every real build.
@@ -2313,7 +2315,18 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 template <int NW>
 constexpr int cb16_lds() { return BIMG_F + 3 * 16 * NW * 32 + 4 * 16 * NW * XS + 8 * 96; }
 static_assert(cb16_lds<8>() * 4 + 16 <= 160 * 1024, "chain bwd16 LDS");
-static_assert(8 * 1280 <= 3 * 128 * 32, "bwd16: the partial scratch must fit in Xp | Xc | ZT");
+static_assert(4 * 1280 <= 3 * 128 * 32, "bwd16: the partial scratch (waves 4-7) must fit in Xp | Xc | ZT");
+
+// sum over the 16 lanes of each DPP row (row_ror 8, 4, 2, 1: every lane ends with the row's total,
+// in a fixed order)
+template <int CTRL>
+LBWN_DEV float dpp_row(float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false)); }
+LBWN_DEV float row16_sum(float v) {
+  v += dpp_row<0x128>(v);
+  v += dpp_row<0x124>(v);
+  v += dpp_row<0x122>(v);
+  return v + dpp_row<0x121>(v);
+}
 
 // GC rows of a wave whose 16 positions are not one voice: dv column sums per run of equal ids,
 // one atomic per run and column (as gc_scatter_x3, 16 positions)
@@ -2455,6 +2468,16 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         gv[xb] = v;
         *(floatx4*)gp = v;
       }
+      // the dx operands of its first k-step (S = 0), read ahead of the dz MFMAs: their LDS latency
+      // overlaps dz and dv instead of opening dx
+      bf16x8 fa0[2][3], fc0[2][3];
+#pragma unroll
+      for (int xb = 0; xb < 2; ++xb)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          fa0[xb][p] = *(const bf16x8*)(WD + (32 + 16 * xb + i16) * XW_ROW + 64 * p + 8 * g);
+          fc0[xb][p] = *(const bf16x8*)(WD + (16 * xb + i16) * XW_ROW + 64 * p + 8 * g);
+        }
       // 2. dz = dZ + RES·g  (f32 MFMA 16x16x4: k = g's channel 16xb + 4g + rr)
       floatx4 dz[2];
       {
@@ -2518,8 +2541,13 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         for (int xb = 0; xb < 2; ++xb)
 #pragma unroll
           for (int p = 0; p < 3; ++p) {
-            fa[xb][p] = *(const bf16x8*)(WD + (32 + 16 * xb + i16) * XW_ROW + 64 * p + 32 * S + 8 * g);
-            fc[xb][p] = *(const bf16x8*)(WD + (16 * xb + i16) * XW_ROW + 64 * p + 32 * S + 8 * g);
+            if (S == 0) {
+              fa[xb][p] = fa0[xb][p];
+              fc[xb][p] = fc0[xb][p];
+            } else {
+              fa[xb][p] = *(const bf16x8*)(WD + (32 + 16 * xb + i16) * XW_ROW + 64 * p + 32 * S + 8 * g);
+              fc[xb][p] = *(const bf16x8*)(WD + (16 * xb + i16) * XW_ROW + 64 * p + 32 * S + 8 * g);
+            }
           }
         bf16x8 bx[3];
         if (S == 0) split8(dvs[0], dvs[1], bx);
@@ -2555,6 +2583,24 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
       __syncthreads();  // DV, G, OC, Xp/Xc/ZT complete; the weight image is dead
       if (tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
       if (a.gc_dtab && !tile_uni) gc_scatter16(a.gc_dtab + (long)l * 64, a.gc_ld, DVs, DVg, w, lane, 32, gc_starts, gc_pid);
+      {  // 8. bias partials of this wave's 16 positions (column sums of dv_sig, dv_gate, g: the SIG /
+         //    GATE / RES bias gradients) from the registers, by DPP row sums, after the publish (off
+         //    the cross-tile path); lane 0 of row g holds its 8 channels of each -> part[w][96]
+        floatx4 bs4[6] = {dvs[0], dvs[1], dvg[0], dvg[1], gv[0], gv[1]};
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bs4[k][e] = row16_sum(bs4[k][e]);
+        if (i16 == 0) {
+          float* pw = part + w * 96;
+#pragma unroll
+          for (int bb = 0; bb < 2; ++bb) {
+            *(floatx4*)(pw + 8 * (q0 + bb) + 4 * h) = bs4[bb];
+            *(floatx4*)(pw + 32 + 8 * (q0 + bb) + 4 * h) = bs4[2 + bb];
+            *(floatx4*)(pw + 64 + 16 * bb + 4 * g) = bs4[4 + bb];
+          }
+        }
+      }
       XSTAMP(4);
       // 6. dSIG / dGATE tile t4 = w & 3 (2·kind + tap) over this wave's position half:
       //    A[i = in][k = pos] = X_tap[pos][in], B[k = pos][j = o] = DV_kind[pos][o]
@@ -2611,21 +2657,11 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         }
       }
       XSTAMP(11);
-      // 8. bias partials (column sums of DVs, DVg, G: waves 0-2; lane = (row class pc, 4-column
-      //    group c4), rows pc + 8p)
       float* slab = a.slab + ((long)l * ntiles + tile) * SLAB;
-      if (w < 3) {
-        const int c4 = (lane & 7) * 4, pc = lane >> 3;
-        const float* pl = w == 0 ? DVs : w == 1 ? DVg : G;
-        floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int p = 0; p < TP / 8; ++p) s4 += *(const floatx4*)(pl + (pc + 8 * p) * XS + c4);
-        *(floatx4*)(part + pc * 96 + 32 * w + c4) = s4;
-      }
       // the next layer's producer: its flag (published after its dx of this layer, half a layer
       // ago) and then its out_c0 rows, loaded after the barrier below
       const int pn = tt + max(1, d / TP);
-      if (l > 0 && pn < tps && tid == 192 && !s_fail) {   // wave 3: no bias sums, so its poll overlaps waves 0-2's
+      if (l > 0 && pn < tps && tid == 192 && !s_fail) {
         if (!wait_flag_ge(a.flags + (long)b * tps + pn, (unsigned)(a.L - l), a.status, 2u)) s_fail = 1;
       }
       __syncthreads();   // every read of Xp/Xc/ZT/DV/G of this layer is done; part complete; the flag seen
@@ -2639,10 +2675,10 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
           gl[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
         }
       }
-      if (tid < 96) {
+      if (tid < 96) {   // the waves' bias partials in wave order
         float s1 = 0.f;
 #pragma unroll
-        for (int pc = 0; pc < 8; ++pc) s1 += part[pc * 96 + tid];
+        for (int ww = 0; ww < NW; ++ww) s1 += part[ww * 96 + tid];
         slab[5120 + tid] = s1;
       }
       XSTAMP(12);
@@ -2655,23 +2691,26 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) slab[4096 + (16 * (t4 >> 1) + 4 * g + q) * 32 + 16 * (t4 & 1) + i16] = accR[q];
       } else {
-        float* SCR = Xp + w * 1280;
+        // (only waves 4-7 park theirs: waves 0-3 add their own half from registers, in the same order)
+        if (w >= 4) {
+          float* SCR = Xp + (w - 4) * 1280;
 #pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4)
-          *(floatx4*)(SCR + (q4 * 64 + lane) * 4) = floatx4{accT[4 * q4], accT[4 * q4 + 1], accT[4 * q4 + 2], accT[4 * q4 + 3]};
-        *(floatx4*)(SCR + 1024 + lane * 4) = accR;
+          for (int q4 = 0; q4 < 4; ++q4)
+            *(floatx4*)(SCR + (q4 * 64 + lane) * 4) = floatx4{accT[4 * q4], accT[4 * q4 + 1], accT[4 * q4 + 2], accT[4 * q4 + 3]};
+          *(floatx4*)(SCR + 1024 + lane * 4) = accR;
+        }
         __syncthreads();
         XSTAMP(13);
         if (w < 4) {
-          const float* S0 = Xp + w * 1280;
-          const float* S1 = Xp + (w + 4) * 1280;
+          const float* S1 = Xp + w * 1280;
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) {
-            const floatx4 v = *(const floatx4*)(S0 + (q4 * 64 + lane) * 4) + *(const floatx4*)(S1 + (q4 * 64 + lane) * 4);
+            const floatx4 v = floatx4{accT[4 * q4], accT[4 * q4 + 1], accT[4 * q4 + 2], accT[4 * q4 + 3]} +
+                              *(const floatx4*)(S1 + (q4 * 64 + lane) * 4);
 #pragma unroll
             for (int e = 0; e < 4; ++e) slab[w * 1024 + acc_row(4 * q4 + e, lane >> 5) * 32 + (lane & 31)] = v[e];
           }
-          const floatx4 v = *(const floatx4*)(S0 + 1024 + lane * 4) + *(const floatx4*)(S1 + 1024 + lane * 4);
+          const floatx4 v = accR + *(const floatx4*)(S1 + 1024 + lane * 4);
 #pragma unroll
           for (int q = 0; q < 4; ++q) slab[4096 + (16 * (w >> 1) + 4 * g + q) * 32 + 16 * (w & 1) + i16] = v[q];
         }

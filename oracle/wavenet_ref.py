@@ -507,7 +507,8 @@ def sample_from_logits(logits_row, u):
 
 
 def generate(arch, P, batch_sz, n_steps, seed=0, teacher_q=None, gc_ids=None,
-             pre_bias=True, return_logits=False, forced_q=None):
+             pre_bias=True, return_logits=False, forced_q=None, start=0, init_rings=None, init_q=None,
+             return_state=False):
     """imodel.py:214-272 restated with ring lookback buffers (semantically the
     reference's shift-by-chunk buffers, imodel.py:88-98, :190-207).
     Step i: input = zero vector (i=0) else onehot(prev draw) or onehot(teacher_q[i-1]).
@@ -516,7 +517,12 @@ def generate(arch, P, batch_sz, n_steps, seed=0, teacher_q=None, gc_ids=None,
     of this run's own draw, so the logits and draws are evaluated along another run's
     trajectory (e.g. the GPU's) and compared draw by draw without a single near-tie flip
     making the two streams diverge.
-    Returns (samples int[B,n], wav float[B,n], [logits[B,n,Q]])."""
+    Resuming (test use): ``start`` = the global index of this call's first step (ring slot
+    (start + i) mod d, the draw's uniform of step start + i), ``init_rings`` = every layer's
+    [B, d, Cr] ring at that point (layer order, slot = step mod d, as the GPU's "rings"), and
+    ``init_q`` [B] = the code the first step takes as input (the previous step's draw);
+    ``return_state`` appends the rings after the last step (the next call's init_rings).
+    Returns (samples int[B,n], wav float[B,n], [logits[B,n,Q]], [rings])."""
     dt = P['PRE'].dtype
     L = n_layers(arch)
     ub = arch['use_bias']
@@ -524,7 +530,8 @@ def generate(arch, P, batch_sz, n_steps, seed=0, teacher_q=None, gc_ids=None,
     rings = []
     for l in range(L):
         _, _, d = layer_index(arch, l)
-        rings.append(np.zeros((batch_sz, d, Cr), dt))   # ring of the last d inputs
+        rings.append(np.zeros((batch_sz, d, Cr), dt) if init_rings is None
+                     else np.array(init_rings[l], dt).reshape(batch_sz, d, Cr))   # ring of the last d inputs
     gce = None
     if arch['n_gc_embed'] > 0:
         gce = P['GC_EMBED'][np.asarray(gc_ids)]
@@ -532,7 +539,11 @@ def generate(arch, P, batch_sz, n_steps, seed=0, teacher_q=None, gc_ids=None,
     all_logits = np.zeros((batch_sz, n_steps, arch['n_quant']), dt) if return_logits else None
     prev_q = None
     for i in range(n_steps):
-        if i == 0:
+        t = start + i
+        if i == 0 and init_q is not None:
+            z = P['PRE'][np.asarray(init_q, np.int64)].copy()
+        elif i == 0:
+            assert start == 0, 'a resumed run needs init_q'
             z = np.zeros((batch_sz, Cr), dt)
         else:
             if teacher_q is not None and i - 1 < len(teacher_q):
@@ -548,7 +559,7 @@ def generate(arch, P, batch_sz, n_steps, seed=0, teacher_q=None, gc_ids=None,
         for l in range(L):
             b, bl, d = layer_index(arch, l)
             sfx = '_%d_%d' % (b, bl)
-            slot = i % d
+            slot = t % d
             prev = rings[l][:, slot].copy()                # input d steps ago (0 if none)
             rings[l][:, slot] = z
             v = {}
@@ -576,14 +587,13 @@ def generate(arch, P, batch_sz, n_steps, seed=0, teacher_q=None, gc_ids=None,
             lg = lg + P['POST2_BIAS']
         if return_logits:
             all_logits[:, i] = lg
-        q = np.array([sample_from_logits(lg[bb], philox_uniform(seed, bb, i))
+        q = np.array([sample_from_logits(lg[bb], philox_uniform(seed, bb, t))
                       for bb in range(batch_sz)], np.int64)
         samples[:, i] = q
         prev_q = q
     wav = mu_decode_tf32(samples, arch['n_quant'])
-    if return_logits:
-        return samples, wav, all_logits
-    return samples, wav
+    out = (samples, wav) + ((all_logits,) if return_logits else ()) + ((rings,) if return_state else ())
+    return out
 
 
 # ----------------------------------------------------------------------------------

@@ -201,3 +201,43 @@ def test_gen_trace_build_same_draws(monkeypatch, B):
         assert int(g.tensor('status', torch.int32).item()) == 0
         out.append(g.samples().cpu().numpy()[:, :200].copy())
     np.testing.assert_array_equal(out[0], out[1])
+
+
+def test_gen_arch3_c3_length_last_chunk(form):
+    """The C3 benchmark's whole run (3 s at 16 kHz = 48,000 steps, B=10, chunk 1000: 48 graph
+    replays) checked at its end: after 47,000 steps the device state -- every layer's lookback
+    ring and the last draw -- is read back, the last 1,000 steps run on, and the oracle, resumed
+    from that state (generate(start=47000, init_rings=, init_q=)), evaluates them along the GPU's
+    trajectory: each draw is checked against the float64 logits it was drawn from (near CDF ties
+    excepted, as test_gen_arch3_full_ring_depth).  A ring slot, the step counter or the RNG step
+    going wrong anywhere in the 47 chunk shifts would show as a draw the state does not explain."""
+    arch = load_arch(os.path.join(ROOT, 'par', 'arch3.json'))
+    B, n0, n1 = 10, 47000, 1000
+    g, P = make_gen(arch, B, chunk=1000)
+    g.build_graph(n0 + n1)
+    g.init_buffers()
+    g.step(n0)
+    torch.cuda.synchronize()
+    assert int(g.tensor('step', torch.int64).item()) == n0
+    rings_flat = g.tensor('rings').cpu().numpy().astype(np.float64)
+    L, Cr = R.n_layers(arch), arch['n_res']
+    rings, off = [], 0
+    for l in range(L):
+        d = R.layer_index(arch, l)[2]
+        rings.append(rings_flat[off:off + B * d * Cr].reshape(B, d, Cr))
+        off += B * d * Cr
+    q_last = g.samples().cpu().numpy()[:, n0 - 1].copy()
+    g.step(n1)
+    torch.cuda.synchronize()
+    g.check_status()
+    assert g.persistent == (form == 'persistent')
+    got = g.samples().cpu().numpy()[:, n0:n0 + n1]
+    assert len(np.unique(got)) > 16
+    ref, _, lg = R.generate(arch, P, B, n1, seed=7, return_logits=True, forced_q=got, start=n0, init_rings=rings,
+                            init_q=q_last)
+    bad = np.argwhere(got != ref)
+    ties = [(int(b), int(i)) for b, i in bad if _near_tie(lg[b, i], R.philox_uniform(7, int(b), n0 + int(i)))]
+    assert len(ties) == len(bad), 'draws differ away from a CDF tie at (stream, step) %s' % (
+        [(b, n0 + i) for b, i in bad[:8].tolist()],)
+    assert len(bad) <= 2, bad.tolist()
+    np.testing.assert_allclose(g.logits().cpu().numpy(), lg[:, -1], rtol=0, atol=1e-4 * np.abs(lg[:, -1]).max())

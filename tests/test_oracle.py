@@ -204,6 +204,20 @@ def test_generation_forced_trajectory():
             assert s2[b, i] == R.sample_from_logits(lg2[b, i], R.philox_uniform(3, b, i))
 
 
+def test_generation_resume_equals_one_run():
+    """generate(..., start=, init_rings=, init_q=) (the GPU C3-length test's checker): a run of 30
+    steps equals 17 steps then 13 resumed from the first call's rings and last draw -- the ring
+    slots and the draws' uniforms follow the global step index."""
+    arch = arch_tiny(gc=0)
+    P, _, _, _, _ = _setup(arch, B=2, T=8)
+    s0, w0, lg0 = R.generate(arch, P, 2, 30, seed=3, return_logits=True)
+    s1, _, lg1, rings = R.generate(arch, P, 2, 17, seed=3, return_logits=True, return_state=True)
+    s2, _, lg2 = R.generate(arch, P, 2, 13, seed=3, return_logits=True, start=17, init_rings=rings,
+                            init_q=s1[:, -1])
+    np.testing.assert_array_equal(np.concatenate([s1, s2], 1), s0)
+    np.testing.assert_allclose(np.concatenate([lg1, lg2], 1), lg0, rtol=0, atol=1e-12)
+
+
 def test_adam_tf1():
     opt = R.AdamTF1(0.1)
     P = {'w': np.array([1.0, -2.0])}
