@@ -18,6 +18,11 @@ struct lbwn_plan {
   int chain_xcd = 0;       // chain_first's XCD-grouped walk
   int dz_xcd2d = 1;        // dZ's tiles blocked 2-D over the XCDs (gemm.hip xcd2d_tile)
   int fwd_mode = -1;       // GEMM arithmetic (lbwn_gemm_mode) the last forward ran; the backward follows it
+  // (S > 0) and (R2 > 0) as GEMM mask bits (lbwn_gemm_args::mbits): written by the skip / post1
+  // epilogues, read by dS / dH1 instead of the f32 S / R2; set by the forward when both ends take
+  // the gemm_x3q_kernel<8> form
+  size_t oMBS = 0, oMBR = 0;
+  bool mb_s = false, mb_r = false;
   bool dv_blk = false;     // the last backward exported DV k-blocked ([2L][m32(M)][32])
   int head_colparts = 0;   // post2-bias column partial rows the last forward's head wrote (0: none)
   lbwn_arch a;
@@ -448,6 +453,8 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   }
   if (p->chain && p->Lo > 0 && lbwn_lc_in_chain_ok(p->Lo))
     p->oLCX = carve(cur, 2 * (size_t)L * std::max(lbwn_lc_image_x3_elems(), lbwn_lc_image16_elems()));
+  p->oMBS = carve(cur, 8 * (size_t)lbwn_gemm_mbits_words(M, p->Cs));
+  p->oMBR = carve(cur, 8 * (size_t)lbwn_gemm_mbits_words(M, p->Cp));
   p->oHEADP = carve(cur, sizeof(float) * 3 * 2048);
   p->oBSUM = carve(cur, sizeof(float) * (size_t)p->Cs);
   p->oWPK = carve(cur, sizeof(float) * (size_t)L * lbwn_layer_image_floats());
@@ -858,6 +865,11 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   }
   // SAVE_l <- last d rows of [SAVE ++ x_l]  (tmodel.py:165)
   if ((e = lbwn_dsep_save_launch(X, p->x_layer_stride, save, L, p->nbl, B, T, H, Cr, st))) return e;
+  // mask bits for the backward's dS / dH1 epilogues: both GEMM ends in the x3q<8> form
+  p->mb_s = lbwn_gemm_x3q8_form((int)M, p->Cs, (int)ldz, 1, w3(p, ws, W3_SKIP_F) != nullptr, 1, 0) &&
+            lbwn_gemm_x3q8_form((int)M, p->Cs, p->Cp, 1, w3(p, ws, W3_POST1_B) != nullptr, 1, 0);
+  p->mb_r = lbwn_gemm_x3q8_form((int)M, p->Cp, p->Cs, 1, w3(p, ws, W3_POST1_F) != nullptr, 1, 0) &&
+            lbwn_gemm_x3q8_form((int)M, p->Cp, p->Q, 1, w3(p, ws, W3_POST2_B) != nullptr, 1, 0);
   // S = Σ_l (z_l·SKIP_l + b) as ONE GEMM over Zcat (tmodel.py:171-184, :316-320)
   if (P->skip_b && !bsum_done && (e = lbwn_sum_bias_launch(P->skip_b, L, p->Cs, bsum, st))) return e;
   {
@@ -866,6 +878,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
     g.M = (int)M; g.N = p->Cs; g.K = (int)ldz; g.bias = P->skip_b ? bsum : nullptr;
     g.b3 = w3(p, ws, W3_SKIP_F);
     g.row_exact = 1;
+    if (p->mb_s) g.mbits_out = at<unsigned long long>(ws, p->oMBS);
     Probe(p, st, "skip_fwd");
     if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
     Probe::end(p, st, "skip_fwd");
@@ -876,6 +889,7 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   g.M = (int)M; g.N = p->Cp; g.K = p->Cs; g.bias = P->post1_b; g.relu_a = 1; g.relu_out = 1;
   g.b3 = w3(p, ws, W3_POST1_F);
   g.row_exact = 1;
+  if (p->mb_r) g.mbits_out = at<unsigned long long>(ws, p->oMBR);
   Probe(p, st, "post1_fwd");
   if ((e = lbwn_gemm_launch(g, 1, 0, 1, nullptr, st))) return e;
   Probe::end(p, st, "post1_fwd");
@@ -944,6 +958,8 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   g.A = LOG; g.lda = Q; g.B = P->post2; g.ldb = Q; g.C = DH; g.ldc = Cp; g.M = (int)M; g.N = Cp; g.K = Q;
   g.mask = R2; g.ldm = Cp;
   g.b3 = w3(p, ws, W3_POST2_B);
+  g.row_exact = 1;
+  if (p->mb_r) g.mbits = at<unsigned long long>(ws, p->oMBR);   // (R2 > 0) from post1's epilogue
   // bias-gradient column partials straight from the epilogues (bf16-split form)
   float* CPART = at<float>(ws, p->oCPART);
   const bool fcols = lbwn_gemm_mode() == 1;
@@ -956,6 +972,8 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   g.A = DH; g.lda = Cp; g.B = P->post1; g.ldb = Cp; g.C = DS; g.ldc = Cs; g.M = (int)M; g.N = Cs; g.K = Cp;
   g.mask = S; g.ldm = Cs;
   g.b3 = w3(p, ws, W3_POST1_B);
+  g.row_exact = 1;
+  if (p->mb_s) g.mbits = at<unsigned long long>(ws, p->oMBS);   // (S > 0) from the skip GEMM's epilogue
   if (fcols && G->skip_b) g.colpart = CPART + (long)lbwn_colpart_parts(M) * Cp;
   Probe(p, st, "ds");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;

@@ -831,6 +831,13 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
     __hip_atomic_fetch_add(g.step_advance, 1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int t = (NB == 10 && g.xcd2d) ? xcd2d_tile((g.M + BM - 1) / BM, tiles_n) : gemm_tile();
   const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  // a consumer's mask-bit word (mbits), loaded now: one 8-B load whose latency the k-loop hides
+  const long mw = ((long)t * 8 + wave) * 64 + lane;
+  // (the k-contiguous form only: in the AMN form, dSKIP's, they cost 8 VGPRs -- 240 -> 248, which
+  // left no room beside it for the side stream's dPRE scatter: 80 -> 297 us, step +40 us)
+  constexpr bool MB = NB == 8 && !AMN;
+  const bool bits_in = MB && g.split_stride == 0 && g.mbits, bits_out = MB && g.split_stride == 0 && g.mbits_out;
+  const unsigned long long mbr = bits_in ? g.mbits[mw] : 0ull;
   const int kz0 = gemm_split() * g.k_per_split;
   const int kz1 = min(g.K, kz0 + g.k_per_split);
   const int ntiles = (kz1 - kz0) / X3_BK;   // K % 32 == 0 (pre-split B; AMN: checked by the launcher)
@@ -998,7 +1005,8 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
         __builtin_amdgcn_raw_buffer_store_b128((floatx4){a0, a1, a2, a3}, rc, off, 0, 16);
       }
     }
-  } else
+  } else {
+  unsigned long long mbw = 0ull;
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     cs[nb] = 0.f;
@@ -1007,11 +1015,10 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int rowc = min(rbase + 16 * (e >> 2) + 4 * fq + (e & 3), g.M - 1);
-      if (!raw && g.mask) mv[e] = g.mask[(long)rowc * g.ldm + colc];
+      if (!raw && g.mask && !bits_in) mv[e] = g.mask[(long)rowc * g.ldm + colc];
       if (!raw && g.accumulate) cv[e] = C[(long)rowc * g.ldc + colc];
     }
     const float bv = (!raw && g.bias) ? g.bias[colc] : 0.f;
-    if (col >= g.N) continue;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int row = rbase + 16 * (e >> 2) + 4 * fq + (e & 3);
@@ -1019,9 +1026,15 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
       if (!raw) {
         v += bv;
         if (g.relu_out) v = fmaxf(v, 0.f);
-        if (g.mask && !(mv[e] > 0.f)) v = 0.f;
+        if (bits_in) {
+          if (!((mbr >> (8 * nb + e)) & 1ull)) v = 0.f;
+        } else if (g.mask && !(mv[e] > 0.f)) {
+          v = 0.f;
+        }
+        if (bits_out && v > 0.f) mbw |= 1ull << (8 * nb + e);
         if (g.accumulate) v += cv[e];
       }
+      if (col >= g.N) continue;
       if (row < g.M) {
         if (g.c_chain_ls)
           C[(col >> 5) * g.c_chain_ls + ((((long)(row >> 5) * 4 + ((col >> 3) & 3)) * 32 + (row & 31)) * 8 + (col & 7))] = v;
@@ -1030,6 +1043,8 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
         cs[nb] += v;
       }
     }
+  }
+  if (bits_out) g.mbits_out[mw] = mbw;
   }
   if (g.colpart && !raw) {   // the block's 256-row column partials: lane quarters, then waves in order
     float* red = (float*)smem;   // free after the k-loop's last barrier
@@ -1124,6 +1139,10 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
                "gemm (bf16 split): chain-order C needs split_k = 1, no accumulate/mask, N %% 32 == 0");
   LBWN_REQUIRE(a.b3 == nullptr || (a.K % X3_BK == 0 && (((uintptr_t)a.b3) & 15) == 0),
                "gemm (bf16 split): pre-split B needs K %% 32 == 0 and 16-B alignment");
+  LBWN_REQUIRE(!(a.mbits || a.mbits_out) ||
+                   (lbwn_gemm_x3q8_form(a.M, a.N, a.K, a_kcontig, a.b3 != nullptr, a.row_exact, a.colpart != nullptr) &&
+                    split_k <= 1),
+               "gemm (bf16 split): mask bits need the gemm_x3q_kernel<8> form without split-K");
   // 256-row tiles (8 waves, 2-stage pipeline) for the tall k-contiguous products with N <= 2048
   // (skip fwd, post1/post2 fwd, dH1, dS: 3-8 % faster; dZ, N = 1600: step -0.5 % in a same-box
   // A/B since the epilogue and split changes); 128-row tiles at 2 blocks per CU for the rest
@@ -1157,7 +1176,7 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
       // a.xcd2d (the caller's choice): the 2-D XCD blocking of the tiles (xcd2d_tile)
       grid.x = (unsigned)(((a.M + 255) / 256) * (a.N / 160));
       gemm_x3q_kernel<10><<<grid, 512, 0, st>>>(g);
-    } else if (X3Q) {
+    } else if (X3Q) {   // (lbwn_gemm_x3q8_form)
       gemm_x3q_kernel<8><<<grid, 512, 0, st>>>(g);
     } else {
       gemm_x3r_kernel<4><<<grid, 512, 0, st>>>(g);
@@ -1205,6 +1224,12 @@ int lbwn_gemm_set_mode_impl(int mode) {
   LBWN_REQUIRE(mode == 0 || mode == 1, "gemm_set_mode: mode must be 0 (f32 MFMA) or 1 (bf16 split)");
   g_gemm_mode = mode;
   return 0;
+}
+
+bool lbwn_gemm_x3q8_form(int M, int N, int K, int a_kcontig, int presplit, int row_exact, int colpart) {
+  const bool wm4 = colpart || (a_kcontig && N <= 2048 && (M >= 8192 || row_exact));
+  return X3Q && lbwn_gemm_mode() == 1 && M >= 4 && N >= 4 && K >= 4 && wm4 && presplit && a_kcontig &&
+         K % X3_BK == 0 && !(N <= 96) && !(N % 160 == 0 && N > 512);
 }
 
 int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,

@@ -36,7 +36,17 @@ struct lbwn_gemm_args {
   // training forward's head GEMMs, so a slice processed in stages equals one long slice bit for
   // bit (README.md:6-21)
   int row_exact;
+  // gemm_x3q_kernel<8> tile form (lbwn_gemm_x3q8_form) only: the relu / mask predicate of the C
+  // values as one 64-bit word per lane ([tile][wave][lane]: bit 8·nb + e = element (e, nb) of the
+  // lane's epilogue), so a later GEMM of the SAME shape and form masks by it (mbits) instead of
+  // reading an f32 M×N mask: mbits_out (producer) sets bit = (final C > 0); mbits (consumer)
+  // replaces mask.  lbwn_gemm_mbits_words(M, N) words each.
+  unsigned long long* mbits_out;
+  const unsigned long long* mbits;
 };
+// the tall pre-split product that runs gemm_x3q_kernel<8> (the form mbits / mbits_out need)
+bool lbwn_gemm_x3q8_form(int M, int N, int K, int a_kcontig, int presplit, int row_exact, int colpart);
+inline long lbwn_gemm_mbits_words(long M, long N) { return ((M + 255) / 256) * ((N + 127) / 128) * 8 * 64; }
 int lbwn_gemm_launch(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int split_k, float* slab_ws,
                      hipStream_t st);
 inline int lbwn_colpart_parts(long M) { return (int)((M + 255) / 256); }

@@ -1011,8 +1011,7 @@ LBWN_DEV void conv16_init(const float* bs, const floatx4 (&cv)[4], int q0, int h
 // of the NP parts (4 / NP accumulator blocks) are read before its MFMAs (NP = 2 halves the live
 // fragments for the register-tight LC form)
 template <int NP = 1>
-LBWN_DEV void conv16_tap(const float* xrow, const unsigned short* Wt, int i16, int g, floatx4 (&acc)[4]) {
-  const floatx4 x0 = *(const floatx4*)(xrow + 8 * g), x1 = *(const floatx4*)(xrow + 8 * g + 4);
+LBWN_DEV void conv16_tap_x(floatx4 x0, floatx4 x1, const unsigned short* Wt, int i16, int g, floatx4 (&acc)[4]) {
   bf16x8 xb[3];
 #pragma unroll
   for (int part = 0; part < NP; ++part) {
@@ -1029,6 +1028,10 @@ LBWN_DEV void conv16_tap(const float* xrow, const unsigned short* Wt, int i16, i
 #pragma unroll
     for (int ii = 0; ii < NB; ++ii) acc[part * NB + ii] = mfma16x3(wf[ii], xb, acc[part * NB + ii]);
   }
+}
+template <int NP = 1>
+LBWN_DEV void conv16_tap(const float* xrow, const unsigned short* Wt, int i16, int g, floatx4 (&acc)[4]) {
+  conv16_tap_x<NP>(*(const floatx4*)(xrow + 8 * g), *(const floatx4*)(xrow + 8 * g + 4), Wt, i16, g, acc);
 }
 
 // lc·[LC_SIGNAL_l | LC_GATE_l] onto the accumulators: A = LC16 image rows, B = the lane's LC input
@@ -1062,6 +1065,9 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
   // after the publish barrier (landing with the next layer's halo loads, like the LC image);
   // the others prefetch it into registers behind the halo loads and write it after the barrier
   constexpr bool DMAIMG = LC;
+  // per-wave halo (below); the LC form keeps the block-wide halo barrier, which also lands its
+  // LDS-DMA'd images
+  constexpr bool WH = !LC;
   constexpr int PF = DMAIMG ? 1 : (IMGF / 4 + NT - 1) / NT;   // float4 per thread to prefetch one image
   constexpr int NR = TP * 8 / NT;                       // float4 per thread of a TP-row tile (2)
   __shared__ __attribute__((aligned(16))) float sm[cf16_lds<NW>(LC)];
@@ -1157,8 +1163,34 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
       const float* br = bias_of(Wl) + 64;
       floatx4 pf[PF];
       FSTAMP(1);
-      // wait for the producer of the halo rows
       const int ptt = tt - max(1, d / TP);
+      floatx4 hx[2];   // WH: this lane's halo row x[t0 + r - d], channels 8g..8g+7 (rows r < d)
+      if (WH) {
+        // per-wave halo: only the waves holding rows r < d wait for the producer (one lane polls)
+        // and load their lanes' halo rows into registers; the rest start the layer at once, so a
+        // SIMD's other wave computes through the hand-off.  The barrier here only publishes the
+        // image written after the last layer's end barrier (the own tap of the next layer reads it
+        // before any later barrier)
+        if (l > 0) __syncthreads();
+        FSTAMP(2);
+        const int nh = min(d, TP);
+        if (16 * w < nh) {
+          if (l > 0 && ptt >= 0 && lane == 0 && !s_fail) {
+            if (!wait_flag_ge(a.flags + (long)b * tps + ptt, (unsigned)l, a.status, 1u)) s_fail = 1;
+          }
+          const __amdgpu_buffer_rsrc_t rs =
+              __builtin_amdgcn_make_buffer_rsrc(xl, (short)0, (int)((long)(a.H + a.T) * 32 * 4), BUF_DW3);
+          const int off = ((a.H + t0 + min(r, nh - 1) - d) * 32 + 8 * g) * 4;
+          hx[0] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+          hx[1] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 16);
+        }
+        if (!DMAIMG) {   // the image of layer l+2 behind the halo loads
+          const floatx4* src = (const floatx4*)(wsrc + (long)min(l + 2, a.L - 1) * IMGF);
+#pragma unroll
+          for (int i = 0; i < PF; ++i) pf[i] = src[min(tid + NT * i, IMGF / 4 - 1)];
+        }
+      } else {
+      // wait for the producer of the halo rows
       if (l > 0 && ptt >= 0) {
         if (tid == 0 && !s_fail) {
           if (!wait_flag_ge(a.flags + (long)b * tps + ptt, (unsigned)l, a.status, 1u)) s_fail = 1;
@@ -1188,6 +1220,7 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
         }
       }
       __syncthreads();
+      }
       FSTAMP(3);
       // residual weights (RT rows 16rb + i16, k group g) read now
       bf16x8 rf[2][3];
@@ -1200,8 +1233,18 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
       }
       __builtin_amdgcn_sched_barrier(0);
       // dilated tap W0·x[t-d], gate
-      const float* xp = (r >= d) ? cur + (r - d) * XS : HALO + r * XS;
-      conv16_tap<LC ? 2 : 1>(xp, (const unsigned short*)Wl, i16, g, acc);
+      if (WH) {
+        const float* xp = cur + max(r - d, 0) * XS + 8 * g;
+        floatx4 x0 = *(const floatx4*)xp, x1 = *(const floatx4*)(xp + 4);
+        if (r < d) {
+          x0 = hx[0];
+          x1 = hx[1];
+        }
+        conv16_tap_x<LC ? 2 : 1>(x0, x1, (const unsigned short*)Wl, i16, g, acc);
+      } else {
+        const float* xp = (r >= d) ? cur + (r - d) * XS : HALO + r * XS;
+        conv16_tap<LC ? 2 : 1>(xp, (const unsigned short*)Wl, i16, g, acc);
+      }
       floatx4 z[2], sg[2];
 #pragma unroll
       for (int bb = 0; bb < 2; ++bb)
@@ -2315,18 +2358,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 template <int NW>
 constexpr int cb16_lds() { return BIMG_F + 3 * 16 * NW * 32 + 4 * 16 * NW * XS + 8 * 96; }
 static_assert(cb16_lds<8>() * 4 + 16 <= 160 * 1024, "chain bwd16 LDS");
-static_assert(4 * 1280 <= 3 * 128 * 32, "bwd16: the partial scratch (waves 4-7) must fit in Xp | Xc | ZT");
-
-// sum over the 16 lanes of each DPP row (row_ror 8, 4, 2, 1: every lane ends with the row's total,
-// in a fixed order)
-template <int CTRL>
-LBWN_DEV float dpp_row(float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false)); }
-LBWN_DEV float row16_sum(float v) {
-  v += dpp_row<0x128>(v);
-  v += dpp_row<0x124>(v);
-  v += dpp_row<0x122>(v);
-  return v + dpp_row<0x121>(v);
-}
+static_assert(8 * 1280 <= 3 * 128 * 32, "bwd16: the partial scratch must fit in Xp | Xc | ZT");
 
 // GC rows of a wave whose 16 positions are not one voice: dv column sums per run of equal ids,
 // one atomic per run and column (as gc_scatter_x3, 16 positions)
@@ -2468,16 +2500,6 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         gv[xb] = v;
         *(floatx4*)gp = v;
       }
-      // the dx operands of its first k-step (S = 0), read ahead of the dz MFMAs: their LDS latency
-      // overlaps dz and dv instead of opening dx
-      bf16x8 fa0[2][3], fc0[2][3];
-#pragma unroll
-      for (int xb = 0; xb < 2; ++xb)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          fa0[xb][p] = *(const bf16x8*)(WD + (32 + 16 * xb + i16) * XW_ROW + 64 * p + 8 * g);
-          fc0[xb][p] = *(const bf16x8*)(WD + (16 * xb + i16) * XW_ROW + 64 * p + 8 * g);
-        }
       // 2. dz = dZ + RES·g  (f32 MFMA 16x16x4: k = g's channel 16xb + 4g + rr)
       floatx4 dz[2];
       {
@@ -2541,13 +2563,8 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         for (int xb = 0; xb < 2; ++xb)
 #pragma unroll
           for (int p = 0; p < 3; ++p) {
-            if (S == 0) {
-              fa[xb][p] = fa0[xb][p];
-              fc[xb][p] = fc0[xb][p];
-            } else {
-              fa[xb][p] = *(const bf16x8*)(WD + (32 + 16 * xb + i16) * XW_ROW + 64 * p + 32 * S + 8 * g);
-              fc[xb][p] = *(const bf16x8*)(WD + (16 * xb + i16) * XW_ROW + 64 * p + 32 * S + 8 * g);
-            }
+            fa[xb][p] = *(const bf16x8*)(WD + (32 + 16 * xb + i16) * XW_ROW + 64 * p + 32 * S + 8 * g);
+            fc[xb][p] = *(const bf16x8*)(WD + (16 * xb + i16) * XW_ROW + 64 * p + 32 * S + 8 * g);
           }
         bf16x8 bx[3];
         if (S == 0) split8(dvs[0], dvs[1], bx);
@@ -2583,24 +2600,6 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
       __syncthreads();  // DV, G, OC, Xp/Xc/ZT complete; the weight image is dead
       if (tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
       if (a.gc_dtab && !tile_uni) gc_scatter16(a.gc_dtab + (long)l * 64, a.gc_ld, DVs, DVg, w, lane, 32, gc_starts, gc_pid);
-      {  // 8. bias partials of this wave's 16 positions (column sums of dv_sig, dv_gate, g: the SIG /
-         //    GATE / RES bias gradients) from the registers, by DPP row sums, after the publish (off
-         //    the cross-tile path); lane 0 of row g holds its 8 channels of each -> part[w][96]
-        floatx4 bs4[6] = {dvs[0], dvs[1], dvg[0], dvg[1], gv[0], gv[1]};
-#pragma unroll
-        for (int k = 0; k < 6; ++k)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) bs4[k][e] = row16_sum(bs4[k][e]);
-        if (i16 == 0) {
-          float* pw = part + w * 96;
-#pragma unroll
-          for (int bb = 0; bb < 2; ++bb) {
-            *(floatx4*)(pw + 8 * (q0 + bb) + 4 * h) = bs4[bb];
-            *(floatx4*)(pw + 32 + 8 * (q0 + bb) + 4 * h) = bs4[2 + bb];
-            *(floatx4*)(pw + 64 + 16 * bb + 4 * g) = bs4[4 + bb];
-          }
-        }
-      }
       XSTAMP(4);
       // 6. dSIG / dGATE tile t4 = w & 3 (2·kind + tap) over this wave's position half:
       //    A[i = in][k = pos] = X_tap[pos][in], B[k = pos][j = o] = DV_kind[pos][o]
@@ -2657,11 +2656,21 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         }
       }
       XSTAMP(11);
+      // 8. bias partials (column sums of DVs, DVg, G: waves 0-2; lane = (row class pc, 4-column
+      //    group c4), rows pc + 8p)
       float* slab = a.slab + ((long)l * ntiles + tile) * SLAB;
+      if (w < 3) {
+        const int c4 = (lane & 7) * 4, pc = lane >> 3;
+        const float* pl = w == 0 ? DVs : w == 1 ? DVg : G;
+        floatx4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < TP / 8; ++p) s4 += *(const floatx4*)(pl + (pc + 8 * p) * XS + c4);
+        *(floatx4*)(part + pc * 96 + 32 * w + c4) = s4;
+      }
       // the next layer's producer: its flag (published after its dx of this layer, half a layer
       // ago) and then its out_c0 rows, loaded after the barrier below
       const int pn = tt + max(1, d / TP);
-      if (l > 0 && pn < tps && tid == 192 && !s_fail) {
+      if (l > 0 && pn < tps && tid == 0 && !s_fail) {
         if (!wait_flag_ge(a.flags + (long)b * tps + pn, (unsigned)(a.L - l), a.status, 2u)) s_fail = 1;
       }
       __syncthreads();   // every read of Xp/Xc/ZT/DV/G of this layer is done; part complete; the flag seen
@@ -2675,10 +2684,10 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
           gl[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
         }
       }
-      if (tid < 96) {   // the waves' bias partials in wave order
+      if (tid < 96) {
         float s1 = 0.f;
 #pragma unroll
-        for (int ww = 0; ww < NW; ++ww) s1 += part[ww * 96 + tid];
+        for (int pc = 0; pc < 8; ++pc) s1 += part[pc * 96 + tid];
         slab[5120 + tid] = s1;
       }
       XSTAMP(12);
@@ -2691,26 +2700,23 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) slab[4096 + (16 * (t4 >> 1) + 4 * g + q) * 32 + 16 * (t4 & 1) + i16] = accR[q];
       } else {
-        // (only waves 4-7 park theirs: waves 0-3 add their own half from registers, in the same order)
-        if (w >= 4) {
-          float* SCR = Xp + (w - 4) * 1280;
+        float* SCR = Xp + w * 1280;
 #pragma unroll
-          for (int q4 = 0; q4 < 4; ++q4)
-            *(floatx4*)(SCR + (q4 * 64 + lane) * 4) = floatx4{accT[4 * q4], accT[4 * q4 + 1], accT[4 * q4 + 2], accT[4 * q4 + 3]};
-          *(floatx4*)(SCR + 1024 + lane * 4) = accR;
-        }
+        for (int q4 = 0; q4 < 4; ++q4)
+          *(floatx4*)(SCR + (q4 * 64 + lane) * 4) = floatx4{accT[4 * q4], accT[4 * q4 + 1], accT[4 * q4 + 2], accT[4 * q4 + 3]};
+        *(floatx4*)(SCR + 1024 + lane * 4) = accR;
         __syncthreads();
         XSTAMP(13);
         if (w < 4) {
-          const float* S1 = Xp + w * 1280;
+          const float* S0 = Xp + w * 1280;
+          const float* S1 = Xp + (w + 4) * 1280;
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) {
-            const floatx4 v = floatx4{accT[4 * q4], accT[4 * q4 + 1], accT[4 * q4 + 2], accT[4 * q4 + 3]} +
-                              *(const floatx4*)(S1 + (q4 * 64 + lane) * 4);
+            const floatx4 v = *(const floatx4*)(S0 + (q4 * 64 + lane) * 4) + *(const floatx4*)(S1 + (q4 * 64 + lane) * 4);
 #pragma unroll
             for (int e = 0; e < 4; ++e) slab[w * 1024 + acc_row(4 * q4 + e, lane >> 5) * 32 + (lane & 31)] = v[e];
           }
-          const floatx4 v = accR + *(const floatx4*)(S1 + 1024 + lane * 4);
+          const floatx4 v = *(const floatx4*)(S0 + 1024 + lane * 4) + *(const floatx4*)(S1 + 1024 + lane * 4);
 #pragma unroll
           for (int q = 0; q < 4; ++q) slab[4096 + (16 * (w >> 1) + 4 * g + q) * 32 + 16 * (w & 1) + i16] = v[q];
         }
