@@ -1065,9 +1065,8 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
   // after the publish barrier (landing with the next layer's halo loads, like the LC image);
   // the others prefetch it into registers behind the halo loads and write it after the barrier
   constexpr bool DMAIMG = LC;
-  // per-wave halo (below); the LC form keeps the block-wide halo barrier, which also lands its
-  // LDS-DMA'd images
-  constexpr bool WH = !LC;
+  // per-wave halo (below)
+  constexpr bool WH = true;
   constexpr int PF = DMAIMG ? 1 : (IMGF / 4 + NT - 1) / NT;   // float4 per thread to prefetch one image
   constexpr int NR = TP * 8 / NT;                       // float4 per thread of a TP-row tile (2)
   __shared__ __attribute__((aligned(16))) float sm[cf16_lds<NW>(LC)];
@@ -1165,12 +1164,18 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
       FSTAMP(1);
       const int ptt = tt - max(1, d / TP);
       floatx4 hx[2];   // WH: this lane's halo row x[t0 + r - d], channels 8g..8g+7 (rows r < d)
+      // (zeroed in the LC form: left undefined on the waves that do not load it, the registers
+      // stayed live around the loop there and spilled; zeroed in the others, C2's forward measured
+      // 206 -> 216 us)
+      if (LC) hx[0] = hx[1] = floatx4{0.f, 0.f, 0.f, 0.f};
       if (WH) {
         // per-wave halo: only the waves holding rows r < d wait for the producer (one lane polls)
         // and load their lanes' halo rows into registers; the rest start the layer at once, so a
         // SIMD's other wave computes through the hand-off.  The barrier here only publishes the
         // image written after the last layer's end barrier (the own tap of the next layer reads it
         // before any later barrier)
+        // (DMAIMG: the images of layer l+1 DMA'd at the end of the last layer land first)
+        if (DMAIMG && l > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (l > 0) __syncthreads();
         FSTAMP(2);
         const int nh = min(d, TP);
@@ -1223,14 +1228,17 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
       }
       FSTAMP(3);
       // residual weights (RT rows 16rb + i16, k group g) read now
+      // (the LC form, register-tight, reads them after the dilated tap: with the halo row in
+      // registers across them it spilled)
       bf16x8 rf[2][3];
-      {
+      auto read_rf = [&]() {
         const unsigned short* rt = (const unsigned short*)Wl + 64 * XW_ROW + i16 * XR_ROW + 8 * g;
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
           for (int p = 0; p < 3; ++p) rf[rb][p] = *(const bf16x8*)(rt + 16 * rb * XR_ROW + 32 * p);
-      }
+      };
+      if (!LC) read_rf();
       __builtin_amdgcn_sched_barrier(0);
       // dilated tap W0·x[t-d], gate
       if (WH) {
@@ -1241,6 +1249,7 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
           x1 = hx[1];
         }
         conv16_tap_x<LC ? 2 : 1>(x0, x1, (const unsigned short*)Wl, i16, g, acc);
+        if (LC) read_rf();
       } else {
         const float* xp = (r >= d) ? cur + (r - d) * XS : HALO + r * XS;
         conv16_tap<LC ? 2 : 1>(xp, (const unsigned short*)Wl, i16, g, acc);
@@ -1254,6 +1263,23 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
           z[bb][j] = gate_zs(acc[bb][j], acc[2 + bb][j], sq);
           sg[bb][j] = sq;
         }
+      // z (skip GEMM input) and σ rows (sg_off blocks for chain_bwd_x3_kernel): issued last, after
+      // the publish, so the drain before it does not wait for them -- except in the LC form, whose
+      // 16 registers they hold through the residual and the next own tap spilled with the
+      // per-wave halo
+      auto store_zs = [&]() {
+        if (valid) {
+          float* zr = a.Z + m * a.ldz + (long)l * a.Cd;
+#pragma unroll
+          for (int bb = 0; bb < 2; ++bb) *(floatx4*)(zr + 8 * (q0 + bb) + 4 * h) = z[bb];
+          if (a.SG) {
+            float* sgl = a.SG + (long)l * a.sgls;
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb) *(floatx4*)(sgl + sg_off(m, q0 + bb, h)) = sg[bb];
+          }
+        }
+      };
+      if (LC) store_zs();
       FSTAMP(4);
       if (l + 1 < a.L) {
         // residual: x_{l+1} = x_l + br + RES·z → LDS (next layer's rows) and HBM (sc1 for halo rows)
@@ -1312,17 +1338,7 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
         }
       }
       FSTAMP(6);
-      // z (skip GEMM input) and σ rows (sg_off blocks for chain_bwd_x3_kernel), issued last
-      if (valid) {
-        float* zr = a.Z + m * a.ldz + (long)l * a.Cd;
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb) *(floatx4*)(zr + 8 * (q0 + bb) + 4 * h) = z[bb];
-        if (a.SG) {
-          float* sgl = a.SG + (long)l * a.sgls;
-#pragma unroll
-          for (int bb = 0; bb < 2; ++bb) *(floatx4*)(sgl + sg_off(m, q0 + bb, h)) = sg[bb];
-        }
-      }
+      if (!LC) store_zs();
       FSTAMP(7);
     }
 #undef FSTAMP
