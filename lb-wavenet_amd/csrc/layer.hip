@@ -2374,7 +2374,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 template <int NW>
 constexpr int cb16_lds() { return BIMG_F + 3 * 16 * NW * 32 + 4 * 16 * NW * XS + 8 * 96; }
 static_assert(cb16_lds<8>() * 4 + 16 <= 160 * 1024, "chain bwd16 LDS");
-static_assert(8 * 1280 <= 3 * 128 * 32, "bwd16: the partial scratch must fit in Xp | Xc | ZT");
+static_assert(4 * 1280 <= 3 * 128 * 32, "bwd16: the partial scratch (waves 4-7) must fit in Xp | Xc | ZT");
 
 // GC rows of a wave whose 16 positions are not one voice: dv column sums per run of equal ids,
 // one atomic per run and column (as gc_scatter_x3, 16 positions)
@@ -2716,23 +2716,26 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) slab[4096 + (16 * (t4 >> 1) + 4 * g + q) * 32 + 16 * (t4 & 1) + i16] = accR[q];
       } else {
-        float* SCR = Xp + w * 1280;
+        // (only waves 4-7 park theirs: waves 0-3 add their own half from registers, in the same order)
+        if (w >= 4) {
+          float* SCR = Xp + (w - 4) * 1280;
 #pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4)
-          *(floatx4*)(SCR + (q4 * 64 + lane) * 4) = floatx4{accT[4 * q4], accT[4 * q4 + 1], accT[4 * q4 + 2], accT[4 * q4 + 3]};
-        *(floatx4*)(SCR + 1024 + lane * 4) = accR;
+          for (int q4 = 0; q4 < 4; ++q4)
+            *(floatx4*)(SCR + (q4 * 64 + lane) * 4) = floatx4{accT[4 * q4], accT[4 * q4 + 1], accT[4 * q4 + 2], accT[4 * q4 + 3]};
+          *(floatx4*)(SCR + 1024 + lane * 4) = accR;
+        }
         __syncthreads();
         XSTAMP(13);
         if (w < 4) {
-          const float* S0 = Xp + w * 1280;
-          const float* S1 = Xp + (w + 4) * 1280;
+          const float* S1 = Xp + w * 1280;
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) {
-            const floatx4 v = *(const floatx4*)(S0 + (q4 * 64 + lane) * 4) + *(const floatx4*)(S1 + (q4 * 64 + lane) * 4);
+            const floatx4 v = floatx4{accT[4 * q4], accT[4 * q4 + 1], accT[4 * q4 + 2], accT[4 * q4 + 3]} +
+                              *(const floatx4*)(S1 + (q4 * 64 + lane) * 4);
 #pragma unroll
             for (int e = 0; e < 4; ++e) slab[w * 1024 + acc_row(4 * q4 + e, lane >> 5) * 32 + (lane & 31)] = v[e];
           }
-          const floatx4 v = *(const floatx4*)(S0 + 1024 + lane * 4) + *(const floatx4*)(S1 + 1024 + lane * 4);
+          const floatx4 v = accR + *(const floatx4*)(S1 + 1024 + lane * 4);
 #pragma unroll
           for (int q = 0; q < 4; ++q) slab[4096 + (16 * (w >> 1) + 4 * g + q) * 32 + 16 * (w & 1) + i16] = v[q];
         }
