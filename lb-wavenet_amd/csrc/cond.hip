@@ -129,7 +129,8 @@ __global__ void lc_pack_kernel(float* __restrict__ cat, float* __restrict__ wsig
     const int n = (int)(i % ((long)L * 2 * Cd)), k = (int)(i / ((long)L * 2 * Cd));
     const int l = n / (2 * Cd), s = (n / Cd) & 1, o = n % Cd;
     float* w = (s == 0 ? wsig : wgate) + ((long)l * Clc + k) * Cd + o;
-    if (pack) cat[i] = *w;
+    if (pack == 1) cat[i] = *w;
+    else if (pack == 2) *w = cat[(long)n * Clc + k];   // unpack from catᵀ [L·2Cd][Clc]
     else *w = cat[i];
   }
 }

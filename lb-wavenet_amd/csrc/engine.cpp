@@ -18,6 +18,7 @@ struct lbwn_plan {
   int chain_xcd = 0;       // chain_first's XCD-grouped walk
   int dz_xcd2d = 1;        // dZ's tiles blocked 2-D over the XCDs (gemm.hip xcd2d_tile)
   int fwd_mode = -1;       // GEMM arithmetic (lbwn_gemm_mode) the last forward ran; the backward follows it
+  int ncu = 0;             // compute units (ensure_device)
   // (S > 0) and (R2 > 0) as GEMM mask bits (lbwn_gemm_args::mbits): written by the skip / post1
   // epilogues, read by dS / dH1 instead of the f32 S / R2; set by the forward when both ends take
   // the gemm_x3q_kernel<8> form
@@ -51,7 +52,7 @@ struct lbwn_plan {
   // backward path needs it (cond_valid: this step's COND is in the workspace)
   size_t oLCX = 0;
   bool cond_valid = false;
-  int split_dlc, split_dlcx, split_up[8];
+  int split_dlc, split_dlcx, split_dlct, split_up[8];
   size_t oSPLIT_AUX = 0;         // split-K workspace of the aux2 stream (LC / GC grads beside dSKIP)
   bool up_fused = false;         // LC upsample as one fused launch per direction (cond.hip)
   bool up_fused_bwd = false;     // ... for the backward (<= 256 mel frames; else per-stage GEMMs)
@@ -368,6 +369,11 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     const long dtiles = (M + 255) / 256 * ((p->Lo + 127) / 128);
     p->split_dlcx = (int)std::max<long>(1, std::min<long>(256 / std::max<long>(1, dtiles), (2L * L * p->Cd) / 256));
     p->split_floats = std::max(p->split_floats, (long)p->split_dlcx * M * p->Lo);
+    // dLCcat as DVᵀ·lc (the AMN form, lc_wgrad): ceil(L·2Cd / 256) row tiles, K = M split to
+    // about one block per CU
+    const long ttiles = (2L * L * p->Cd + 255) / 256;
+    p->split_dlct = (int)std::max<long>(1, std::min<long>(256 / ttiles, M / 256));
+    p->split_floats = std::max(p->split_floats, (long)p->split_dlct * 2 * L * p->Cd * p->Lo);
     long rows = (long)B * (T / hop);
     for (int i = 0; i < p->nup; ++i) {
       const int I = i == 0 ? p->Li : p->Lo;
@@ -518,6 +524,7 @@ int ensure_device(lbwn_plan* p) {
   int dev = 0, ncu = 0;
   LBWN_HIP(hipGetDevice(&dev));
   LBWN_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  p->ncu = ncu;
   const int ntiles = p->B * ((p->T + LBWN_LAYER_POS - 1) / LBWN_LAYER_POS);
   p->chain_grid = std::max(1, std::min(ntiles, ncu));
   const int tpf = lbwn_chain_fwd_tile(p->fwd_nw);
@@ -658,6 +665,20 @@ int gc_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G, void* 
 int lc_wgrad(lbwn_plan* p, const lbwn_params* G, void* ws, float* spl, hipStream_t st) {
   int e;
   const long ncond = 2L * p->L * p->Cd;
+  if (p->dv_blk && lbwn_gemm_mode() == 1 && p->M % 32 == 0 && p->Lo % 4 == 0 && ncond >= 256) {
+    // dLCcatᵀ = DVᵀ·lc on the A-in-registers weight-gradient kernel (AMN, 96-column tiles): A = the
+    // k-blocked DV export read as 32-row groups (a_gstride), B = the LC rows; C = [L·2Cd][Lo]
+    // (the LDS-staged kernel on lcᵀ·DV: C4 569 us)
+    lbwn_gemm_args g = gemm0();
+    g.A = at<float>(ws, p->oDVALL); g.lda = 32; g.a_gstride = m32(p->M) * 32;
+    g.B = at<float>(ws, p->oLCACT[p->nup - 1]); g.ldb = p->Lo;
+    g.C = at<float>(ws, p->oDLCCAT); g.ldc = p->Lo;
+    g.M = (int)ncond; g.N = p->Lo; g.K = (int)p->M;
+    Probe(p, st, "lc_wgrad");
+    if ((e = lbwn_gemm_launch(g, 0, 0, p->split_dlct, spl, st))) return e;
+    Probe::end(p, st, "lc_wgrad");
+    return lbwn_lc_pack_launch(at<float>(ws, p->oDLCCAT), G->lc_sig, G->lc_gate, p->L, p->Lo, p->Cd, 2, st);
+  }
   lbwn_gemm_args g = gemm0();
   g.A = at<float>(ws, p->oLCACT[p->nup - 1]); g.lda = p->Lo; g.B = at<float>(ws, p->oDVALL); g.ldb = ncond;
   if (p->dv_blk) { g.ldb = 32; g.b_gstride = m32(p->M) * 32; }
@@ -1121,13 +1142,16 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     r.slab = SLABS; r.nparts = ntiles; r.stride = sstr; r.Cr = Cr; r.Cd = Cd;
     r.dsig = G->sig; r.dgate = G->gate; r.dres = G->res;
     r.dbsig = G->sig_b; r.dbgate = G->gate_b; r.dbres = G->res_b;
-    // Side stream, beside the main stream's dlc (LC archs) and dSKIP: dLCcat = lcᵀ·DV first (the
-    // largest piece), then dPRE and the slab reduction (the small scatter grid starts while the
-    // main stream's GEMM blocks still leave room: step -0.5 %), the GC table grads,
-    // and the LC upsample backward once dlc (main stream) is done: small latency-bound GEMMs that
-    // fill the room dSKIP leaves.
+    // Side stream (the higher priority), beside the main stream's dlc (LC archs) and dSKIP:
+    // dLCcat = lcᵀ·DV first while dlc takes one round of blocks (C5), then dPRE and the slab
+    // reduction (the small scatter grid starts while the main stream's GEMM blocks still leave
+    // room: step -0.5 %) and the GC table grads.  When dlc needs more than one
+    // round of blocks (C4: 512 tiles), dLCcat's higher-priority blocks took its CUs and both
+    // streamed the 1.7 GB DV export at once (dlc 1235 us, alone 584): there dLCcat follows the
+    // LC upsample backward on the main stream.
     float* SPLA = p->oSPLIT_AUX ? at<float>(ws, p->oSPLIT_AUX) : SPL;
-    if (p->Lo > 0 && (e = lc_wgrad(p, G, ws, SPLA, rst))) return e;
+    const bool lc_seq = p->Lo > 0 && (p->M + 255) / 256 * (long)p->split_dlcx > p->ncu;
+    if (p->Lo > 0 && !lc_seq && (e = lc_wgrad(p, G, ws, SPLA, rst))) return e;
     if ((e = lbwn_pre_grad_launch(wav_q, at<float>(ws, p->oGA[0]), at<float>(ws, p->oGC0[0]), 1, B, T, Cr, Q, G->pre,
                                   G->pre_b, at<float>(ws, p->oSPLIT2), rst)))
       return e;
@@ -1137,12 +1161,11 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     if (c.tile_gid && (e = lbwn_gc_tile_sum_launch(SLABS, L, ntiles, c.tile_gid, cd.gc_dtab, cd.gc_ld, p->ncat1, rst)))
       return e;
     if ((e = gc_backward(p, P, G, ws, rst))) return e;
-    // main stream: dlc, then the LC upsample backward (it needs dlc), then dSKIP below; the side
-    // stream keeps dLCcat, dPRE, the slab reduction and the GC grads (arch5 tail 916 -> ~800 us:
-    // behind dLCcat on the side stream the upsample backward was the last thing to finish)
+    // main stream: dlc, the LC upsample backward (it needs dlc), [dLCcat,] then dSKIP below
     if (p->Lo > 0) {
       if ((e = lc_dlc(p, P, ws, SPL, st))) return e;
       if ((e = lc_upsample_bwd(p, P, G, ws, mel, SPL, st, rst))) return e;   // its frame sum on the side
+      if (lc_seq && (e = lc_wgrad(p, G, ws, SPL, st))) return e;
     }
     if (p->aux2) LBWN_HIP(hipEventRecord(p->ev_join2, rst));
   } else {

@@ -851,9 +851,13 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
 
   const int fr = lane & 15, fq = lane >> 4;
   const long aks = g.a_kstride ? g.a_kstride : X3_BK;   // floats per 32-deep k-step of A
-  const float* pa0 = AMN ? g.A + min(m0 + 32 * wave + fr, g.M - 1) + (long)(kz0 + 8 * fq) * g.lda
+  // (AMN with a_gstride: the wave's 32 rows are one 32-row group, clamped whole into the matrix)
+  const int ag0 = min(m0 + 32 * wave, max((g.M - 1) & ~31, 0));
+  const float* pa0 = AMN ? (g.a_gstride ? g.A + (ag0 >> 5) * g.a_gstride + fr + (long)(kz0 + 8 * fq) * 32
+                                        : g.A + min(m0 + 32 * wave + fr, g.M - 1) + (long)(kz0 + 8 * fq) * g.lda)
                          : g.A + (long)min(m0 + 32 * wave + fr, g.M - 1) * g.lda + (kz0 / X3_BK) * aks + 8 * fq;
-  const float* pa1 = AMN ? g.A + min(m0 + 32 * wave + 16 + fr, g.M - 1) + (long)(kz0 + 8 * fq) * g.lda
+  const float* pa1 = AMN ? (g.a_gstride ? pa0 + 16
+                                        : g.A + min(m0 + 32 * wave + 16 + fr, g.M - 1) + (long)(kz0 + 8 * fq) * g.lda)
                          : g.A + (long)min(m0 + 32 * wave + 16 + fr, g.M - 1) * g.lda + (kz0 / X3_BK) * aks + 8 * fq;
   const int alo = g.relu_a ? 0 : (int)0x80000000;   // relu as an integer max (x3_store4)
   floatx4 av[2][4];
@@ -1087,6 +1091,10 @@ int gemm_setup(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int& split
                "gemm: k-blocked A needs k-contiguous A, lda = 32, K %% 32 == 0 and the bf16-split form");
   LBWN_REQUIRE(!a.b_gstride || (!b_kcontig && a.ldb == 32 && !a.b3 && lbwn_gemm_mode() == 1),
                "gemm: mn-blocked B needs mn-contiguous B, ldb = 32, no pre-split and the bf16-split form");
+  LBWN_REQUIRE(!a.a_gstride || (!a_kcontig && a.lda == 32 && !b_kcontig && !a.b_gstride && !a.b3 && a.M >= 256 &&
+                                a.K % 32 == 0 && !a.mask && !a.bias && !a.colpart && !a.c_chain_ls && !a.a_codes &&
+                                lbwn_gemm_mode() == 1),
+               "gemm: mn-blocked A needs the AMN weight-gradient form (lda = 32, M >= 256, K %% 32 == 0)");
   if (split_k < 1) split_k = 1;
   g = a;
   int kps = (a.K + split_k - 1) / split_k;
@@ -1155,12 +1163,14 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
   if (e) return e;
   const bool kfull = a.K % X3_BK == 0, pre = a.b3 != nullptr;
   if (X3Q && !a_kcontig && !b_kcontig && kfull && !pre && !a.mask && !a.bias && !a.colpart && !a.c_chain_ls &&
-      !a.b_gstride && a.M >= 256 && a.N % 4 == 0 && ((a.M + 255) / 256) * ((a.N + 127) / 128) >= 8) {
+      !a.b_gstride && a.M >= 256 && a.N % 4 == 0 && (((a.M + 255) / 256) * ((a.N + 127) / 128) >= 8 || a.a_gstride)) {
     // the weight-gradient products with >= 8 output tiles (dSKIP, dPOST1): 256 x 128 tiles with A
     // in registers (gemm_x3q_kernel AMN).  tools/gemm_bench.py, same box: dSKIP split 9 315 vs
-    // 355 us, dPOST1 split 32 97 vs 107; dPOST2 (4 tiles) 87 vs 77 stays on the 2-per-CU kernel
-    if ((e = gemm_setup(a, a_kcontig, b_kcontig, split_k, slab_ws, X3_BK, 256, 128, g, grid))) return e;
-    gemm_x3q_kernel<8, true><<<grid, 512, 0, st>>>(g);
+    // 355 us, dPOST1 split 32 97 vs 107; dPOST2 (4 tiles) 87 vs 77 stays on the 2-per-CU kernel.
+    // N <= 96 (dLCcat as DVᵀ·lc, N = n_lc_out): 96-column tiles
+    if ((e = gemm_setup(a, a_kcontig, b_kcontig, split_k, slab_ws, X3_BK, 256, a.N <= 96 ? 96 : 128, g, grid))) return e;
+    if (a.N <= 96) gemm_x3q_kernel<6, true><<<grid, 512, 0, st>>>(g);
+    else gemm_x3q_kernel<8, true><<<grid, 512, 0, st>>>(g);
     LBWN_CHECK_LAUNCH();
     return splitk_finish(a, split_k, slab_ws, st);
   }

@@ -29,8 +29,10 @@ struct lbwn_gemm_args {
   // k-blocked operands (the backward chain's DV export, [K/32][Mp][32]): 0 = plain layout.
   // a_kstride: A k-contiguous with lda = 32, element (m, k) at A[m·32 + (k/32)·a_kstride + k%32]
   // (gemm_x3q_kernel only); b_gstride: B mn-contiguous with ldb = 32, element (k, n) at
-  // B[k·32 + (n/32)·b_gstride + n%32] (the LDS-staged bf16-split kernel only)
-  long a_kstride, b_gstride;
+  // B[k·32 + (n/32)·b_gstride + n%32] (the LDS-staged bf16-split kernel only); a_gstride: A
+  // mn-contiguous with lda = 32, element (m, k) at A[k·32 + (m/32)·a_gstride + m%32] (the AMN
+  // form of gemm_x3q_kernel only: dLCcat as DVᵀ·lc)
+  long a_kstride, b_gstride, a_gstride;
   // 1: every output row is computed by the same kernel and k order whatever M is (the tall
   // 256-row form below M = 8192 too), so a row's value depends only on its own A row: the
   // training forward's head GEMMs, so a slice processed in stages equals one long slice bit for
