@@ -79,6 +79,7 @@ struct lbwn_plan {
   hipEvent_t ev_chain = nullptr, ev_join2 = nullptr;
   hipEvent_t ev_fwd_fork = nullptr, ev_fwd_up = nullptr;   // forward: LC upsample on aux2
   hipEvent_t ev_upb = nullptr;   // backward: the upsample's per-frame pass done (main) -> its sum (aux2)
+  hipEvent_t ev_dlc = nullptr;   // backward (dlc over more than one round of blocks): dlc done -> aux2
   bool up_forked = false;        // this forward launched the fused upsample on aux2
   bool bwd_chain_event = false;  // the last backward recorded ev_chain (lbwn_plan_stream_wait)
   bool wpk_valid = false;        // the f32 layer images were packed this step
@@ -93,6 +94,7 @@ struct lbwn_plan {
     if (ev_fwd_fork) (void)hipEventDestroy(ev_fwd_fork);
     if (ev_fwd_up) (void)hipEventDestroy(ev_fwd_up);
     if (ev_upb) (void)hipEventDestroy(ev_upb);
+    if (ev_dlc) (void)hipEventDestroy(ev_dlc);
     if (ev_join2) (void)hipEventDestroy(ev_join2);
   }
   // one-shot event probe
@@ -540,6 +542,7 @@ int ensure_device(lbwn_plan* p) {
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_fwd_fork, hipEventDisableTiming));
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_fwd_up, hipEventDisableTiming));
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_upb, hipEventDisableTiming));
+    LBWN_HIP(hipEventCreateWithFlags(&p->ev_dlc, hipEventDisableTiming));
   }
   return 0;
 }
@@ -1151,6 +1154,15 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     // LC upsample backward on the main stream.
     float* SPLA = p->oSPLIT_AUX ? at<float>(ws, p->oSPLIT_AUX) : SPL;
     const bool lc_seq = p->Lo > 0 && (p->M + 255) / 256 * (long)p->split_dlcx > p->ncu;
+    if (lc_seq) {   // dlc, the upsample backward and dLCcat first; the side stream then runs beside dSKIP
+      if ((e = lc_dlc(p, P, ws, SPL, st))) return e;
+      if ((e = lc_upsample_bwd(p, P, G, ws, mel, SPL, st, st))) return e;
+      if ((e = lc_wgrad(p, G, ws, SPL, st))) return e;
+      if (rst != st) {
+        LBWN_HIP(hipEventRecord(p->ev_dlc, st));
+        LBWN_HIP(hipStreamWaitEvent(rst, p->ev_dlc, 0));
+      }
+    }
     if (p->Lo > 0 && !lc_seq && (e = lc_wgrad(p, G, ws, SPLA, rst))) return e;
     if ((e = lbwn_pre_grad_launch(wav_q, at<float>(ws, p->oGA[0]), at<float>(ws, p->oGC0[0]), 1, B, T, Cr, Q, G->pre,
                                   G->pre_b, at<float>(ws, p->oSPLIT2), rst)))
@@ -1163,9 +1175,8 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     if ((e = gc_backward(p, P, G, ws, rst))) return e;
     // main stream: dlc, the LC upsample backward (it needs dlc), [dLCcat,] then dSKIP below
     if (p->Lo > 0) {
-      if ((e = lc_dlc(p, P, ws, SPL, st))) return e;
-      if ((e = lc_upsample_bwd(p, P, G, ws, mel, SPL, st, rst))) return e;   // its frame sum on the side
-      if (lc_seq && (e = lc_wgrad(p, G, ws, SPL, st))) return e;
+      if (!lc_seq && (e = lc_dlc(p, P, ws, SPL, st))) return e;
+      if (!lc_seq && (e = lc_upsample_bwd(p, P, G, ws, mel, SPL, st, rst))) return e;   // its frame sum on the side
     }
     if (p->aux2) LBWN_HIP(hipEventRecord(p->ev_join2, rst));
   } else {
