@@ -875,6 +875,13 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
         av[S][j >> 2][j & 3] = pa0[ko + j * g.lda];
         av[S][2 + (j >> 2)][j & 3] = pa1[ko + j * g.lda];
       }
+    } else if (NB == 10) {
+      // dZ: A row panels non-temporal, so that the 6.4 panels in flight per XCD do not evict the
+      // B half its L2 keeps for the launch (xcd2d_tile)
+      av[S][0] = __builtin_nontemporal_load((const floatx4*)(pa0 + kt * aks));
+      av[S][1] = __builtin_nontemporal_load((const floatx4*)(pa0 + kt * aks + 4));
+      av[S][2] = __builtin_nontemporal_load((const floatx4*)(pa1 + kt * aks));
+      av[S][3] = __builtin_nontemporal_load((const floatx4*)(pa1 + kt * aks + 4));
     } else {
       av[S][0] = *(const floatx4*)(pa0 + kt * aks);
       av[S][1] = *(const floatx4*)(pa0 + kt * aks + 4);
@@ -1014,6 +1021,61 @@ __global__ __launch_bounds__(512, 1) void gemm_x3q_kernel(lbwn_gemm_args g) {
         __builtin_amdgcn_raw_buffer_store_b128((floatx4){a0, a1, a2, a3}, rc, off, 0, 16);
       }
     }
+  } else if (!g.accumulate && (g.ldc & 3) == 0 && (g.N & 3) == 0 && !((uintptr_t)C & 15)) {
+    // row-major C: the elementwise epilogue per element, then the dZ path's 4x4 quad transpose so
+    // that each lane stores one row x 4 consecutive columns as one 16-B store (64 single-float
+    // stores per lane before)
+    unsigned long long mbw = 0ull;
+    const int c = fr & 3;
+    const bool odd = c & 1, hi = c & 2;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      cs[nb] = 0.f;
+      const int col0 = n0 + nb * 16;
+      if (col0 >= g.N) continue;   // wave-uniform
+      const int col = col0 + fr, colc = min(col, g.N - 1);
+      float mv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int rowc = min(rbase + 16 * (e >> 2) + 4 * fq + (e & 3), g.M - 1);
+        if (!raw && g.mask && !bits_in) mv[e] = g.mask[(long)rowc * g.ldm + colc];
+      }
+      const float bv = (!raw && g.bias) ? g.bias[colc] : 0.f;
+      float vv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int row = rbase + 16 * (e >> 2) + 4 * fq + (e & 3);
+        float v = acc[e >> 2][nb][e & 3];
+        if (!raw) {
+          v += bv;
+          if (g.relu_out) v = fmaxf(v, 0.f);
+          if (bits_in) {
+            if (!((mbr >> (8 * nb + e)) & 1ull)) v = 0.f;
+          } else if (g.mask && !(mv[e] > 0.f)) {
+            v = 0.f;
+          }
+          if (bits_out && v > 0.f) mbw |= 1ull << (8 * nb + e);
+        }
+        vv[e] = v;
+        if (col < g.N && row < g.M) cs[nb] += v;
+      }
+      const int colq = col0 + 4 * (fr >> 2);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        float a0 = vv[4 * mi], a1 = vv[4 * mi + 1], a2 = vv[4 * mi + 2], a3 = vv[4 * mi + 3];
+        {
+          const float r0 = quad_xor<0xB1>(odd ? a0 : a1), r1 = quad_xor<0xB1>(odd ? a2 : a3);
+          if (odd) { a0 = r0; a2 = r1; } else { a1 = r0; a3 = r1; }
+        }
+        {
+          const float q0 = quad_xor<0x4E>(hi ? a0 : a2), q1 = quad_xor<0x4E>(hi ? a1 : a3);
+          if (hi) { a0 = q0; a1 = q1; } else { a2 = q0; a3 = q1; }
+        }
+        const int row = rbase + 16 * mi + 4 * fq + c;
+        if (row < g.M && colq < g.N) *(floatx4*)(C + (long)row * g.ldc + colq) = (floatx4){a0, a1, a2, a3};
+      }
+    }
+    if (bits_out) g.mbits_out[mw] = mbw;
   } else {
   unsigned long long mbw = 0ull;
 #pragma unroll

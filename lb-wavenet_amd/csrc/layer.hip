@@ -1834,11 +1834,23 @@ __global__ __launch_bounds__(256) void chain_bwd_kernel(ChainBK a) {
 //    b128 writes and the column reads of the weight-gradient products are conflict-free.
 // Backward image per layer: WD[tap][in][plane][kk] (bf16, row XW_ROW) with kk = 16s+8h+j holding
 // out channel o = 32(s>>1) + 16(s&1) + 8(j>>2) + 4h + (j&3) (sig 0..31 | gate 32..63): the k order
-// of the dv registers used as the B operand; then Rs f32 [c][XS] for the dz product.  Padded to
-// a whole number of 1-KiB DMA pieces.
+// of the dv registers used as the B operand; then Rs f32 [c][XS] for the dz product of
+// chain_bwd_x3_kernel, padded to a whole number of 1-KiB DMA pieces (BX_F: what that kernel
+// loads); then RX, the same residual weights split for chain_bwd16_kernel's dz on the bf16 cores:
+// RX[c][plane][kk] (bf16, row RX_ROW) with kk = 8g + e holding res channel 16(e >> 2) + 4g + (e & 3)
+// (the order of the lane's two N-layout g registers).  chain_bwd16_kernel loads WD and RX only
+// (B16IMG_F floats: global pieces [0, BD_PC) and [RX_GPC, RX_GPC + RX_PC)).
 constexpr int BD_US = 2 * 32 * XW_ROW;
-constexpr int BIMG_F = (BD_US / 2 + 32 * XS + 255) / 256 * 256;   // 7680 floats
-constexpr int CBX_LDS = BIMG_F + 7 * LP * 32 + 8 * 96;            // IMG | Xp Xc ZT | DVs DVg G OC | part
+constexpr int BX_F = (BD_US / 2 + 32 * XS + 255) / 256 * 256;   // 7680 floats
+// 224-B RX rows (14 16-B slots): the 16x16x32 A-fragment reads (rows ch16(bb, i), slot 4p + g) hit
+// 16 distinct slots in every ds_read_b128 lane group (MI355X_MICROARCH.md §LDS)
+constexpr int RX_ROW = 112;
+constexpr int RX_F = 32 * RX_ROW / 2;                          // 1792 floats
+constexpr int BIMG_F = BX_F + RX_F;                            // 9472 floats: global stride per layer
+constexpr int B16IMG_F = BD_US / 2 + RX_F;                     // 8192 floats in chain_bwd16_kernel's LDS
+constexpr int BD_PC = BD_US / 2 / 256, RX_GPC = BX_F / 256, RX_PC = RX_F / 256;
+static_assert(BD_US / 2 % 256 == 0 && RX_F % 256 == 0 && B16IMG_F % 256 == 0, "bwd image: whole DMA pieces");
+constexpr int CBX_LDS = BX_F + 7 * LP * 32 + 8 * 96;              // IMG | Xp Xc ZT | DVs DVg G OC | part
 static_assert(CBX_LDS * 4 + 16 <= 160 * 1024, "chain bwd x3 LDS");
 
 LBWN_DEV void pack_bx3_body(int l, const float* sig, const float* gate, const float* res, float* out, int Cr, int Cd) {
@@ -1869,7 +1881,23 @@ LBWN_DEV void pack_bx3_body(int l, const float* sig, const float* gate, const fl
     const int c = e / XS, o = e % XS;
     rs[e] = (c < Cd && o < Cr) ? wr[c * Cr + o] : 0.f;
   }
-  for (int e = BD_US / 2 + 32 * XS + threadIdx.x; e < BIMG_F; e += blockDim.x) img[e] = 0.f;
+  for (int e = BD_US / 2 + 32 * XS + threadIdx.x; e < BX_F; e += blockDim.x) img[e] = 0.f;
+  unsigned short* rx = (unsigned short*)(img + BX_F);
+  for (int e = threadIdx.x; e < 32 * 16; e += blockDim.x) {
+    const int c = e >> 4, kk = 2 * (e & 15);
+    floatx2 x = {0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k2 = kk + u, gg = k2 >> 3, ee = k2 & 7, o = 16 * (ee >> 2) + 4 * gg + (ee & 3);
+      if (c < Cd && o < Cr) x[u] = wr[c * Cr + o];
+    }
+    unsigned hi, mi, lo;
+    split2(x, hi, mi, lo);
+    unsigned short* row = rx + c * RX_ROW + kk;
+    *(unsigned*)(row) = hi;
+    *(unsigned*)(row + 32) = mi;
+    *(unsigned*)(row + 64) = lo;
+  }
 }
 
 __global__ void pack_layers_x3_kernel(const float* sig, const float* gate, const float* sig_b, const float* gate_b,
@@ -2002,7 +2030,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
   float* IMG = sm;
   const unsigned short* WD = (const unsigned short*)IMG;
   const float* Rs = IMG + BD_US / 2;
-  float* Xp = IMG + BIMG_F;
+  float* Xp = IMG + BX_F;
   float* Xc = Xp + LP * 32;
   float* ZT = Xc + LP * 32;
   float* DVs = ZT + LP * 32;
@@ -2051,7 +2079,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
     };
     auto dma_image = [&](int l) {
       const float* src = a.bimg + (long)l * BIMG_F + lane * 4;
-      for (int i = w; i < BIMG_F / 256; i += 4) dma16(src + i * 256, IMG + i * 256);
+      for (int i = w; i < BX_F / 256; i += 4) dma16(src + i * 256, IMG + i * 256);
     };
     __syncthreads();  // previous tile's LDS use done
     dma_image(a.L - 1);
@@ -2257,7 +2285,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const int pc = w + 4 * i;
-            if (pc < BIMG_F / 256 && !CONF(1024)) dma16(isrc + pc * 256, IMG + pc * 256);
+            if (pc < BX_F / 256 && !CONF(1024)) dma16(isrc + pc * 256, IMG + pc * 256);
           }
           load_regs(l - 1);
         }
@@ -2361,8 +2389,9 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 // layouts per lane (q0 = 2(g >> 1), h = g & 1):
 //   N  (x / g / out_a / out_c0): block xb register r = channel 16xb + 4g + r;
 //   Zl (dz / z / σ / dv, the forward's z layout): block b register r = channel 8(q0 + b) + 4h + r.
-//  * dz = dZ + RES·g on v_mfma_f32_16x16x4_f32 (f32 products, as chain_bwd_x3_kernel): A row i of
-//    block b = z channel ch16(b, i), k = g's channel 16xb + 4g + r;
+//  * dz = dZ + RES·g on 16x16x32 bf16 splits (round 5; 16 f32 16x16x4 MFMAs before): A row i of
+//    block b = z channel ch16(b, i) from the RX image, k = 8g + e = g's channel 16(e >> 2) + 4g +
+//    (e & 3), i.e. the lane's two N-layout g registers split as they are;
 //  * dx = W·dv on 16x16x32 bf16 splits, k-step S = sig / gate: the lane's 8 dv values of kind S
 //    (Zl blocks 0, 1) are exactly the backward image's k order kk = 32S + 8g + e (WD unchanged);
 //  * dSIG / dGATE: wave w takes weight-gradient tile w & 3 (2·kind + tap) over positions
@@ -2372,7 +2401,7 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 // LDS rows: Xp / Xc / ZT unpadded (LDS-DMA), DVs / DVg / G / OC padded to XS = 36 floats (the
 // b128 own-row writes of 16 consecutive rows fall on 16 distinct bank groups).
 template <int NW>
-constexpr int cb16_lds() { return BIMG_F + 3 * 16 * NW * 32 + 4 * 16 * NW * XS + 8 * 96; }
+constexpr int cb16_lds() { return B16IMG_F + 3 * 16 * NW * 32 + 4 * 16 * NW * XS + 8 * 96; }
 static_assert(cb16_lds<8>() * 4 + 16 <= 160 * 1024, "chain bwd16 LDS");
 static_assert(4 * 1280 <= 3 * 128 * 32, "bwd16: the partial scratch (waves 4-7) must fit in Xp | Xc | ZT");
 
@@ -2404,8 +2433,8 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
   __shared__ int s_fail;
   float* IMG = sm;
   const unsigned short* WD = (const unsigned short*)IMG;
-  const float* Rs = IMG + BD_US / 2;
-  float* Xp = IMG + BIMG_F;
+  const unsigned short* RX = WD + BD_US;
+  float* Xp = IMG + B16IMG_F;
   float* Xc = Xp + TP * 32;
   float* ZT = Xc + TP * 32;
   float* DVs = ZT + TP * 32;
@@ -2453,7 +2482,7 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
     };
     auto dma_image = [&](int l) {
       const float* src = a.bimg + (long)l * BIMG_F + lane * 4;
-      for (int i = w; i < BIMG_F / 256; i += NW) dma16(src + i * 256, IMG + i * 256);
+      for (int i = w; i < B16IMG_F / 256; i += NW) dma16(src + (i < BD_PC ? i : i - BD_PC + RX_GPC) * 256, IMG + i * 256);
     };
     __syncthreads();  // previous tile's LDS use done
     dma_image(a.L - 1);
@@ -2516,27 +2545,22 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         gv[xb] = v;
         *(floatx4*)gp = v;
       }
-      // 2. dz = dZ + RES·g  (f32 MFMA 16x16x4: k = g's channel 16xb + 4g + rr)
+      // 2. dz = dZ + RES·g on the bf16 cores: one 32-deep k-step of six split products per block
+      //    bb (A row i = z channel ch16(bb, i) of RX, k = 8g + e = the lane's g registers in order)
       floatx4 dz[2];
       {
-        floatx4 rx[2][2];
+        bf16x8 gb[3];
+        split8(gv[0], gv[1], gb);
 #pragma unroll
-        for (int bb = 0; bb < 2; ++bb)
+        for (int bb = 0; bb < 2; ++bb) {
+          bf16x8 rx[3];
 #pragma unroll
-          for (int xb = 0; xb < 2; ++xb) rx[bb][xb] = *(const floatx4*)(Rs + ch16(bb, i16) * XS + 16 * xb + 4 * g);
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb) dz[bb] = valid ? dzr[bb] : floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int xb = 0; xb < 2; ++xb) {
-#pragma unroll
-          for (int rr = 0; rr < 4; ++rr)
-#pragma unroll
-            for (int bb = 0; bb < 2; ++bb)
-              dz[bb] = __builtin_amdgcn_mfma_f32_16x16x4f32(rx[bb][xb][rr], gv[xb][rr], dz[bb], 0, 0, 0);
+          for (int p = 0; p < 3; ++p) rx[p] = *(const bf16x8*)(RX + ch16(bb, i16) * RX_ROW + 32 * p + 8 * g);
+          dz[bb] = mfma16x3(rx, gb, valid ? dzr[bb] : floatx4{0.f, 0.f, 0.f, 0.f});
           // x / z rows of this layer: pieces k = w, w + NW, ... (3·TP/8 rows of 8 over the block)
 #pragma unroll
           for (int k2 = 0; k2 < TP / 8 / NW / 2 + 1; ++k2) {
-            const int k = w + NW * (2 * k2 + xb);
+            const int k = w + NW * (2 * k2 + bb);
             if (k < TP / 8) dma_rows3(k);
           }
         }

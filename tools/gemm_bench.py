@@ -35,11 +35,16 @@ def timeit(fn, reps=20):
     return s.elapsed_time(e) / reps * 1e-3
 
 
-only = os.environ.get('GEMM_ONLY')
+# GEMM_KSCAN=1: the post1 shape (N = 512, pre-split B) at K = 128 .. 2048 -- time against K separates
+# the per-tile fixed cost (prologue fill, epilogue) from the k-loop
+SHAPES += [('kscan%d' % k, M, 512, k, 1, 0, 1) for k in (128, 256, 512, 1024, 1600, 2048)]
+only = os.environ.get('GEMM_ONLY') or ('kscan' if os.environ.get('GEMM_KSCAN') else None)
 splits = os.environ.get('GEMM_SPLITS')   # e.g. "4,9,16": every listed split-K for the selected shapes
 runs = [(s[0], s[1], s[2], s[3], s[4], s[5], int(x)) for s in SHAPES for x in splits.split(',')] if splits else SHAPES
 for name, m, n, k, akc, bkc, split in runs:
-    if only and name not in only.split(','):
+    if only and name not in only.split(',') and not (only == 'kscan' and name.startswith('kscan')):
+        continue
+    if not only and name.startswith('kscan'):
         continue
     A = torch.randn(m, k, device='cuda') if akc else torch.randn(k, m, device='cuda')
     B = torch.randn(n, k, device='cuda') if bkc else torch.randn(k, n, device='cuda')
