@@ -1067,6 +1067,12 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
   constexpr bool DMAIMG = LC;
   // per-wave halo (below)
   constexpr bool WH = true;
+  // LC form: the LC term of layer l+1 (72 MFMAs per wave) runs after layer l's publish instead of
+  // inside its store drain, where it outlasted the drain and held the publish back; its image is
+  // DMA'd during layer l (after the dilated tap: ahead of the halo loads it would have held their
+  // vmcnt waits) into the single LCI buffer, which nothing reads between layer l's top barrier and
+  // its publish barrier
+  constexpr bool LCLATE = LC;
   constexpr int PF = DMAIMG ? 1 : (IMGF / 4 + NT - 1) / NT;   // float4 per thread to prefetch one image
   constexpr int NR = TP * 8 / NT;                       // float4 per thread of a TP-row tile (2)
   __shared__ __attribute__((aligned(16))) float sm[cf16_lds<NW>(LC)];
@@ -1250,6 +1256,7 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
         }
         conv16_tap_x<LC ? 2 : 1>(x0, x1, (const unsigned short*)Wl, i16, g, acc);
         if (LC) read_rf();
+        if (LCLATE && l > 0 && l + 1 < a.L) dma_lc16_image<NW>(a.lcimg, l + 1, LCI, w, lane);
       } else {
         const float* xp = (r >= d) ? cur + (r - d) * XS : HALO + r * XS;
         conv16_tap<LC ? 2 : 1>(xp, (const unsigned short*)Wl, i16, g, acc);
@@ -1313,7 +1320,7 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
         conv16_init(bias_of(Wn), cv, q0, h, acc);
         if (has_cond && l + 2 < a.L) load_cond16<CM>(a, l + 2, myid, m, valid, q0, h, cv);
         conv16_tap<LC ? 2 : 1>(nrow, (const unsigned short*)Wn + 96, i16, g, acc);
-        if (LC) lc16_terms(LCIu, lcv, i16, g, acc);
+        if (LC && !LCLATE) lc16_terms(LCIu, lcv, i16, g, acc);
       }
       FSTAMP(5);
       // publish x_{l+1}: every wave drains its stores, barrier, one lane signals
@@ -1322,13 +1329,15 @@ __global__ __launch_bounds__(64 * NW) void chain_fwd16_kernel(ChainFK a) {
       __syncthreads();
       FSTAMP(10);
       if (tid == 0 && l + 1 < a.L) publish_flag(a.flags + tile, (unsigned)(l + 1));
-      if (LC && l + 2 < a.L) dma_lc16_image<NW>(a.lcimg, l + 2, LCI, w, lane);
+      if (LC && !LCLATE && l + 2 < a.L) dma_lc16_image<NW>(a.lcimg, l + 2, LCI, w, lane);
       if (DMAIMG && l + 2 < a.L) {
         const float* src = wsrc + (long)(l + 2) * IMGF + lane * 4;
         float* dst = IMG0 + (l & 1) * IMGF;
 #pragma unroll
         for (int i = 0; i < IMGF / 256 / NW; ++i) dma16(src + (w + NW * i) * 256, dst + (w + NW * i) * 256);
       }
+      // (LCLATE) the LC image of layer l+1 landed by the drain before the barrier above
+      if (LCLATE && l + 1 < a.L) lc16_terms(LCIu, lcv, i16, g, acc);
       if (!DMAIMG && l + 2 < a.L) {
         float* dst = IMG0 + (l & 1) * IMGF;
 #pragma unroll
