@@ -198,7 +198,11 @@ LBWN_DEV float dot4f(floatx4 a, floatx4 b, float c) {
   return fmaf(a[3], b[3], c);
 }
 
-// Forward: LDS = W (the stage's filter, [s·Lo][I + 4]) | two row buffers [R][Lo + 4]
+// Forward: LDS = W (the stage's filter, [s·Lo][I + 4]) | two row buffers [R][Lo + 4].
+// SC > 0: every stage's stride is SC (arch5: 4, 4, 4, 4), so the j loop has no runtime guard: with
+// `if (j < s)` each j's filter read sat in its own basic block behind an `s_waitcnt vmcnt(0)
+// lgkmcnt(0)`, one exposed LDS round trip (and store drain) per j and k-step.
+template <int SC>
 __global__ __launch_bounds__(UP_THREADS) void lc_up_fwd_kernel(UpK a) {
   __shared__ __attribute__((aligned(16))) float sm[UP_LDS];
   const int f = blockIdx.x, tid = threadIdx.x, Lo = a.Lo, LP = Lo + 4;
@@ -209,35 +213,52 @@ __global__ __launch_bounds__(UP_THREADS) void lc_up_fwd_kernel(UpK a) {
     if (i + 1 < a.nup) last_in *= a.s[i];
   }
   float* W = sm;
-  float* buf[2] = {sm + maxw, sm + maxw + last_in * LP};
-  float* in = buf[0];
-  up_load_tile(in, a.mel + (long)f * a.Li, 1, a.Li, tid);   // stage 0 input: the mel frame (row stride Li + 4)
+  // the two row buffers by offset from the LDS array (a pointer table indexed at run time lost
+  // the address space: the x reads became flat loads, each k-step waiting on vmcnt(0) behind the
+  // block's outstanding global stores)
+  const int ob0 = maxw, ob1 = maxw + last_in * LP;
+  int in_off = ob0;
+  up_load_tile(sm + in_off, a.mel + (long)f * a.Li, 1, a.Li, tid);   // stage 0 input: the mel frame (row stride Li + 4)
   int IP = a.Li + 4;
+  constexpr int NJ = SC ? SC : UP_MAXS;
   for (int i = 0; i < a.nup; ++i) {
-    const int s = a.s[i], N = s * Lo;
+    const int s = SC ? SC : a.s[i], N = s * Lo;
     up_load_rows(W, a.F[i], 0, N, I, tid);
     __syncthreads();
-    float* out = buf[(i + 1) & 1];
+    const int out_off = ((i + 1) & 1) ? ob1 : ob0;
+    const float* in = sm + in_off;
+    float* out = sm + out_off;
     const bool keep = i + 1 < a.nup;
     float* g = a.act[i] + (long)f * R * s * Lo;
     const int RT = (R + 3) / 4;
     for (int w = tid; w < Lo * RT; w += UP_THREADS) {
       const int o = w % Lo, rt = w / Lo;
-      float acc[4][UP_MAXS];
+      float acc[4][NJ];
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
-        for (int j = 0; j < UP_MAXS; ++j) acc[ii][j] = 0.f;
+        for (int j = 0; j < NJ; ++j) acc[ii][j] = 0.f;
+#pragma unroll 2
       for (int k = 0; k < I; k += 4) {
         floatx4 x[4];
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii) x[ii] = *(const floatx4*)(in + min(4 * rt + ii, R - 1) * IP + k);
+        if (SC) {   // every filter read of the k-step issued before the FMAs
+          floatx4 wv[NJ];
 #pragma unroll
-        for (int j = 0; j < UP_MAXS; ++j) {
-          if (j < s) {
-            const floatx4 wv = *(const floatx4*)(W + (j * Lo + o) * (I + 4) + k);
+          for (int j = 0; j < NJ; ++j) wv[j] = *(const floatx4*)(W + (j * Lo + o) * (I + 4) + k);
 #pragma unroll
-            for (int ii = 0; ii < 4; ++ii) acc[ii][j] = dot4f(x[ii], wv, acc[ii][j]);
+          for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int ii = 0; ii < 4; ++ii) acc[ii][j] = dot4f(x[ii], wv[j], acc[ii][j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            if (j < s) {
+              const floatx4 wv = *(const floatx4*)(W + (j * Lo + o) * (I + 4) + k);
+#pragma unroll
+              for (int ii = 0; ii < 4; ++ii) acc[ii][j] = dot4f(x[ii], wv, acc[ii][j]);
+            }
           }
         }
       }
@@ -246,7 +267,7 @@ __global__ __launch_bounds__(UP_THREADS) void lc_up_fwd_kernel(UpK a) {
         const int t = 4 * rt + ii;
         if (t >= R) break;
 #pragma unroll
-        for (int j = 0; j < UP_MAXS; ++j) {
+        for (int j = 0; j < NJ; ++j) {
           if (j < s) {
             g[(long)(s * t + j) * Lo + o] = acc[ii][j];
             if (keep) out[(s * t + j) * LP + o] = acc[ii][j];
@@ -255,7 +276,7 @@ __global__ __launch_bounds__(UP_THREADS) void lc_up_fwd_kernel(UpK a) {
       }
     }
     __syncthreads();   // W and `in` are free; `out` is the next stage's input
-    in = out;
+    in_off = out_off;
     IP = LP;
     R *= s;
     I = Lo;
@@ -408,7 +429,10 @@ int lbwn_lc_up_fwd_launch(int nup, const int* s, int Li, int Lo, int frames, con
                           float* const* act, hipStream_t st) {
   LBWN_REQUIRE(lbwn_lc_up_fused_ok(nup, s, Li, Lo), "lc upsample: shape outside the fused kernel's envelope");
   UpK k = up_args(nup, s, Li, Lo, frames, mel, F, act);
-  lc_up_fwd_kernel<<<frames, UP_THREADS, 0, st>>>(k);
+  bool all4 = true;
+  for (int i = 0; i < nup; ++i) all4 = all4 && s[i] == 4;
+  if (all4) lc_up_fwd_kernel<4><<<frames, UP_THREADS, 0, st>>>(k);
+  else lc_up_fwd_kernel<0><<<frames, UP_THREADS, 0, st>>>(k);
   LBWN_CHECK_LAUNCH();
   return 0;
 }
