@@ -151,7 +151,8 @@ struct UpK {
   const float* mel;                  // [frames][Li]
   const float* F[4];                 // stage filters [s][Lo][I]
   float* act[4];                     // stage outputs, [frames·R_{i+1}][Lo]
-  const float* dlc;                  // backward: d(last stage output) [frames·hop][Lo]
+  const float* dlc;                  // backward: d(last stage output) [frames·hop][Lo], or its
+  int dlc_parts; long dlc_stride;    // dlc_parts split-K partials dlc_stride floats apart (summed here)
   float* dpart;                      // backward: per-frame filter-gradient partials [frames][Σ_i s_i·Lo·I_i]
   int nup, s[4], Li, Lo, frames;
 };
@@ -302,7 +303,16 @@ __global__ __launch_bounds__(UP_THREADS) void lc_up_bwd_kernel(UpK a) {
   float* DN = D + hop * LP;
   float* INB = DN + (hop / a.s[a.nup - 1]) * LP;
   float* W = INB + (hop / a.s[a.nup - 1]) * (Imax + 4);
-  up_load_tile(D, a.dlc + (long)f * hop * Lo, hop, Lo, tid);
+  {   // D = d(last stage output) rows of this frame: the dlc GEMM's split-K partials summed in order
+    const float* src = a.dlc + (long)f * hop * Lo;
+    const int C4 = Lo / 4, tot = hop * C4;
+    for (int e = tid; e < tot; e += UP_THREADS) {
+      const long off = (long)(e / C4) * Lo + 4 * (e % C4);
+      floatx4 v = *(const floatx4*)(src + off);
+      for (int z = 1; z < a.dlc_parts; ++z) v += *(const floatx4*)(src + z * a.dlc_stride + off);
+      *(floatx4*)(D + (e / C4) * LP + 4 * (e % C4)) = v;
+    }
+  }
   int R = hop;
   for (int i = a.nup - 1; i >= 0; --i) {
     const int s = a.s[i], I = i ? Lo : a.Li, IP = I + 4, N = s * Lo;
@@ -316,6 +326,7 @@ __global__ __launch_bounds__(UP_THREADS) void lc_up_bwd_kernel(UpK a) {
     for (int w = tid; w < (N / 4) * C4; w += UP_THREADS) {
       const int c4 = w % C4, n4 = w / C4, j = (4 * n4) / Lo, o = (4 * n4) % Lo;
       floatx4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll 4
       for (int t = 0; t < R; ++t) {
         const floatx4 dv = *(const floatx4*)(D + (s * t + j) * LP + o);
         const floatx4 xv = *(const floatx4*)(INB + t * IP + 4 * c4);
@@ -340,6 +351,7 @@ __global__ __launch_bounds__(UP_THREADS) void lc_up_bwd_kernel(UpK a) {
         const int w = tid + u * UP_THREADS;
         if (w >= nwork) break;
         const int c4 = w % C4, r2 = w / C4, t0 = 2 * r2, t1 = min(2 * r2 + 1, R - 1);
+#pragma unroll 2
         for (int o = 0; o < Lo; o += 4) {
           const floatx4 d0 = *(const floatx4*)(D + (s * t0 + j) * LP + o);
           const floatx4 d1 = *(const floatx4*)(D + (s * t1 + j) * LP + o);
@@ -439,10 +451,11 @@ int lbwn_lc_up_fwd_launch(int nup, const int* s, int Li, int Lo, int frames, con
 
 int lbwn_lc_up_bwd_launch(int nup, const int* s, int Li, int Lo, int frames, const float* mel, const float* const* F,
                           float* const* act, const float* dlc, float* dpart, float* const* dF, hipStream_t st,
-                          hipStream_t st_sum, hipEvent_t ev) {
+                          hipStream_t st_sum, hipEvent_t ev, int dlc_parts, long dlc_stride) {
   LBWN_REQUIRE(lbwn_lc_up_fused_ok(nup, s, Li, Lo), "lc upsample: shape outside the fused kernel's envelope");
   UpK k = up_args(nup, s, Li, Lo, frames, mel, F, act);
   k.dlc = dlc; k.dpart = dpart;
+  k.dlc_parts = std::max(dlc_parts, 1); k.dlc_stride = dlc_stride;
   lc_up_bwd_kernel<<<frames, UP_THREADS, 0, st>>>(k);
   LBWN_CHECK_LAUNCH();
   int ptot = 0;

@@ -55,6 +55,7 @@ struct lbwn_plan {
   int split_dlc, split_dlcx, split_dlct, split_up[8];
   size_t oSPLIT_AUX = 0;         // split-K workspace of the aux2 stream (LC / GC grads beside dSKIP)
   bool up_fused = false;         // LC upsample as one fused launch per direction (cond.hip)
+  int dlc_parts = 1;             // split-K partials the last dlc GEMM left for the fused upsample backward
   bool up_fused_bwd = false;     // ... for the backward (<= 256 mel frames; else per-stage GEMMs)
   size_t oUPPART = 0;            // its per-frame filter-gradient partials
   size_t total;
@@ -713,6 +714,10 @@ int lc_dlc(lbwn_plan* p, const lbwn_params* P, void* ws, float* spl, hipStream_t
     if ((e = lbwn_split_planes_launch(1, &w, &ld, &rows, &K, &tr, &o, st))) return e;
     g.b3 = o;
   }
+  // the fused upsample backward sums dlc's split-K partials as it loads them (no reduce launch
+  // between the two on the main stream); the per-stage path reads the reduced dlc
+  p->dlc_parts = 1;
+  if (p->up_fused_bwd) g.splits_deferred = &p->dlc_parts;
   Probe(p, st, "lc_dlc");
   if ((e = lbwn_gemm_launch(g, 1, 1, p->split_dlcx, spl, st))) return e;
   Probe::end(p, st, "lc_dlc");
@@ -728,8 +733,11 @@ int lc_upsample_bwd(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G, vo
     float* act[8];
     for (int i = 0; i < p->nup; ++i) { F[i] = P->lc_up[i]; act[i] = at<float>(ws, p->oLCACT[i]); }
     Probe(p, st, "lc_up_bwd");
-    e = lbwn_lc_up_bwd_launch(p->nup, p->up, p->Li, p->Lo, (int)(p->M / p->hop), mel, F, act, dout,
-                              at<float>(ws, p->oUPPART), G->lc_up, st, st_sum, p->ev_upb);
+    // dlc as the dlc GEMM left it: dlc_parts split-K partials in spl, or the product itself
+    const bool parts = p->dlc_parts > 1;
+    e = lbwn_lc_up_bwd_launch(p->nup, p->up, p->Li, p->Lo, (int)(p->M / p->hop), mel, F, act, parts ? spl : dout,
+                              at<float>(ws, p->oUPPART), G->lc_up, st, st_sum, p->ev_upb, p->dlc_parts,
+                              parts ? p->M * p->Lo : 0);
     Probe::end(p, st, "lc_up_bwd");
     return e;
   }

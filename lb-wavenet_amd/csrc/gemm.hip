@@ -1182,6 +1182,11 @@ int gemm_setup(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int& split
 }
 
 int splitk_finish(const lbwn_gemm_args& a, int split_k, const float* slab_ws, hipStream_t st) {
+  if (a.splits_deferred) {   // the consumer sums the partials itself (lc_up_bwd_kernel)
+    LBWN_REQUIRE(!a.bias && !a.relu_out && !a.mask && !a.accumulate, "gemm: deferred split-K needs a plain product");
+    *a.splits_deferred = split_k;
+    return 0;
+  }
   if (split_k > 1) {
     const long total = (long)a.M * (a.N / 4);
     int blocks = (int)std::min<long>((total + 255) / 256, 4096);

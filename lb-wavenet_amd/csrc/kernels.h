@@ -24,6 +24,8 @@ struct lbwn_gemm_args {
   // sg_off(m, c / 8, (c / 4) & 1) + c % 4 (layer.hip), so the chain's own-row loads are 1-KiB runs
   long c_chain_ls;
   int k_per_split;     // set by the launcher
+  int* splits_deferred;   // host, nullable: split-K partials left unsummed in the slab workspace
+                          // ([splits][M][N]); the launcher stores the split count here (1: C written)
   long split_stride;   // set by the launcher
   int xcd2d;           // gemm_x3q_kernel<10> (N % 160 == 0): the 2-D XCD blocking of its tiles (xcd2d_tile)
   // k-blocked operands (the backward chain's DV export, [K/32][Mp][32]): 0 = plain layout.
@@ -276,4 +278,5 @@ int lbwn_lc_up_fwd_launch(int nup, const int* s, int Li, int Lo, int frames, con
 // the per-frame pass on st; the frame-partial sum on st_sum (after ev, recorded on st, when they differ)
 int lbwn_lc_up_bwd_launch(int nup, const int* s, int Li, int Lo, int frames, const float* mel, const float* const* F,
                           float* const* act, const float* dlc, float* dpart, float* const* dF, hipStream_t st,
-                          hipStream_t st_sum = nullptr, hipEvent_t ev = nullptr);
+                          hipStream_t st_sum = nullptr, hipEvent_t ev = nullptr, int dlc_parts = 1,
+                          long dlc_stride = 0);
