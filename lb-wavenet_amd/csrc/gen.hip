@@ -973,8 +973,14 @@ LBWN_DEV void persist_head(const PersistK& a, int m, float* sm, int b0, int B, l
     if (tr && s == n - 1) tr[2] = wall_clock64();
     // B. gather the whole skip vector: thread k = tid polls column k of every stream
     if (tid < Cs) {
+      // as many granule loads per poll as the group has streams, in fours (a group of 10 polled
+      // 16 per thread before: 6 re-reads of its last stream)
       float v[P_MAXB];
-      sweep<P_MAXB>(a.sg, (unsigned)(b0 * Cs + tid), (unsigned)Cs, B, tag, v, a.status);
+      const unsigned o0 = (unsigned)(b0 * Cs + tid);
+      if (B <= 4) sweep<4>(a.sg, o0, (unsigned)Cs, B, tag, *reinterpret_cast<float(*)[4]>(v), a.status);
+      else if (B <= 8) sweep<8>(a.sg, o0, (unsigned)Cs, B, tag, *reinterpret_cast<float(*)[8]>(v), a.status);
+      else if (B <= 12) sweep<12>(a.sg, o0, (unsigned)Cs, B, tag, *reinterpret_cast<float(*)[12]>(v), a.status);
+      else sweep<P_MAXB>(a.sg, o0, (unsigned)Cs, B, tag, v, a.status);
       const float bs = a.bsum ? a.bsum[tid] : 0.f;
 #pragma unroll
       for (int bb = 0; bb < P_MAXB; ++bb)
