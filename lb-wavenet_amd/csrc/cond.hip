@@ -144,7 +144,7 @@ int grid_for(long n) { return (int)std::min<long>((n + 255) / 256, 4096); }
 // direction instead of a (split-K) GEMM per stage and direction (arch5 B = 8: 4 + 9 launches of
 // 20-40 µs each, latency-bound).  f32 FMA, 4 x s / 4 x 4 / 2 x 4 register micro-tiles over LDS
 // operands (b128 reads, filter rows padded to I + 4 floats: conflict-free).
-constexpr int UP_THREADS = 512;
+constexpr int UP_THREADS = 1024;   // 16 waves: the stages are LDS-latency bound at one block per CU
 constexpr int UP_MAXS = 8;           // stride per stage
 constexpr int UP_LDS = 40448;        // floats (158 KiB)
 struct UpK {
