@@ -51,13 +51,14 @@ def chain_forms():
 
 def chain_ceiling(name, arch, x3):
     """Peak of the arithmetic the chain kernel actually runs (f32-equivalent FLOP/s), per
-    algorithmic FLOP: in the bf16-split build the backward chain (either form) does dx and
-    dSIG/dGATE (16·Cr·Cd per position and layer) as split products and dz, dRES (4·Cr·Cd) on the
-    f32 MFMA; the forward chain does its conv and residual (10·Cr·Cd) as split products."""
+    algorithmic FLOP: in the bf16-split build the backward chain (chain_bwd16_kernel, the default
+    form) does dx, dSIG/dGATE and, since round 5, dz (18·Cr·Cd per position and layer) as split
+    products and dRES (2·Cr·Cd) on the f32 MFMA (358 TF; 313 TF while dz was on the f32 MFMA too);
+    the forward chain does its conv and residual (10·Cr·Cd) as split products."""
     if not x3:
         return FP32_MFMA_PEAK
     if name == 'layer_bwd':
-        return 20.0 / (16.0 / X3_PEAK + 4.0 / FP32_MFMA_PEAK)
+        return 20.0 / (18.0 / X3_PEAK + 2.0 / FP32_MFMA_PEAK)
     return X3_PEAK
 
 
@@ -441,7 +442,7 @@ class TrainBench:
                'traffic': traffic_from_profiles(name, traffic if isinstance(traffic, str) else None) if traffic else None,
                'mfma_busy': mfma_from_profiles(name, traffic if isinstance(traffic, str) else None) if traffic else None}
         if bound == 'mfma':
-            out['arith'] = ('bf16-split (6 products) for dx and dSIG/dGATE, f32 MFMA for dz and dRES'
+            out['arith'] = ('bf16-split (6 products) for dx, dz and dSIG/dGATE, f32 MFMA for dRES'
                             if x3 and name == 'layer_bwd' else ('bf16-split' if x3 else 'f32 MFMA'))
             out['frac_of_f32_peak'] = ach / FP32_MFMA_PEAK
         if name == 'layer_fwd':
