@@ -106,6 +106,11 @@ def kernel_work(name, arch, M):
         # (The gate recompute and the weight-gradient products the chain also does are not
         # counted: algorithmic work only.)
         return 'mfma', 20.0 * M * Cr * Cd * L
+    if name == 'layer_wgrad':
+        # the residual stack's weight gradients over the backward chain's exports (LBWN_BWD_WGRAD=1):
+        # per layer and position x_l (Cr; the dilated tap re-read from cache), z (Cd), dv (2 Cd)
+        # and G (Cr) read once
+        return 'hbm', 4.0 * M * (2 * Cr + 3 * Cd) * L
     if name == 'layer_fwd':
         # the whole residual stack (persistent chain launch, or the span of the L per-layer
         # launches): per layer and position x_l in (Cr), x_{l+1} out (Cr), z out (Cd); the
@@ -538,7 +543,16 @@ def chain_dilation_sweep(arch_file, B, T, dp, steps=4, gc=None, tile=None):
 DEFAULT_TILE = '128'    # the library's default chain form (engine.cpp, LBWN_CHAIN_TILE unset)
 
 
-CANDS = ['layer_bwd', 'dskip', 'layer_fwd', 'post1_fwd', 'dpost1', 'ds', 'post2_fwd', 'dpost2', 'dh']
+def wgrad_out():
+    """The plans of this process take the residual stack's weight gradients out of the backward
+    chain (LBWN_BWD_WGRAD, read at plan creation, engine.cpp; default: in the chain)."""
+    return os.environ.get('LBWN_BWD_WGRAD', '0') == '1'
+
+
+def cands():
+    """Launches probed during warmup (one per warmup step) to find the dominant kernel."""
+    wg = ['layer_wgrad'] if wgrad_out() else []
+    return ['layer_bwd'] + wg + ['dskip', 'layer_fwd', 'post1_fwd', 'dpost1', 'ds', 'post2_fwd', 'dpost2', 'dh']
 
 
 def sub_bench(arch_file, B, T, dp, steps, warmup, gc=None, backward=True, label='', traffic_tag=None):
@@ -546,7 +560,7 @@ def sub_bench(arch_file, B, T, dp, steps, warmup, gc=None, backward=True, label=
     from lbwn.arch import load_arch
     arch = load_arch(arch_file, num_global_cond=gc)
     tb = TrainBench(arch, B, T, dp, backward=backward)
-    ms, dom, samples, warm_t = tb.run(steps, warmup, probes=CANDS if backward else None)
+    ms, dom, samples, warm_t = tb.run(steps, warmup, probes=cands() if backward else None)
     out = {'workload': label, 'arch': os.path.basename(arch_file), 'batch_per_gpu': B, 'slice_sz': T,
            'value': dp.world * B * T / (ms / 1000.0), 'unit': 'audio samples/s', 'ms_per_step': ms,
            'steps': steps, 'warmup': warmup}
@@ -669,7 +683,7 @@ def main(argv=None):
     B, T = args.batch, args.slice
     tb = TrainBench(arch, B, T, dp)
     net = tb.net
-    ms, dom, samples, warm_t = tb.run(args.steps, args.warmup, probes=CANDS, probe_mode=args.probe)
+    ms, dom, samples, warm_t = tb.run(args.steps, args.warmup, probes=cands(), probe_mode=args.probe)
     value = world * B * T / (ms / 1000.0)
     cid = {'arch3.json': 'C2' + (' per GPU' if world > 1 else ''),
            'arch5.json': 'C5' if B == 8 and world > 1 else 'arch5'}.get(os.path.basename(arch_file), 'custom')

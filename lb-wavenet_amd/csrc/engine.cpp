@@ -48,6 +48,11 @@ struct lbwn_plan {
   size_t oGCTAB, oGCD, oGCPART, oLCACT[8], oCOND, oDVALL, oLCCAT, oDLCCAT, oDLC[2];
   size_t oLCCAT3 = 0;   // LCcat pre-split into bf16 planes (dlc's B; 0 = not used: K % 32 != 0)
   size_t oTGID = 0;              // GC + chain: per-tile uniform voice id (lbwn_gc_tile_sum_launch)
+  // Residual-stack weight gradients outside the backward chain (LBWN_BWD_WGRAD=1, round 6): the
+  // chain exports DV (oDVALL, k-blocked) and G = dx_{l+1} rows (oGX [L][m32(M)][32]);
+  // layer_wgrad_kernel sums them per layer into the slab (oGCS: GC per-tile dv sums)
+  bool wg_out = false;
+  size_t oGX = 0, oGCS = 0;
   // in-chain LC (bf16-split forward chain): L split LC images; COND is then computed only when a
   // backward path needs it (cond_valid: this step's COND is in the workspace)
   size_t oLCX = 0;
@@ -347,6 +352,10 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     // launch); LBWN_DZ_XCD=0 keeps the 1-D remap.  Placement only: bitwise the same results.
     const char* dv = getenv("LBWN_DZ_XCD");
     p->dz_xcd2d = (dv && dv[0] == '0') ? 0 : 1;
+    // weight gradients of the residual stack: inside the backward chain (0) or by
+    // layer_wgrad_kernel over the chain's exports (1; 16-position backward on 128-position tiles)
+    const char* wv = getenv("LBWN_BWD_WGRAD");
+    p->wg_out = (wv && wv[0] == '1') && bwd_nw == 8;
   }
   p->Li = a->n_lc_in;
   p->nup = a->n_lc_out > 0 ? a->n_lc_upsample : 0;
@@ -449,7 +458,12 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     // 10.56-10.57)
     p->up_fused_bwd = p->up_fused && M / hop <= 256;
     if (p->up_fused) p->oUPPART = carve(cur, f * (size_t)lbwn_lc_up_part_floats(p->nup, p->up, p->Li, p->Lo, (int)(M / hop)));
-    p->oDVALL = p->Lo ? carve(cur, f * (size_t)m32(M) * ncond) : 0;   // rows or [2L][m32(M)][32]
+    // rows or [2L][m32(M)][32]; also the export form's DV
+    p->oDVALL = (p->Lo || (p->chain && p->wg_out)) ? carve(cur, f * (size_t)m32(M) * ncond) : 0;
+    if (p->chain && p->wg_out) {
+      p->oGX = carve(cur, f * (size_t)L * m32(M) * 32);
+      p->oGCS = p->Ge ? carve(cur, f * (size_t)L * B * ((T + 127) / 128) * 64) : 0;
+    }
     p->oLCCAT = p->Lo ? carve(cur, f * (size_t)p->Lo * ncond) : 0;
     if (p->Lo && ncond % 32 == 0)
       p->oLCCAT3 = carve(cur, sizeof(unsigned short) * lbwn_split_planes_elems(p->Lo, (int)ncond));
@@ -1126,10 +1140,17 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
       if (cd.gc_dtab) c.tile_gid = at<int>(ws, p->oTGID);
       if (cd.dv_out) c.dvks = m32(M) * 32;   // DV k-blocked: contiguous GEMM k-steps for dlc / dLCcat
     }
-    p->dv_blk = c.dvks != 0;
     c.slab = SLABS; c.ocg = at<float>(ws, p->oOCG); c.ocls = M * 32;
     c.gc_tab = cd.gc_tab; c.gc_ld = cd.gc_ld; c.cond = cd.cond; c.ldcond = cd.ldcond;
     c.gc_dtab = cd.gc_dtab; c.dv_out = cd.dv_out; c.lddv = cd.ldcond;
+    // export form: the weight gradients come from layer_wgrad_kernel below
+    const bool wgo = b16 && p->wg_out && p->bwd_nw == 8;
+    if (wgo) {
+      c.dv_out = at<float>(ws, p->oDVALL); c.lddv = 2L * L * Cd; c.dvks = m32(M) * 32;
+      c.gx = at<float>(ws, p->oGX); c.gxls = m32(M) * 32;
+      c.tile_gid = nullptr;
+    }
+    p->dv_blk = c.dvks != 0;
     c.dx0_a = at<float>(ws, p->oGA[0]); c.dx0_c = at<float>(ws, p->oGC0[0]);
     c.flags = at<unsigned>(ws, p->oFLAGS + p->nflag_bytes); c.status = at<unsigned>(ws, p->oSTATUS);
     c.xcd = p->chain_xcd;
@@ -1141,6 +1162,24 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     Probe(p, st, "layer_bwd");
     if ((e = lbwn_chain_bwd_launch(c, st))) return e;
     Probe::end(p, st, "layer_bwd");
+    int wg_parts = ntiles;   // slab partials per layer
+    if (wgo) {
+      lbwn_wgrad_args wa;
+      memset(&wa, 0, sizeof(wa));
+      wa.X = X; wa.xls = p->x_layer_stride; wa.Z = Z; wa.lddz = ldz;
+      wa.DV = c.dv_out; wa.dvks = c.dvks; wa.GX = c.gx; wa.gxls = c.gxls;
+      wa.slab = SLABS; wa.stride = sstr;
+      if (cd.gc_dtab) {
+        wa.ids = ids; wa.tile_gid = at<int>(ws, p->oTGID); wa.gcs = at<float>(ws, p->oGCS);
+        wa.gtab = cd.gc_dtab; wa.gc_ld = cd.gc_ld;
+      }
+      wa.B = B; wa.T = T; wa.H = p->H; wa.L = L; wa.nbl = p->nbl;
+      wa.tpc = lbwn_layer_wgrad_tiles_per_chunk(ntiles, L, p->ncu);
+      wg_parts = (ntiles + wa.tpc - 1) / wa.tpc;
+      Probe(p, st, "layer_wgrad");
+      if ((e = lbwn_layer_wgrad_launch(wa, st))) return e;
+      Probe::end(p, st, "layer_wgrad");
+    }
     // slab reduction + dPRE on the second side stream (HBM-bound, beside dSKIP's MFMA work)
     hipStream_t rst = st;
     if (p->aux2) {
@@ -1150,7 +1189,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
       p->bwd_chain_event = true;
     }
     lbwn_layer_red_args r;
-    r.slab = SLABS; r.nparts = ntiles; r.stride = sstr; r.Cr = Cr; r.Cd = Cd;
+    r.slab = SLABS; r.nparts = wg_parts; r.stride = sstr; r.Cr = Cr; r.Cd = Cd;
     r.dsig = G->sig; r.dgate = G->gate; r.dres = G->res;
     r.dbsig = G->sig_b; r.dbgate = G->gate_b; r.dbres = G->res_b;
     // Side stream (the higher priority), beside the main stream's dlc (LC archs) and dSKIP:
@@ -1176,9 +1215,13 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
                                   G->pre_b, at<float>(ws, p->oSPLIT2), rst)))
       return e;
     Probe(p, rst, "layer_reduce");
-    if ((e = lbwn_layer_reduce_all_launch(r, L, (long)ntiles * sstr, rst))) return e;
+    if ((e = lbwn_layer_reduce_all_launch(r, L, (long)wg_parts * sstr, rst))) return e;
     Probe::end(p, rst, "layer_reduce");
     if (c.tile_gid && (e = lbwn_gc_tile_sum_launch(SLABS, L, ntiles, c.tile_gid, cd.gc_dtab, cd.gc_ld, p->ncat1, rst)))
+      return e;
+    if (wgo && cd.gc_dtab &&
+        (e = lbwn_gc_tile_sum_rows_launch(at<float>(ws, p->oGCS), L, ntiles, at<int>(ws, p->oTGID), cd.gc_dtab,
+                                          cd.gc_ld, p->ncat1, rst)))
       return e;
     if ((e = gc_backward(p, P, G, ws, rst))) return e;
     // main stream: dlc, the LC upsample backward (it needs dlc), [dLCcat,] then dSKIP below

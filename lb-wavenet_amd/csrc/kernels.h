@@ -191,6 +191,7 @@ struct lbwn_chain_args {
   float* SG = nullptr; long sgls = 0;
   const float* bimg = nullptr;
   int* tile_gid = nullptr;     // x3 backward + GC: [ntiles] uniform voice id per tile or -1
+  float* gx = nullptr; long gxls = 0;   // chain_bwd16_kernel export form: G rows [L][Mp][32] (+ dv_out, dvks)
   // forward, bf16-split form: in-chain LC term (instead of cond): LC input [M][Lo], split images
   const float* lcact = nullptr; const unsigned short* lcimg = nullptr; int Lo = 0;
   int fwd_nw = 0;              // forward form (lbwn_chain_fwd_tile); lcimg in the matching layout
@@ -201,6 +202,20 @@ struct lbwn_chain_args {
 int lbwn_chain_fwd_launch(const lbwn_chain_args& c, hipStream_t st);
 int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st);
 int lbwn_layer_reduce_all_launch(const lbwn_layer_red_args& r, int L, long slab_layer, hipStream_t st);
+// residual-stack weight-gradient partials from the backward chain's exports (layer_wgrad_kernel):
+// slab [L][nchunk][stride] for lbwn_layer_reduce_all_launch (nparts = nchunk); GC (gcs non-null):
+// tile ids + per-tile dv column sums [L][ntiles][64] for lbwn_gc_tile_sum_rows_launch
+struct lbwn_wgrad_args {
+  const float* X; long xls; const float* Z; long lddz;
+  const float* DV; long dvks; const float* GX; long gxls;
+  float* slab; long stride;
+  const int* ids; int* tile_gid; float* gcs; float* gtab; long gc_ld;
+  int B, T, H, L, nbl, tpc;
+};
+int lbwn_layer_wgrad_tiles_per_chunk(int ntiles, int L, int ncu);
+int lbwn_layer_wgrad_launch(const lbwn_wgrad_args& g, hipStream_t st);
+int lbwn_gc_tile_sum_rows_launch(const float* gcs, int L, int ntiles, const int* tile_gid, float* gtab, long ld,
+                                 int ncat1, hipStream_t st);
 int lbwn_chain_fwd_lds_bytes();
 
 // D-separation state transfer for ALL layers at once.

@@ -1432,6 +1432,7 @@ struct ChainBK {
   // bf16-split form (chain_bwd_x3_kernel): z rows (row stride lddz), σ rows [L][M][32], images
   const float* Zf; const float* SG; long sgls; const float* bimg;
   int* tile_gid;               // GC: per tile its uniform voice id or -1 (x3 chain), or null
+  float* gx; long gxls;        // chain_bwd16_kernel<.., false>: G export [L][Mp][32] (layer stride gxls)
 };
 
 // dv rows of wave w's 32 positions (DV, position-major) scatter-added into the GC gradient
@@ -2409,8 +2410,15 @@ __global__ __launch_bounds__(256) void chain_bwd_x3_kernel(ChainBK a) {
 //    two halves' partials are summed through LDS by waves 0-3.
 // LDS rows: Xp / Xc / ZT unpadded (LDS-DMA), DVs / DVg / G / OC padded to XS = 36 floats (the
 // b128 own-row writes of 16 consecutive rows fall on 16 distinct bank groups).
+// WG = false (round 6): the weight gradients leave the chain.  Per layer a tile runs only the
+// dependent path (G build, dz / dv, dx, publish) and exports the rows the weight gradients need:
+// DV (k-blocked [2L][Mp][32], as the LC products read it) and G = dx_{l+1} ([L][Mp][32]);
+// layer_wgrad_kernel forms dSIG / dGATE / dRES / the biases (and the GC sums) from them over all
+// positions of a layer.  No x / z DMA, no slab, LDS = image + G + OC.
 template <int NW>
 constexpr int cb16_lds() { return B16IMG_F + 3 * 16 * NW * 32 + 4 * 16 * NW * XS + 8 * 96; }
+template <int NW>
+constexpr int cb16_lds_nowg() { return B16IMG_F + 2 * 16 * NW * XS; }
 static_assert(cb16_lds<8>() * 4 + 16 <= 160 * 1024, "chain bwd16 LDS");
 static_assert(4 * 1280 <= 3 * 128 * 32, "bwd16: the partial scratch (waves 4-7) must fit in Xp | Xc | ZT");
 
@@ -2434,21 +2442,22 @@ LBWN_DEV void gc_scatter16(float* gtab, long ld, const float* DVs, const float* 
   }
 }
 
-template <int NW, bool TR>
+template <int NW, bool TR, bool WG>
 __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
   constexpr int TP = 16 * NW, NT = 64 * NW, NH = NW / 4, PH = TP / NH;   // PH: positions per half
   constexpr int NR = TP * 8 / NT;                                        // float4 per thread of a tile (2)
-  __shared__ __attribute__((aligned(16))) float sm[cb16_lds<NW>()];
+  __shared__ __attribute__((aligned(16))) float sm[WG ? cb16_lds<NW>() : cb16_lds_nowg<NW>()];
   __shared__ int s_fail;
   float* IMG = sm;
   const unsigned short* WD = (const unsigned short*)IMG;
   const unsigned short* RX = WD + BD_US;
+  // WG: Xp | Xc | ZT | DVs | DVg | G | OC | part;  !WG: G | OC
   float* Xp = IMG + B16IMG_F;
   float* Xc = Xp + TP * 32;
   float* ZT = Xc + TP * 32;
   float* DVs = ZT + TP * 32;
   float* DVg = DVs + TP * XS;
-  float* G = DVg + TP * XS;
+  float* G = WG ? DVg + TP * XS : IMG + B16IMG_F;
   float* OC = G + TP * XS;
   float* part = OC + TP * XS;   // [8][96] bias partials
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -2465,14 +2474,15 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
     const bool valid = t < a.T;
     const long mb = (long)b * a.T, m = mb + t, mc = mb + min(t, a.T - 1);
     const long sb = (long)b * (a.H + a.T) * 32;
-    const int myid = (a.gc_tab && valid) ? a.ids[m] : 0;
-    const int tile_id = a.gc_tab ? a.ids[mb + t0] : 0;
-    const bool tile_uni = __syncthreads_and(!valid || myid == tile_id);
-    if (a.tile_gid && tid == 0) a.tile_gid[tile] = tile_uni ? tile_id : -1;
+    const int myid = (WG && a.gc_tab && valid) ? a.ids[m] : 0;
+    const int tile_id = (WG && a.gc_tab) ? a.ids[mb + t0] : 0;
+    // (!WG: the GC sums and tile ids come from layer_wgrad_kernel)
+    const bool tile_uni = WG ? __syncthreads_and(!valid || myid == tile_id) : true;
+    if (WG && a.tile_gid && tid == 0) a.tile_gid[tile] = tile_uni ? tile_id : -1;
     // this wave's id runs over its 16 positions (lanes j of the first group), -1 past T
     const int gc_pid = valid ? myid : -1;
-    const int gc_prev = __shfl(gc_pid, max(lane - 1, 0) & 15);
-    const unsigned gc_starts = (unsigned)(__ballot(g == 0 && (i16 == 0 || gc_pid != gc_prev)) & 0xffffull);
+    const int gc_prev = WG ? __shfl(gc_pid, max(lane - 1, 0) & 15) : 0;
+    const unsigned gc_starts = WG ? (unsigned)(__ballot(g == 0 && (i16 == 0 || gc_pid != gc_prev)) & 0xffffull) : 0u;
     // per-layer rows of this lane's position (Zl channels): dZ, z, σ, issued a layer ahead
     // (buffer loads: a per-layer scalar base and one 32-bit lane offset per array, instead of three
     // 64-bit lane addresses held across the layer loop; the launcher checks the byte ranges)
@@ -2552,7 +2562,12 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         floatx4 v = dn ? *(const floatx4*)gp : floatx4{0.f, 0.f, 0.f, 0.f};
         v += oa[xb];
         gv[xb] = v;
-        *(floatx4*)gp = v;
+        if (WG) *(floatx4*)gp = v;
+      }
+      if (!WG && valid) {   // G export for the weight gradients
+        float* gxo = a.gx + (long)l * a.gxls + m * 32;
+#pragma unroll
+        for (int xb = 0; xb < 2; ++xb) *(floatx4*)(gxo + 16 * xb + 4 * g) = gv[xb];
       }
       // 2. dz = dZ + RES·g on the bf16 cores: one 32-deep k-step of six split products per block
       //    bb (A row i = z channel ch16(bb, i) of RX, k = 8g + e = the lane's g registers in order)
@@ -2570,7 +2585,7 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
 #pragma unroll
           for (int k2 = 0; k2 < TP / 8 / NW / 2 + 1; ++k2) {
             const int k = w + NW * (2 * k2 + bb);
-            if (k < TP / 8) dma_rows3(k);
+            if (WG && k < TP / 8) dma_rows3(k);
           }
         }
       }
@@ -2593,14 +2608,18 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) {
           const int c = 8 * (q0 + bb) + 4 * h;
-          *(floatx4*)(DVs + r * XS + c) = dvs[bb];
-          *(floatx4*)(DVg + r * XS + c) = dvg[bb];
+          if (WG) {
+            *(floatx4*)(DVs + r * XS + c) = dvs[bb];
+            *(floatx4*)(DVg + r * XS + c) = dvg[bb];
+          }
           if (dvo) {
             *(floatx4*)(dvo + c) = dvs[bb];
             *(floatx4*)(dvo + dgo + c) = dvg[bb];
           }
         }
       }
+      // !WG: the next layer's dZ / z / σ rows now (this layer's are consumed)
+      if (!WG && l > 0) load_regs(l - 1);
       XSTAMP(2);
       // 4. dx on the bf16 cores: out_a = g + W1·dv, out_c0 = W0·dv (k-steps S = 0 sig, 1 gate)
       floatx4 acc_a[2] = {gv[0], gv[1]}, acc_c[2];
@@ -2648,6 +2667,32 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // DV, G, OC, Xp/Xc/ZT complete; the weight image is dead
       if (tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
+      if (!WG) {
+        XSTAMP(4);
+        if (l == 0) continue;
+        // the next layer's image (this layer's dx was its last reader), then the producer of the
+        // next layer's G rows: each wave polls its flag (lane 0) and loads its own rows, so no
+        // block barrier sits between the publish and the next layer's G build
+        dma_image(l - 1);
+        const int pn = tt + max(1, d / TP);
+        if (pn < tps) {
+          if (lane == 0 && !s_fail) {
+            if (!wait_flag_ge(a.flags + (long)b * tps + pn, (unsigned)(a.L - l), a.status, 2u)) s_fail = 1;
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
+        XSTAMP(5);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)l * a.ocls, (short)0, oc_bytes, BUF_DW3);
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int e = tid + NT * i, c4 = (e & 7) * 4;
+          const int ts = min(t0 + (e >> 3) + d, a.T - 1);
+          gl[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
+        }
+        XSTAMP(6);
+        continue;
+      }
       if (a.gc_dtab && !tile_uni) gc_scatter16(a.gc_dtab + (long)l * 64, a.gc_ld, DVs, DVg, w, lane, 32, gc_starts, gc_pid);
       XSTAMP(4);
       // 6. dSIG / dGATE tile t4 = w & 3 (2·kind + tap) over this wave's position half:
@@ -2817,6 +2862,217 @@ __global__ __launch_bounds__(256) void layer_reduce_all_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) tot += scratch[j * 32 + tid];
     slab_store(k, c, tot);
+  }
+}
+
+// ---- residual-stack weight gradients over all positions (round 6) --------------------------
+// layer_wgrad_kernel<GC>: block (chunk, l) sums, over the positions of tpc consecutive chain tiles
+// (128 positions each, tile = b·tps + tt as in the chains), the weight-gradient partials of layer
+// l that chain_bwd16_kernel<.., true> forms per tile inside the chain (tmodel.py:136-148 conv,
+// :171-184 residual, differentiated at :354-358):
+//   dSIG / dGATE[tap][in][o] = Σ_t x_l[t - (1-tap)·d][in] · dv_{sig|gate}[t][o],
+//   dRES[c][o] = Σ_t z_l[t][c] · G[t][o],  biases = Σ_t dv_sig, dv_gate, G,
+// from the rows the chain exported (DV k-blocked [2L][Mp][32], G [L][Mp][32]) and the forward's x
+// and z rows.  Products on 32x32x16 bf16 splits (six products, f32 accumulate),
+// k = 16 positions: lane (c = lane & 31, kh = lane >> 5) holds positions 8kh..8kh+7 of channel c
+// for both operands, loaded as scalars straight from the position-major rows (two 128-B runs per
+// instruction), the next k-step's 48 values in flight behind this one's MFMAs.  Wave w takes
+// tiles w, w + 4, ... of the chunk; the four waves' partials meet in LDS in a fixed order and the
+// block writes one slab partial [l][chunk][SLAB] in the layout layer_reduce_all_kernel reads.
+// GC: per tile, the wave tests the voice ids; a uniform tile's dv column sums go to gcs
+// [l][tile][64] for gc_tile_sum_kernel (deterministic), a mixed tile's runs are added to the GC
+// table with atomics, as the chains do.
+struct WgK {
+  const float* X; long xls;       // x_l rows [B][H+T][32] per layer
+  const float* Z; long lddz;      // z rows [M][L·32]
+  const float* DV; long dvks;     // [2L][Mp][32] (sig chunk 2l, gate chunk 2l+1)
+  const float* GX; long gxls;     // [L][Mp][32]
+  float* slab; long stride;       // [L][nchunk][stride]
+  const int* ids; int* tile_gid; float* gcs; float* gtab; long gc_ld;
+  int B, T, H, L, nbl, tps, ntiles, tpc, nchunk;
+};
+
+constexpr int WG_TPC_MAX = 64;   // tiles per chunk
+
+template <bool GC>
+__global__ __launch_bounds__(256, 2) void layer_wgrad_kernel(WgK a) {
+  __shared__ __attribute__((aligned(16))) float scr[3 * SLAB];
+  __shared__ int s_gid[WG_TPC_MAX];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, kh = lane >> 5;
+  const int l = blockIdx.y, ch = blockIdx.x;
+  const int d = 1 << (l % a.nbl);
+  const int tile_beg = ch * a.tpc + w, tile_end = min((ch + 1) * a.tpc, a.ntiles);
+  const int nsteps = tile_beg < tile_end ? (tile_end - tile_beg + 3) / 4 * 8 : 0;
+  // buffer resources: x[t] and x[t-d] share one lane offset (the tap's base is d rows lower), so
+  // do dv_sig, dv_gate and G (one offset per position, three bases)
+  const float* xl = a.X + (long)l * a.xls;
+  const __amdgpu_buffer_rsrc_t rxc = __builtin_amdgcn_make_buffer_rsrc((void*)xl, (short)0, 0x7fffffff, BUF_DW3);
+  const __amdgpu_buffer_rsrc_t rxp = __builtin_amdgcn_make_buffer_rsrc((void*)(xl - 32L * d), (short)0, 0x7fffffff, BUF_DW3);
+  const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void*)(a.Z + (long)l * 32), (short)0, 0x7fffffff, BUF_DW3);
+  const float* dvl = a.DV + 2L * l * a.dvks;
+  const __amdgpu_buffer_rsrc_t rvs = __builtin_amdgcn_make_buffer_rsrc((void*)dvl, (short)0, 0x7fffffff, BUF_DW3);
+  const __amdgpu_buffer_rsrc_t rvg = __builtin_amdgcn_make_buffer_rsrc((void*)(dvl + a.dvks), (short)0, 0x7fffffff, BUF_DW3);
+  const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc((void*)(a.GX + (long)l * a.gxls), (short)0, 0x7fffffff, BUF_DW3);
+  floatx16 acc[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[i][q] = 0.f;
+  float bsum[3] = {0.f, 0.f, 0.f};
+  // k-step j of this wave: tile tile_beg + 4(j >> 3), 16 positions from 16(j & 7); this lane's 8
+  // positions start at t; positions past T are loaded at row T-1 and their dv / G zeroed
+  auto pos = [&](int j, int& b, int& t) {
+    const int tile = tile_beg + 4 * (j >> 3);
+    b = tile / a.tps;
+    t = (tile - b * a.tps) * 128 + 16 * (j & 7) + 8 * kh;
+  };
+  auto load = [&](int j, float (&v)[6][8]) {
+    int b, t;
+    pos(j, b, t);
+    const int mrow = b * a.T, xoff = (b + 1) * a.H * 128;   // x row = m + (b+1)·H
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int m = mrow + min(t + e, a.T - 1);
+      const int om = (m * 32 + c) * 4;
+      v[0][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rxp, om, xoff, 0));
+      v[1][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rxc, om, xoff, 0));
+      v[2][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rz, (int)(((long)m * a.lddz + c) * 4), 0, 0));
+      v[3][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rvs, om, 0, 0));
+      v[4][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rvg, om, 0, 0));
+      v[5][e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, om, 0, 0));
+    }
+  };
+  float bt[3] = {0.f, 0.f, 0.f};   // column sums of dv_sig, dv_gate, G over the current tile
+  auto compute = [&](int j, float (&v)[6][8]) {
+    int b, t;
+    pos(j, b, t);
+    const int nv = a.T - t;   // valid positions of this lane's 8 (<= 0: none)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (e >= nv) v[3][e] = v[4][e] = v[5][e] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bt[0] += v[3][e];
+      bt[1] += v[4][e];
+      bt[2] += v[5][e];
+    }
+    bf16x8 fs[3], fg[3], fx[3];
+    split8(floatx4{v[3][0], v[3][1], v[3][2], v[3][3]}, floatx4{v[3][4], v[3][5], v[3][6], v[3][7]}, fs);
+    split8(floatx4{v[4][0], v[4][1], v[4][2], v[4][3]}, floatx4{v[4][4], v[4][5], v[4][6], v[4][7]}, fg);
+    split8(floatx4{v[0][0], v[0][1], v[0][2], v[0][3]}, floatx4{v[0][4], v[0][5], v[0][6], v[0][7]}, fx);
+    acc[0] = mfma_x3(fx, fs, acc[0]);
+    acc[2] = mfma_x3(fx, fg, acc[2]);
+    split8(floatx4{v[1][0], v[1][1], v[1][2], v[1][3]}, floatx4{v[1][4], v[1][5], v[1][6], v[1][7]}, fx);
+    acc[1] = mfma_x3(fx, fs, acc[1]);
+    acc[3] = mfma_x3(fx, fg, acc[3]);
+    split8(floatx4{v[2][0], v[2][1], v[2][2], v[2][3]}, floatx4{v[2][4], v[2][5], v[2][6], v[2][7]}, fx);
+    split8(floatx4{v[5][0], v[5][1], v[5][2], v[5][3]}, floatx4{v[5][4], v[5][5], v[5][6], v[5][7]}, fs);
+    acc[4] = mfma_x3(fx, fs, acc[4]);
+  };
+  // GC: every tile of this wave tested for one voice id before any row load is in flight (the
+  // wait for the ids is then not a wait for the prefetched rows); the id or -1 in s_gid
+  if (GC) {
+    for (int tile = tile_beg; tile < tile_end; tile += 4) {
+      const int b = tile / a.tps, t0 = (tile - b * a.tps) * 128;
+      const long mb = (long)b * a.T;
+      const int i0 = a.ids[mb + min(t0 + lane, a.T - 1)], i1 = a.ids[mb + min(t0 + 64 + lane, a.T - 1)];
+      const int id0 = __shfl(i0, 0);
+      const int gid = __all(i0 == id0 && i1 == id0) ? id0 : -1;
+      if (lane == 0) {
+        a.tile_gid[tile] = gid;
+        s_gid[tile - ch * a.tpc] = gid;
+      }
+    }
+  }
+  // the tile of k-step j is complete: its sums into the totals (and, one voice, to gcs)
+  auto close_tile = [&](int j) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) bsum[i] += bt[i];
+    if (GC) {   // every tile (no branch: gc_tile_sum reads only the one-voice tiles)
+      const int tile = tile_beg + 4 * (j >> 3);
+      const float g0 = bt[0] + __shfl_xor(bt[0], 32), g1 = bt[1] + __shfl_xor(bt[1], 32);
+      float* o = a.gcs + ((long)l * a.ntiles + tile) * 64 + c;
+      o[32 * kh] = kh ? g1 : g0;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) bt[i] = 0.f;
+  };
+  if (nsteps > 0) {
+    float va[6][8], vb[6][8];
+    load(0, va);
+    // a tile's 8 k-steps unrolled (a branch inside the k-step loop cost 112 spilled VGPRs); the
+    // next tile's first rows are in flight across the tile boundary; the last prefetch re-loads
+    for (int jb = 0; jb < nsteps; jb += 8) {
+#pragma unroll
+      for (int s2 = 0; s2 < 8; s2 += 2) {
+        load(jb + s2 + 1, vb);
+        compute(jb + s2, va);
+        load(min(jb + s2 + 2, nsteps - 1), va);
+        compute(jb + s2 + 1, vb);
+      }
+      close_tile(jb);
+    }
+  }
+  // GC, tiles of more than one voice (rare): one atomic per run of equal ids, lane = (column c,
+  // position half kh), dv re-read from the export
+  if (GC) {
+    for (int tile = tile_beg; tile < tile_end; tile += 4) {
+      if (s_gid[tile - ch * a.tpc] >= 0) continue;
+      const int b = tile / a.tps, t0 = (tile - b * a.tps) * 128 + 64 * kh;
+      const long mb = (long)b * a.T;
+      const float* dvs = dvl + c;
+      float s0 = 0.f, s1 = 0.f;
+      int cur = -1;
+      for (int p = 0; p < 64 && t0 + p < a.T; ++p) {
+        const long m = mb + t0 + p;
+        const int id = a.ids[m];
+        if (id != cur && cur >= 0) {
+          atomicAdd(a.gtab + (long)cur * a.gc_ld + (long)l * 64 + c, s0);
+          atomicAdd(a.gtab + (long)cur * a.gc_ld + (long)l * 64 + 32 + c, s1);
+          s0 = s1 = 0.f;
+        }
+        cur = id;
+        s0 += dvs[m * 32];
+        s1 += dvs[a.dvks + m * 32];
+      }
+      if (cur >= 0) {
+        atomicAdd(a.gtab + (long)cur * a.gc_ld + (long)l * 64 + c, s0);
+        atomicAdd(a.gtab + (long)cur * a.gc_ld + (long)l * 64 + 32 + c, s1);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) bsum[i] += __shfl_xor(bsum[i], 32);
+  // slab index of accumulator register q: tiles t4 = 2·kind + tap at t4·1024, dRES at 4096
+  if (w > 0) {
+    float* S = scr + (w - 1) * SLAB;
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) S[i * 1024 + acc_row(q, kh) * 32 + c] = acc[i][q];
+    if (kh == 0) {
+      S[5120 + c] = bsum[0];
+      S[5152 + c] = bsum[1];
+      S[5184 + c] = bsum[2];
+    }
+  }
+  __syncthreads();
+  if (w == 0) {
+    float* out = a.slab + ((long)l * a.nchunk + ch) * a.stride;
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int k = i * 1024 + acc_row(q, kh) * 32 + c;
+        out[k] = ((acc[i][q] + scr[k]) + scr[SLAB + k]) + scr[2 * SLAB + k];
+      }
+    if (kh == 0) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int k = 5120 + 32 * i + c;
+        out[k] = ((bsum[i] + scr[k]) + scr[SLAB + k]) + scr[2 * SLAB + k];
+      }
+    }
   }
 }
 
@@ -3328,12 +3584,19 @@ int lbwn_chain_bwd_launch(const lbwn_chain_args& c, hipStream_t st) {
   if (c.bwd_nw)   // 32-bit byte offsets of the per-lane row loads (chain_bwd16_kernel load_regs)
     LBWN_REQUIRE(c.dzls * 4 < 0x7fffffffL && c.sgls * 4 < 0x7fffffffL && (long)c.B * c.T * c.ldz * 4 < 0x7fffffffL,
                  "chain bwd: dZ / SG layer or z rows past 2 GiB");
+  k.gx = c.gx; k.gxls = c.gxls;
+  if (c.gx)   // weight gradients outside the chain (layer_wgrad_kernel): DV and G exported
+    LBWN_REQUIRE(c.bwd_nw == 8 && c.dv_out && c.dvks > 0 && c.gxls >= (long)c.B * c.T * 32,
+                 "chain bwd: the export form needs 8 waves and the k-blocked DV export");
   if (c.bwd_nw == 8) {
-    if (k.trace) chain_bwd16_kernel<8, true><<<c.grid, 512, 0, st>>>(k);
-    else chain_bwd16_kernel<8, false><<<c.grid, 512, 0, st>>>(k);
+    if (c.gx) {
+      if (k.trace) chain_bwd16_kernel<8, true, false><<<c.grid, 512, 0, st>>>(k);
+      else chain_bwd16_kernel<8, false, false><<<c.grid, 512, 0, st>>>(k);
+    } else if (k.trace) chain_bwd16_kernel<8, true, true><<<c.grid, 512, 0, st>>>(k);
+    else chain_bwd16_kernel<8, false, true><<<c.grid, 512, 0, st>>>(k);
   } else if (c.bwd_nw == 4) {
-    if (k.trace) chain_bwd16_kernel<4, true><<<c.grid, 256, 0, st>>>(k);
-    else chain_bwd16_kernel<4, false><<<c.grid, 256, 0, st>>>(k);
+    if (k.trace) chain_bwd16_kernel<4, true, true><<<c.grid, 256, 0, st>>>(k);
+    else chain_bwd16_kernel<4, false, true><<<c.grid, 256, 0, st>>>(k);
   } else if (x3 && k.trace) chain_bwd_x3_kernel<true><<<c.grid, 256, 0, st>>>(k);
   else if (x3) chain_bwd_x3_kernel<false><<<c.grid, 256, 0, st>>>(k);
   else chain_bwd_kernel<<<c.grid, 256, 0, st>>>(k);
@@ -3360,10 +3623,11 @@ namespace {
 // sums slab[l][tile][5120 + c].  Block = (layer, id), thread = column: the block scans the tile ids
 // 64 at a time (one per lane, ballot), then adds its matching tiles' partials in tile order
 // (deterministic; blocks of ids with no uniform tile only scan).
-__global__ __launch_bounds__(64) void gc_tile_sum_kernel(const float* __restrict__ slab, long slab_layer, int ntiles,
-                                                         const int* __restrict__ tile_gid, float* gtab, long ld) {
+__global__ __launch_bounds__(64) void gc_tile_sum_kernel(const float* __restrict__ slab, long slab_layer, long tstride,
+                                                         int ntiles, const int* __restrict__ tile_gid, float* gtab,
+                                                         long ld) {
   const int l = blockIdx.x, id = blockIdx.y, c = threadIdx.x;
-  const float* sl = slab + l * slab_layer + 5120 + c;
+  const float* sl = slab + l * slab_layer + c;
   float acc = 0.f;
   bool any = false;
   for (int t0 = 0; t0 < ntiles; t0 += 64) {
@@ -3373,7 +3637,7 @@ __global__ __launch_bounds__(64) void gc_tile_sum_kernel(const float* __restrict
     while (mask) {
       const int j = __ffsll((long long)mask) - 1;
       mask &= mask - 1;
-      acc += sl[(long)(t0 + j) * SLAB];
+      acc += sl[(long)(t0 + j) * tstride];
     }
   }
   if (any) gtab[(long)id * ld + (long)l * 64 + c] += acc;
@@ -3383,7 +3647,45 @@ __global__ __launch_bounds__(64) void gc_tile_sum_kernel(const float* __restrict
 int lbwn_gc_tile_sum_launch(const float* slab, int L, int ntiles, const int* tile_gid, float* gtab, long ld,
                             int ncat1, hipStream_t st) {
   LBWN_REQUIRE(ncat1 >= 1 && slab && tile_gid && gtab, "gc tile sums: bad arguments");
-  gc_tile_sum_kernel<<<dim3(L, ncat1), 64, 0, st>>>(slab, (long)ntiles * SLAB, ntiles, tile_gid, gtab, ld);
+  gc_tile_sum_kernel<<<dim3(L, ncat1), 64, 0, st>>>(slab + 5120, (long)ntiles * SLAB, SLAB, ntiles, tile_gid, gtab, ld);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_layer_wgrad_tiles_per_chunk(int ntiles, int L, int ncu) {
+  // about eight blocks of the grid per CU (two resident per CU): long per-wave streams, a small
+  // slab ([L][nchunk][SLAB]: 33 MB at C2 and C4)
+  int tpc = 8;
+  while (tpc < WG_TPC_MAX && (long)(ntiles / (2 * tpc)) * L >= 8L * ncu) tpc *= 2;
+  return tpc;
+}
+
+int lbwn_layer_wgrad_launch(const lbwn_wgrad_args& g, hipStream_t st) {
+  LBWN_REQUIRE(g.X && g.Z && g.DV && g.GX && g.slab && g.tpc >= 1 && g.tpc <= WG_TPC_MAX && g.stride >= SLAB,
+               "layer wgrad: bad arguments");
+  LBWN_REQUIRE(!g.gcs || (g.ids && g.tile_gid && g.gtab), "layer wgrad: GC needs ids, tile ids and the tables");
+  const int tps = (g.T + 127) / 128, ntiles = g.B * tps;
+  // 32-bit lane offsets (buffer loads): z rows, the exports, x
+  LBWN_REQUIRE((long)g.B * g.T * g.lddz * 4 < 0x7fffffffL && g.dvks * 4 < 0x7fffffffL && g.gxls * 4 < 0x7fffffffL &&
+                   g.xls * 4 < 0x7fffffffL && g.dvks >= (long)g.B * g.T * 32 && g.gxls >= (long)g.B * g.T * 32,
+               "layer wgrad: rows past 2 GiB per layer");
+  WgK k;
+  k.X = g.X; k.xls = g.xls; k.Z = g.Z; k.lddz = g.lddz; k.DV = g.DV; k.dvks = g.dvks; k.GX = g.GX; k.gxls = g.gxls;
+  k.slab = g.slab; k.stride = g.stride;
+  k.ids = g.ids; k.tile_gid = g.tile_gid; k.gcs = g.gcs; k.gtab = g.gtab; k.gc_ld = g.gc_ld;
+  k.B = g.B; k.T = g.T; k.H = g.H; k.L = g.L; k.nbl = g.nbl; k.tps = tps; k.ntiles = ntiles; k.tpc = g.tpc;
+  k.nchunk = (ntiles + g.tpc - 1) / g.tpc;
+  const dim3 grid(k.nchunk, g.L);
+  if (g.gcs) layer_wgrad_kernel<true><<<grid, 256, 0, st>>>(k);
+  else layer_wgrad_kernel<false><<<grid, 256, 0, st>>>(k);
+  LBWN_CHECK_LAUNCH();
+  return 0;
+}
+
+int lbwn_gc_tile_sum_rows_launch(const float* gcs, int L, int ntiles, const int* tile_gid, float* gtab, long ld,
+                                 int ncat1, hipStream_t st) {
+  LBWN_REQUIRE(ncat1 >= 1 && gcs && tile_gid && gtab, "gc tile sums: bad arguments");
+  gc_tile_sum_kernel<<<dim3(L, ncat1), 64, 0, st>>>(gcs, (long)ntiles * 64, 64, ntiles, tile_gid, gtab, ld);
   LBWN_CHECK_LAUNCH();
   return 0;
 }

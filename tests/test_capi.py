@@ -93,6 +93,27 @@ def test_plan_chain_tile_env(monkeypatch):
         assert b'LBWN_CHAIN_TILE' in lib.lbwn_last_error()
 
 
+def test_plan_bwd_wgrad_env(monkeypatch):
+    """LBWN_BWD_WGRAD=1 (read at plan creation) takes the residual stack's weight gradients out
+    of the backward chain: the plan then carves the chain's DV and G exports (the workspace grows
+    by 3 x 128 B per position and layer, rounded to 32-row blocks); 0 keeps them in the chain."""
+    import ctypes
+    from lbwn import _lib
+    lib = _lib.load()
+    lib.lbwn_plan_workspace_bytes.restype = ctypes.c_size_t
+    a = _lib.Arch()
+    a.n_blocks, a.n_block_layers, a.n_quant, a.n_res, a.n_dil, a.n_skip, a.n_post = 5, 10, 256, 32, 32, 512, 512
+    sizes = {}
+    for v in ('0', '1'):
+        monkeypatch.setenv('LBWN_BWD_WGRAD', v)
+        h = ctypes.c_void_p()
+        assert lib.lbwn_plan_create(ctypes.byref(a), 8, 4096, ctypes.byref(h)) == 0, v
+        sizes[v] = lib.lbwn_plan_workspace_bytes(h)
+        lib.lbwn_plan_destroy(h)
+    grow = sizes['1'] - sizes['0']
+    assert 3 * 128 * 50 * 8 * 4096 <= grow <= 3 * 128 * 50 * 8 * 4096 + 3 * 4096 * 50, grow
+
+
 def test_gemm_mode_env_selects_f32_mfma():
     """LBWN_GEMM=f32 (read once, at the first GEMM or mode query) selects the f32-MFMA GEMMs
     (mode 0); unset or anything else keeps the bf16-split form (mode 1).  Fresh processes: the

@@ -44,6 +44,9 @@ tr = allr[1]   # backward
 if net.lib.lbwn_gemm_get_mode() == 1:      # chain_bwd_x3_kernel: XSTAMP(0..6)
     names = ['G wait+build, DMA issue', 'dz,dv,DV', 'dx MFMA + OC', 'publish+img DMA+prefetch', 'dSIG MFMA',
              'dRES+bias+slab+bar']
+    if os.environ.get('LBWN_BWD_WGRAD') == '1':   # export form: no weight gradients in the chain
+        names = ['G build (G rows landed)', 'dz,dv, DV+G export', 'dx MFMA + OC', 'drain+bar+publish',
+                 'image DMA + flag poll', 'G row loads issue']
     order = list(range(L - 1, -1, -1))
     seg = np.diff(tr[:, :7], axis=1)[order]
     med = np.median(seg[1:-1], axis=0)
