@@ -61,6 +61,7 @@ struct lbwn_plan {
   size_t oSPLIT_AUX = 0;         // split-K workspace of the aux2 stream (LC / GC grads beside dSKIP)
   bool up_fused = false;         // LC upsample as one fused launch per direction (cond.hip)
   int dlc_parts = 1;             // split-K partials the last dlc GEMM left for the fused upsample backward
+  const float* dlc_spl = nullptr;   // ... in this split-K workspace (checked by lc_upsample_bwd)
   bool up_fused_bwd = false;     // ... for the backward (<= 256 mel frames; else per-stage GEMMs)
   size_t oUPPART = 0;            // its per-frame filter-gradient partials
   size_t total;
@@ -431,6 +432,13 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
   }
   const char* nc = getenv("LBWN_NO_CHAIN");
   p->chain = p->Cr == 32 && p->Cd == 32 && !(nc && nc[0] == '1');
+  // the 16-position backward chain addresses its per-layer dZ / σ / z rows with 32-bit lane offsets
+  // (chain_bwd16_kernel load_regs): refuse here, not at the first backward after a whole forward
+  if (p->chain && bwd_nw && (long)M * ldz * 4 >= 0x7fffffffL) {
+    delete p;
+    LBWN_REQUIRE(false, "plan: B*T*n_layers*n_dil*4 = %ld bytes of z rows is past the backward chain's 2 GiB lane "
+                        "offsets (LBWN_NO_CHAIN=1 runs the per-layer kernels)", (long)M * ldz * 4);
+  }
   p->oOCG = p->chain ? carve(cur, sizeof(float) * (size_t)L * M * 32) : 0;
   p->oSG = p->chain ? carve(cur, sizeof(float) * (size_t)L * m32(M) * 32) : 0;   // sg_off: whole 32-row blocks
   p->overlap = p->chain;
@@ -731,6 +739,7 @@ int lc_dlc(lbwn_plan* p, const lbwn_params* P, void* ws, float* spl, hipStream_t
   // the fused upsample backward sums dlc's split-K partials as it loads them (no reduce launch
   // between the two on the main stream); the per-stage path reads the reduced dlc
   p->dlc_parts = 1;
+  p->dlc_spl = spl;
   if (p->up_fused_bwd) g.splits_deferred = &p->dlc_parts;
   Probe(p, st, "lc_dlc");
   if ((e = lbwn_gemm_launch(g, 1, 1, p->split_dlcx, spl, st))) return e;
@@ -747,8 +756,11 @@ int lc_upsample_bwd(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G, vo
     float* act[8];
     for (int i = 0; i < p->nup; ++i) { F[i] = P->lc_up[i]; act[i] = at<float>(ws, p->oLCACT[i]); }
     Probe(p, st, "lc_up_bwd");
-    // dlc as the dlc GEMM left it: dlc_parts split-K partials in spl, or the product itself
+    // dlc as the dlc GEMM left it: dlc_parts split-K partials in spl, or the product itself.  The
+    // partials live only in that workspace: lc_dlc must have run last on this same spl (no launch
+    // that uses spl may sit between the two, on any stream -- the three call sites hold this)
     const bool parts = p->dlc_parts > 1;
+    LBWN_REQUIRE(!parts || p->dlc_spl == spl, "lc upsample bwd: dlc's split-K partials are in another workspace");
     e = lbwn_lc_up_bwd_launch(p->nup, p->up, p->Li, p->Lo, (int)(p->M / p->hop), mel, F, act, parts ? spl : dout,
                               at<float>(ws, p->oUPPART), G->lc_up, st, st_sum, p->ev_upb, p->dlc_parts,
                               parts ? p->M * p->Lo : 0);

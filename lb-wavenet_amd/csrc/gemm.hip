@@ -1246,6 +1246,10 @@ int gemm_launch_x3(const lbwn_gemm_args& a, int a_kcontig, int b_kcontig, int sp
     LBWN_CHECK_LAUNCH();
     return splitk_finish(a, split_k, slab_ws, st);
   }
+  // every other kernel below reads A row-major: an mn-blocked A (a_gstride) would be read in the
+  // wrong layout there
+  LBWN_REQUIRE(!a.a_gstride, "gemm: mn-blocked A (a_gstride) needs the AMN A-in-registers form (X3Q, no pre-split B, "
+                             "no epilogue, M >= 256)");
   if (wm == 4 && X3R && kfull && pre && a_kcontig) {
     if (a.N <= 96) {   // 96-column tiles: the grid is re-formed for them
       grid.x = (unsigned)(((a.M + 255) / 256) * ((a.N + 95) / 96));

@@ -2516,6 +2516,7 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
     // the weight-gradient products, when the producer published long ago): its flag wait and
     // load latency overlap the bias sums and slab stores instead of opening the next layer
     floatx4 gl[NR];
+    floatx4 gx_keep[2], dvs_keep[2], dvg_keep[2];   // !WG: this layer's export rows
     for (int l = a.L - 1; l >= 0; --l) {
       XSTAMP(0);
       const int d = 1 << (l % a.nbl);
@@ -2538,8 +2539,10 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         }
         XSTAMP(14);
         // lands this wave's part of the weight image (DMA'd during the last layer) and the
-        // prefetched rows; the barrier then covers every wave's part
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // prefetched rows; the barrier then covers every wave's part (!WG: not the 6 export
+        // stores issued after them)
+        if (WG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         XSTAMP(15);
         __syncthreads();
       }
@@ -2563,11 +2566,6 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
         v += oa[xb];
         gv[xb] = v;
         if (WG) *(floatx4*)gp = v;
-      }
-      if (!WG && valid) {   // G export for the weight gradients
-        float* gxo = a.gx + (long)l * a.gxls + m * 32;
-#pragma unroll
-        for (int xb = 0; xb < 2; ++xb) *(floatx4*)(gxo + 16 * xb + 4 * g) = gv[xb];
       }
       // 2. dz = dZ + RES·g on the bf16 cores: one 32-deep k-step of six split products per block
       //    bb (A row i = z channel ch16(bb, i) of RX, k = 8g + e = the lane's g registers in order)
@@ -2612,7 +2610,7 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
             *(floatx4*)(DVs + r * XS + c) = dvs[bb];
             *(floatx4*)(DVg + r * XS + c) = dvg[bb];
           }
-          if (dvo) {
+          if (WG && dvo) {
             *(floatx4*)(dvo + c) = dvs[bb];
             *(floatx4*)(dvo + dgo + c) = dvg[bb];
           }
@@ -2662,6 +2660,11 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
       }
       oa[0] = acc_a[0];
       oa[1] = acc_a[1];
+      if (!WG) {   // kept for the exports after the publish
+        gx_keep[0] = gv[0]; gx_keep[1] = gv[1];
+        dvs_keep[0] = dvs[0]; dvs_keep[1] = dvs[1];
+        dvg_keep[0] = dvg[0]; dvg_keep[1] = dvg[1];
+      }
       XSTAMP(3);
       // 5. publish out_c0_l (the drain also lands this layer's x / z DMA pieces)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2669,26 +2672,46 @@ __global__ __launch_bounds__(64 * NW) void chain_bwd16_kernel(ChainBK a) {
       if (tid == 0 && l > 0) publish_flag(a.flags + tile, (unsigned)(a.L - l));
       if (!WG) {
         XSTAMP(4);
-        if (l == 0) continue;
-        // the next layer's image (this layer's dx was its last reader), then the producer of the
-        // next layer's G rows: each wave polls its flag (lane 0) and loads its own rows, so no
-        // block barrier sits between the publish and the next layer's G build
-        dma_image(l - 1);
-        const int pn = tt + max(1, d / TP);
-        if (pn < tps) {
-          if (lane == 0 && !s_fail) {
-            if (!wait_flag_ge(a.flags + (long)b * tps + pn, (unsigned)(a.L - l), a.status, 2u)) s_fail = 1;
+        if (l > 0) {
+          // the next layer's image (this layer's dx was its last reader), then the producer of the
+          // next layer's G rows: each wave polls its flag (lane 0) and loads its own rows, so no
+          // block barrier sits between the publish and the next layer's G build
+          dma_image(l - 1);
+          const int pn = tt + max(1, d / TP);
+          if (pn < tps) {
+            if (lane == 0 && !s_fail) {
+              if (!wait_flag_ge(a.flags + (long)b * tps + pn, (unsigned)(a.L - l), a.status, 2u)) s_fail = 1;
+            }
+            __builtin_amdgcn_wave_barrier();
           }
-          __builtin_amdgcn_wave_barrier();
-        }
-        XSTAMP(5);
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)l * a.ocls, (short)0, oc_bytes, BUF_DW3);
+          XSTAMP(5);
+          const __amdgpu_buffer_rsrc_t rs =
+              __builtin_amdgcn_make_buffer_rsrc(a.ocg + (long)l * a.ocls, (short)0, oc_bytes, BUF_DW3);
 #pragma unroll
-        for (int i = 0; i < NR; ++i) {
-          const int e = tid + NT * i, c4 = (e & 7) * 4;
-          const int ts = min(t0 + (e >> 3) + d, a.T - 1);
-          gl[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
+          for (int i = 0; i < NR; ++i) {
+            const int e = tid + NT * i, c4 = (e & 7) * 4;
+            const int ts = min(t0 + (e >> 3) + d, a.T - 1);
+            gl[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((mb + ts) * 32 + c4) * 4), 0, 16);
+          }
+        }
+        // the exports for the weight gradients (G = dx_{l+1} rows, DV) only now, behind the G row
+        // loads: the publish drain did not wait for them, and the next G build waits only for what
+        // was issued before them (vmcnt(6)).  Every lane stores (a past-T lane at an offset past
+        // the record: the store is dropped), so each wave issues exactly 6 of them.
+        {
+          const int nrec = (int)std::min<long>((long)a.B * a.T * 128, 0x7fffffffL);
+          const int ok = valid ? (int)(m * 128) : 0x7ffffff0;
+          const __amdgpu_buffer_rsrc_t rgx = __builtin_amdgcn_make_buffer_rsrc(a.gx + l * a.gxls, (short)0, nrec, BUF_DW3);
+          const __amdgpu_buffer_rsrc_t rvs = __builtin_amdgcn_make_buffer_rsrc(a.dv_out + 2L * l * a.dvks, (short)0, nrec, BUF_DW3);
+          const __amdgpu_buffer_rsrc_t rvg = __builtin_amdgcn_make_buffer_rsrc(a.dv_out + (2L * l + 1) * a.dvks, (short)0, nrec, BUF_DW3);
+#pragma unroll
+          for (int xb = 0; xb < 2; ++xb) __builtin_amdgcn_raw_buffer_store_b128(gx_keep[xb], rgx, ok + (16 * xb + 4 * g) * 4, 0, 0);
+#pragma unroll
+          for (int bb = 0; bb < 2; ++bb) {
+            const int cz = (8 * (q0 + bb) + 4 * h) * 4;
+            __builtin_amdgcn_raw_buffer_store_b128(dvs_keep[bb], rvs, ok + cz, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(dvg_keep[bb], rvg, ok + cz, 0, 0);
+          }
         }
         XSTAMP(6);
         continue;
