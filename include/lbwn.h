@@ -84,9 +84,11 @@ int lbwn_plan_probe(lbwn_plan* plan, const char* launch_name, void* ev_start, vo
  * lbwn_train_backward on this plan, so that a data-parallel caller can start a gradient
  * all-reduce bucket before the backward ends.  point "head_grads": the POST1/POST2 weight
  * gradients, their biases and SKIP_BIAS are final and the backward chain has completed (no
- * collective can then share the chip with a persistent chain launch).  *waited = 1 if the plan
- * has that point (chain plans without padded head widths), else 0 and nothing is enqueued
- * (wait for the whole backward instead).  Added in ABI 2. */
+ * collective can then share the chip with a persistent chain launch).  point "side_grads": the
+ * end of the plan's side stream -- PRE, SIGNAL, GATE, RESIDUAL, the GC tables and their biases
+ * are final (dSKIP may still run).  *waited = 1 if the plan has that point (chain plans; for
+ * "head_grads" without padded head widths), else 0 and nothing is enqueued (wait for the whole
+ * backward instead).  Added in ABI 2 ("side_grads": round 6, same ABI). */
 int lbwn_plan_stream_wait(lbwn_plan* plan, const char* point, void* stream, int* waited);
 /* receptive field F = n_blocks·Σ2^l (tmodel.py:50-51) */
 int lbwn_recep_field_sz(const lbwn_arch* arch);

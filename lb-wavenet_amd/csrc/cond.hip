@@ -39,38 +39,33 @@ __global__ void gc_table_kernel(const float* __restrict__ emb, const float* __re
 constexpr int GC_CSPLIT = 16;   // category chunks of the weight-gradient pass
 constexpr int GC_EMAX = 32;     // n_gc_embed supported by the gradient kernels
 
-// part[k][e][n] = Σ_{c in chunk k} emb[c][e] · gcd[c][n]   (grid: n blocks × GC_CSPLIT chunks)
-__global__ __launch_bounds__(256) void gc_wgrad_part_kernel(const float* __restrict__ emb,
-                                                            const float* __restrict__ gcd, float* __restrict__ part,
-                                                            int N, int ncat1, int Ge) {
-  const int n = blockIdx.x * 256 + threadIdx.x, k = blockIdx.y;
-  const int per = (ncat1 + GC_CSPLIT - 1) / GC_CSPLIT, c0 = k * per, c1 = min(ncat1, c0 + per);
-  float acc[GC_EMAX];
+// dW(n)[e] = Σ_c emb[c][e] · gcd[c][n], one thread per (e, n), the categories in order
+// (deterministic).  At most 32 VGPRs (scalar index math, batches of 4 loads): it runs on the side
+// stream beside dSKIP's A-in-registers GEMM blocks (2 waves of 240 VGPRs per SIMD leave 32), so it
+// must fit in what they leave free or it waits for them (round 5: 164 us at C4 as a 32-accumulator
+// split-C kernel whose blocks could not start beside dSKIP).
+__global__ __launch_bounds__(256) void gc_wgrad_kernel(const float* __restrict__ emb, const float* __restrict__ gcd,
+                                                       float* __restrict__ dsig, float* __restrict__ dgate, int N,
+                                                       int ncat1, int Ge, int Cd) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Ge * N) return;
+  const int e = i / N, n = i - e * N;
+  float acc = 0.f;
+  int c = 0;
+  for (; c + 4 <= ncat1; c += 4) {
+    float g[4], w[4];
+    const float* gp = gcd + c * N + n;
+    const float* wp = emb + c * Ge + e;
 #pragma unroll
-  for (int e = 0; e < GC_EMAX; ++e) acc[e] = 0.f;
-  if (n < N) {
-    for (int c = c0; c < c1; ++c) {
-      const float g = gcd[(long)c * N + n];
-#pragma unroll
-      for (int e = 0; e < GC_EMAX; ++e)
-        if (e < Ge) acc[e] += emb[(long)c * Ge + e] * g;
+    for (int j = 0; j < 4; ++j) {
+      g[j] = gp[j * N];
+      w[j] = wp[j * Ge];
     }
 #pragma unroll
-    for (int e = 0; e < GC_EMAX; ++e)
-      if (e < Ge) part[((long)k * Ge + e) * N + n] = acc[e];
+    for (int j = 0; j < 4; ++j) acc += w[j] * g[j];
   }
-}
-
-// dW(n)[e] = Σ_k part[k][e][n]  (fixed order: deterministic)
-__global__ void gc_wgrad_sum_kernel(const float* __restrict__ part, float* __restrict__ dsig, float* __restrict__ dgate,
-                                    int N, int Ge, int Cd) {
-  const long total = (long)Ge * N;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int n = (int)(i % N), e = (int)(i / N);
-    float s = 0.f;
-    for (int k = 0; k < GC_CSPLIT; ++k) s += part[((long)k * Ge + e) * N + n];
-    *const_cast<float*>(gc_w(dsig, dgate, n, e, Ge, Cd)) = s;
-  }
+  for (; c < ncat1; ++c) acc += emb[c * Ge + e] * gcd[c * N + n];
+  *const_cast<float*>(gc_w(dsig, dgate, n, e, Ge, Cd)) = acc;
 }
 
 // dEMB[c][e] = Σ_n gcd[c][n] · W(n)[e] as a small tiled product: block (category group cg, n chunk
@@ -90,24 +85,31 @@ __global__ __launch_bounds__(256) void gc_egrad_part_kernel(const float* __restr
   const int ep = Ge <= 16 ? 16 : 32, cpb = 256 / ep;
   const int cg = blockIdx.x, k = blockIdx.y, t = threadIdx.x;
   const int n = k * GE_N + t, nc = min(n, N - 1);
-  {
+  {   // batches of 4 loads: at most 32 VGPRs (it runs on the side stream beside dSKIP, as gc_wgrad_kernel)
     const int l = nc / (2 * Cd), s = (nc / Cd) & 1, o = nc % Cd;
-    const float* W = (s == 0 ? wsig : wgate) + (long)l * Ge * Cd + o;
-    float wv[GC_EMAX], gv[16];
-#pragma unroll
-    for (int e = 0; e < GC_EMAX; ++e) wv[e] = W[(long)min(e, Ge - 1) * Cd];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) gv[c] = gcd[(long)min(cg * cpb + min(c, cpb - 1), ncat1 - 1) * N + nc];
+    const float* W = (s == 0 ? wsig : wgate) + l * Ge * Cd + o;
     const bool in = n < N;
+#pragma unroll 1
+    for (int e0 = 0; e0 < GC_EMAX; e0 += 4) {
+      float wv[4];
 #pragma unroll
-    for (int e = 0; e < GC_EMAX; ++e) wsm[t][e] = in ? wv[e] : 0.f;
+      for (int j = 0; j < 4; ++j) wv[j] = W[min(e0 + j, Ge - 1) * Cd];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) gs[c][t] = in ? gv[c] : 0.f;
+      for (int j = 0; j < 4; ++j) wsm[t][e0 + j] = in ? wv[j] : 0.f;
+    }
+#pragma unroll 1
+    for (int c0 = 0; c0 < 16; c0 += 4) {
+      float gv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gv[j] = gcd[min(cg * cpb + min(c0 + j, cpb - 1), ncat1 - 1) * N + nc];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) gs[c0 + j][t] = in ? gv[j] : 0.f;
+    }
   }
   __syncthreads();
   const int cl = t / ep, e = t % ep, c = cg * cpb + cl;
   float acc = 0.f;
-#pragma unroll 8
+#pragma unroll 4
   for (int j = 0; j < GE_N; ++j) acc += gs[cl][j] * wsm[j][e];
   if (c < ncat1 && e < Ge) part[((long)k * ncat1 + c) * Ge + e] = acc;
 }
@@ -484,12 +486,9 @@ int lbwn_gc_grad_launch(const float* emb, const float* wsig, const float* wgate,
                         float* demb, float* dsig, float* dgate, int L, int ncat1, int Ge, int Cd, hipStream_t st) {
   LBWN_REQUIRE(Ge >= 1 && Ge <= GC_EMAX, "gc grads: n_gc_embed must be in [1, %d]", GC_EMAX);
   const int N = 2 * L * Cd;
-  gc_wgrad_part_kernel<<<dim3((N + 255) / 256, GC_CSPLIT), 256, 0, st>>>(emb, gcd, part, N, ncat1, Ge);
+  gc_wgrad_kernel<<<(Ge * N + 255) / 256, 256, 0, st>>>(emb, gcd, dsig, dgate, N, ncat1, Ge, Cd);
   LBWN_CHECK_LAUNCH();
-  gc_wgrad_sum_kernel<<<grid_for((long)Ge * N), 256, 0, st>>>(part, dsig, dgate, N, Ge, Cd);
-  LBWN_CHECK_LAUNCH();
-  // (part is free again: gc_wgrad_sum_kernel consumed it; GC_CSPLIT·Ge·N >= nk·ncat1·Ge floats
-  // holds for every shipped arch and is checked here)
+  // (part: GC_CSPLIT·Ge·N >= nk·ncat1·Ge floats holds for every shipped arch and is checked here)
   const int nk = (N + GE_N - 1) / GE_N, ep = Ge <= 16 ? 16 : 32, cpb = 256 / ep;
   LBWN_REQUIRE((long)nk * ncat1 * Ge <= (long)GC_CSPLIT * Ge * N, "gc grads: partial buffer too small");
   gc_egrad_part_kernel<<<dim3((ncat1 + cpb - 1) / cpb, nk), 256, 0, st>>>(gcd, wsig, wgate, part, N, ncat1, Ge, Cd);

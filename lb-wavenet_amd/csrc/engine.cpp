@@ -24,6 +24,7 @@ struct lbwn_plan {
   // the gemm_x3q_kernel<8> form
   size_t oMBS = 0, oMBR = 0;
   bool mb_s = false, mb_r = false;
+  bool mbits_ok = true;
   bool dv_blk = false;     // the last backward exported DV k-blocked ([2L][m32(M)][32])
   int head_colparts = 0;   // post2-bias column partial rows the last forward's head wrote (0: none)
   lbwn_arch a;
@@ -89,6 +90,7 @@ struct lbwn_plan {
   hipEvent_t ev_dlc = nullptr;   // backward (dlc over more than one round of blocks): dlc done -> aux2
   bool up_forked = false;        // this forward launched the fused upsample on aux2
   bool bwd_chain_event = false;  // the last backward recorded ev_chain (lbwn_plan_stream_wait)
+  bool bwd_side_event = false;   // ... and ev_join2 at the end of its side-stream work
   bool wpk_valid = false;        // the f32 layer images were packed this step
   // Weights pre-split into bf16 planes once per step for the bf16-split GEMMs (gemm.hip):
   // [W3_SKIP_F] SKIPcat as skip-fwd B, [W3_POST1_F] POST1 as post1-fwd B, [W3_POST2_F] POST2 as
@@ -167,6 +169,16 @@ int lbwn_plan_stream_wait(lbwn_plan* p, const char* point, void* stream, int* wa
     // head weight-gradient GEMMs and the bias column sums (padded heads copy theirs out at the end)
     if (p->bwd_chain_event && !p->oPADG) {
       LBWN_HIP(hipStreamWaitEvent((hipStream_t)stream, p->ev_chain, 0));
+      *waited = 1;
+    }
+    return 0;
+  }
+  if (!strcmp(point, "side_grads")) {
+    // ev_join2: recorded on the side stream after its last gradient kernel (dPRE, the slab
+    // reduction of SIG/GATE/RES and their biases, the GC table grads; for LC plans also after
+    // the upsample's frame sum), while dSKIP may still run on the main stream
+    if (p->bwd_side_event) {
+      LBWN_HIP(hipStreamWaitEvent((hipStream_t)stream, p->ev_join2, 0));
       *waited = 1;
     }
     return 0;
@@ -355,6 +367,8 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     p->dz_xcd2d = (dv && dv[0] == '0') ? 0 : 1;
     // weight gradients of the residual stack: inside the backward chain (0) or by
     // layer_wgrad_kernel over the chain's exports (1; 16-position backward on 128-position tiles)
+    const char* mv = getenv("LBWN_GEMM_MBITS");
+    p->mbits_ok = !(mv && mv[0] == '0');
     const char* wv = getenv("LBWN_BWD_WGRAD");
     p->wg_out = (wv && wv[0] == '1') && bwd_nw == 8;
   }
@@ -924,9 +938,11 @@ int lbwn_train_forward(lbwn_plan* p, const lbwn_params* P, void* ws, const int* 
   // SAVE_l <- last d rows of [SAVE ++ x_l]  (tmodel.py:165)
   if ((e = lbwn_dsep_save_launch(X, p->x_layer_stride, save, L, p->nbl, B, T, H, Cr, st))) return e;
   // mask bits for the backward's dS / dH1 epilogues: both GEMM ends in the x3q<8> form
-  p->mb_s = lbwn_gemm_x3q8_form((int)M, p->Cs, (int)ldz, 1, w3(p, ws, W3_SKIP_F) != nullptr, 1, 0) &&
+  // (p->mbits_ok: LBWN_GEMM_MBITS=0 at plan creation forces the f32-mask fallback; a test compares
+  // the two bitwise, tests/test_gpu_parity.py::test_mask_bits_equal_f32_masks)
+  p->mb_s = p->mbits_ok && lbwn_gemm_x3q8_form((int)M, p->Cs, (int)ldz, 1, w3(p, ws, W3_SKIP_F) != nullptr, 1, 0) &&
             lbwn_gemm_x3q8_form((int)M, p->Cs, p->Cp, 1, w3(p, ws, W3_POST1_B) != nullptr, 1, 0);
-  p->mb_r = lbwn_gemm_x3q8_form((int)M, p->Cp, p->Cs, 1, w3(p, ws, W3_POST1_F) != nullptr, 1, 0) &&
+  p->mb_r = p->mbits_ok && lbwn_gemm_x3q8_form((int)M, p->Cp, p->Cs, 1, w3(p, ws, W3_POST1_F) != nullptr, 1, 0) &&
             lbwn_gemm_x3q8_form((int)M, p->Cp, p->Q, 1, w3(p, ws, W3_POST2_B) != nullptr, 1, 0);
   // S = Σ_l (z_l·SKIP_l + b) as ONE GEMM over Zcat (tmodel.py:171-184, :316-320)
   if (P->skip_b && !bsum_done && (e = lbwn_sum_bias_launch(P->skip_b, L, p->Cs, bsum, st))) return e;
@@ -1241,7 +1257,10 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
       if (!lc_seq && (e = lc_dlc(p, P, ws, SPL, st))) return e;
       if (!lc_seq && (e = lc_upsample_bwd(p, P, G, ws, mel, SPL, st, rst))) return e;   // its frame sum on the side
     }
-    if (p->aux2) LBWN_HIP(hipEventRecord(p->ev_join2, rst));
+    if (p->aux2) {
+      LBWN_HIP(hipEventRecord(p->ev_join2, rst));
+      p->bwd_side_event = true;
+    }
   } else {
     p->dv_blk = false;
       for (int l = L - 1; l >= 0; --l) {

@@ -52,12 +52,15 @@ class DPContext:
         optimizer skip the step on the device, so no rank applies garbage gradients; the bits
         travel as per-bit counts, status_to_bits).
 
-        Two buckets, each ONE message (a staging copy of its flat ranges):
+        Three buckets, each ONE message (a staging copy of its flat ranges):
           0 "head": POST1, POST2, their biases, SKIP_BIAS + the stats + the status word — final
             once the backward chain has completed (lbwn_plan_stream_wait "head_grads"), so its
             all-reduce runs on a side stream beside the backward's tail (dSKIP, the slab
             reduction, dPRE, the conditioning grads);
-          1 "rest": every other gradient, after the whole backward.
+          1 "side": PRE, SIGNAL, GATE, RESIDUAL, the GC tables and their biases — final once the
+            plan's side stream has run dPRE, the slab reduction and the GC grads ("side_grads"),
+            while dSKIP may still run on the main stream;
+          2 "rest": SKIP and the LC weights, after the whole backward.
         No collective ever overlaps a persistent chain launch: bucket 0 starts after the backward
         chain, and the current stream waits for both buckets before the optimizer (hence before
         the next step's forward chain).  A chain's tiles assume every block of a round is resident
@@ -67,24 +70,24 @@ class DPContext:
             return
         plan = _Buckets.of(net)
         if not net.grad_flat.is_cuda:   # gloo (CPU tests): the same buckets, in order
-            for k in range(2):
+            for k in range(len(plan.ranges)):
                 plan.pack(k, net)
                 dist.all_reduce(plan.buf[k])
                 plan.unpack(k, net)
             return
         main = torch.cuda.current_stream(net.grad_flat.device)
         comm = self._comm_stream(net.grad_flat.device)
-        if not net.wait_point('head_grads', comm):
-            comm.wait_stream(main)
-        with torch.cuda.stream(comm):
-            plan.pack(0, net)
-            dist.all_reduce(plan.buf[0])
-            plan.unpack(0, net)
-        comm.wait_stream(main)
-        with torch.cuda.stream(comm):
-            plan.pack(1, net)
-            dist.all_reduce(plan.buf[1])
-            plan.unpack(1, net)
+        # each bucket waits for its point of the backward, or for the whole backward when the
+        # plan has no such point (the comm stream's order keeps the buckets' all-reduces serial)
+        for k, point in enumerate(('head_grads', 'side_grads', None)):
+            if not plan.ranges[k] and k > 0:
+                continue
+            if point is None or not net.wait_point(point, comm):
+                comm.wait_stream(main)
+            with torch.cuda.stream(comm):
+                plan.pack(k, net)
+                dist.all_reduce(plan.buf[k])
+                plan.unpack(k, net)
         main.wait_stream(comm)
 
     def reduce_grads_flat(self, net):
@@ -129,13 +132,26 @@ class _Buckets:
     def __init__(self, net):
         lay = net.layout
         kb = lay.kind_base
+        # weights: [pre sig gate res | skip | gc_embed gc_sig gc_gate | lc.. | post1 post2]
         head = [(kb['post1'], lay.n_weights)]
-        rest = [(0, kb['post1'])]
-        if 'skip_b' in kb:
+        side = [(0, kb['skip'])]
+        after_skip = min([kb[k] for k in kb if k.startswith('lc_up') or k in ('lc_sig', 'gc_embed')] + [kb['post1']])
+        rest = [(kb['skip'], after_skip)]
+        if 'gc_embed' in kb:
+            end_gc = min([kb[k] for k in kb if k.startswith('lc_up') or k == 'lc_sig'] + [kb['post1']])
+            side.append((kb['gc_embed'], end_gc))
+            if end_gc < kb['post1']:
+                rest.append((end_gc, kb['post1']))
+        elif after_skip < kb['post1']:
+            rest.append((after_skip, kb['post1']))
+        if 'skip_b' in kb:   # biases: [pre_b sig_b gate_b res_b | skip_b post1_b post2_b]
             head.append((kb['skip_b'], lay.n_total))
-            rest.append((lay.n_weights, kb['skip_b']))
-        self.ranges = [head, rest]
-        sizes = [sum(b - a for a, b in head) + 3 + STATUS_BITS, sum(b - a for a, b in rest)]
+            side.append((lay.n_weights, kb['skip_b']))
+        self.ranges = [head, side, rest]
+        covered = sorted(r for rs in self.ranges for r in rs)
+        assert covered[0][0] == 0 and covered[-1][1] == lay.n_total and all(
+            covered[i][1] == covered[i + 1][0] for i in range(len(covered) - 1)), ('buckets must tile the buffer', covered)
+        sizes = [sum(b - a for a, b in head) + 3 + STATUS_BITS] + [sum(b - a for a, b in r) for r in (side, rest)]
         self.buf = [torch.empty(n, dtype=torch.float32, device=net.grad_flat.device) for n in sizes]
 
     @staticmethod

@@ -3,6 +3,7 @@
 gradient reduction over gloo with world_size 2."""
 import json
 import os
+import re
 import sys
 
 import numpy as np
@@ -266,7 +267,7 @@ def _bucket_worker(rank, world, port, out_path):
     stats = torch.tensor([123.25 + rank, 1000.0 + rank, 7.0 * rank, 0.5])
     a = _FakeNet(grads.clone(), stats.clone(), lay, status=1 + 2 * rank)     # ranks: 0b01, 0b11
     b = _FakeNet(grads.clone(), stats.clone(), lay, status=1 + 2 * rank)
-    dp.reduce_grads(a)          # two buckets (head / rest)
+    dp.reduce_grads(a)          # three buckets (head / side / rest)
     dp.reduce_grads_flat(b)     # one message
     if rank == 0:
         np.savez(out_path, ga=a.grad_flat.numpy(), gb=b.grad_flat.numpy(), sa=a.stats.numpy(), sb=b.stats.numpy(),
@@ -275,9 +276,32 @@ def _bucket_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize('arch_file', ['arch1', 'arch2', 'arch3', 'arch4', 'arch5'])
+def test_dp_buckets_tile_the_gradient(arch_file):
+    """The all-reduce buckets cover every flat gradient range exactly once, by the stream that
+    finalises it: head = POST1 / POST2 / SKIP_BIAS and the head biases (after the backward
+    chain), side = PRE / SIGNAL / GATE / RESIDUAL / GC and their biases (after the side
+    stream), rest = SKIP and LC (after the whole backward)."""
+    from lbwn.dist import _Buckets
+    lay = ParamLayout(load_arch(os.path.join(ROOT, 'par', arch_file + '.json'), num_global_cond=7))
+    bk = _Buckets(_FakeNet(torch.zeros(lay.n_total), torch.zeros(4), lay))
+    owner = np.full(lay.n_total, -1)
+    for k, rs in enumerate(bk.ranges):
+        for a, b in rs:
+            assert (owner[a:b] == -1).all()
+            owner[a:b] = k
+    assert (owner >= 0).all()
+    want = {'POST1': 0, 'POST2': 0, 'SKIP_BIAS': 0, 'POST1_BIAS': 0, 'POST2_BIAS': 0, 'PRE': 1, 'PRE_BIAS': 1,
+            'SIGNAL': 1, 'GATE': 1, 'RESIDUAL': 1, 'SIGNAL_BIAS': 1, 'GATE_BIAS': 1, 'RESIDUAL_BIAS': 1,
+            'GC_EMBED': 1, 'GC_SIGNAL': 1, 'GC_GATE': 1, 'SKIP': 2, 'LC_UPSAMPLE': 2, 'LC_SIGNAL': 2, 'LC_GATE': 2}
+    for n, e in lay.entries.items():
+        stem = re.sub(r'(_\d+)+$', '', n)
+        assert (owner[e.offset:e.offset + e.numel] == want[stem]).all(), n
+
+
 def test_dp_bucketed_equals_flat(tmp_path):
-    """The two-bucket all-reduce (lbwn.dist: head bucket beside the backward's tail, the rest
-    after it) gives bitwise the flat one-message result, for the gradient, the loss stats and
+    """The three-bucket all-reduce (lbwn.dist: head bucket beside the backward's tail, side
+    bucket beside dSKIP, the rest after it) gives bitwise the flat one-message result, for the gradient, the loss stats and
     the status word (any rank's timeout reaches every rank as the OR of the words: 0b01 | 0b11
     = 0b11, where a SUM would read 0b100), over 2 gloo ranks at arch5's layout (GC + LC kinds
     included)."""

@@ -3,7 +3,8 @@ on the real training plan, on one GPU.
 
 The CUDA branch packs the head bucket on a comm stream that waits on the plan's "head_grads"
 point (lbwn_plan_stream_wait) while the backward's tail (dSKIP, the slab reduction, dPRE, the
-conditioning gradients) still runs on the main and side streams.  An early event, or a tail
+conditioning gradients) still runs on the main and side streams, and the side bucket (PRE,
+SIGNAL, GATE, RESIDUAL, GC and their biases) at "side_grads" while dSKIP may still run.  An early event, or a tail
 kernel writing into a head range, would corrupt the gradients silently; so would a missing wait
 before Adam.  The collective itself is replaced by an exact stand-in (x2 on the stream it is
 called on: the ring's SUM over two identical ranks), so the test needs no second GPU and every
@@ -58,9 +59,10 @@ def dp2(monkeypatch):
 
 @pytest.mark.parametrize('name,B,T', [('arch3', 4, 4096), ('arch5', 4, 4096)])
 def test_dp_device_path_bucketed_equals_flat(name, B, T, dp2, monkeypatch):
-    """Per step: the bucketed reduction (comm stream, head bucket after the backward chain)
-    == the flat one-message reduction after a full synchronize, bitwise, for the gradients,
-    the loss stats and the status word; "head_grads" is a real wait point for arch3 and arch5."""
+    """Per step: the bucketed reduction (comm stream, head bucket after the backward chain, side
+    bucket after the side stream's gradient kernels) == the flat one-message reduction after a
+    full synchronize, bitwise, for the gradients, the loss stats and the status word;
+    "head_grads" and "side_grads" are real wait points for arch3 and arch5."""
     arch = load_arch(os.path.join(ROOT, 'par', name + '.json'))
     net = make_net(arch, B, seed=2)
     q, ids, mel = _batch(arch, B, T, 5)
@@ -72,7 +74,7 @@ def test_dp_device_path_bucketed_equals_flat(name, B, T, dp2, monkeypatch):
     net.forward(q, mel, ids)
     dp2.reduce_grads(net)
     torch.cuda.synchronize()
-    assert waits == [True], 'head_grads must be a wait point of the %s chain plan' % name
+    assert waits == [True, True], 'head_grads and side_grads must be wait points of the %s chain plan' % name
     g_a, s_a, w_a = _bits(net.grad_flat), net.stats[:3].cpu().numpy(), _bits(net.status_word())
 
     net.save_flat.copy_(save0)                    # same D-sep state -> the same step again

@@ -604,6 +604,32 @@ def test_placement_switches_bitwise(monkeypatch, env):
         assert np.array_equal(g0[n], g1[n]), n
 
 
+def test_mask_bits_equal_f32_masks(monkeypatch):
+    """The relu masks of dS = dH1·POST1ᵀ ⊙ (S > 0) and dH1 = dlogits·POST2ᵀ ⊙ (R2 > 0) travel as
+    bits written by the skip / post1 GEMM epilogues (lbwn_gemm_args::mbits_out, read back by the
+    same x3q<8> lane layout in dS / dH1); LBWN_GEMM_MBITS=0 (plan creation) makes the backward
+    read the f32 S / R2 instead.  The two must agree bit for bit: dS, dH1, the stats, SAVE and
+    every gradient (arch3 B=4, T=4096: both ends in the x3q<8> form)."""
+    arch = arch3()
+    B, T = 4, 4096
+    q, ids = rand_batch(arch, B, T)
+    out = []
+    for mb in ('1', '0'):
+        monkeypatch.setenv('LBWN_GEMM_MBITS', mb)
+        net = make_net(arch, B)
+        net.forward(q, None, ids, backward=True)
+        torch.cuda.synchronize()
+        assert int(net.plan_tensor(T, 'status').view(torch.int32)[0]) == 0
+        out.append((net.stats[:3].cpu().numpy(), net.save_flat.cpu().numpy(),
+                    {n: g.cpu().numpy() for n, g in net.grads.items()},
+                    net.plan_tensor(T, 'ds').cpu().numpy(), net.plan_tensor(T, 'dh').cpu().numpy()))
+    (s0, v0, g0, ds0, dh0), (s1, v1, g1, ds1, dh1) = out
+    assert np.array_equal(ds0, ds1) and np.array_equal(dh0, dh1)
+    assert np.array_equal(s0, s1) and np.array_equal(v0, v1)
+    for n in g0:
+        assert np.array_equal(g0[n], g1[n]), n
+
+
 def test_chain_trace_build_bitwise(monkeypatch):
     """LBWN_CHAIN_TRACE=<block> (read at plan creation: the chains' traced instantiations, whose
     clock stamps feed tools/chain_trace.py and the bench's C4 dilation sweep) computes exactly what
