@@ -62,7 +62,14 @@ if net.lib.lbwn_gemm_get_mode() == 1:      # chain_bwd_x3_kernel: XSTAMP(0..6)
                         ('dSIG: k-step 1', 10, 5), ('dRES', 5, 11), ('bias + dRES slab + bar', 11, 12),
                         ('dSIG partials + bar', 12, 13), ('dSIG sum + slab', 13, 6)]:
             print('    %-26s %6d' % (n, np.median(sub[:, j] - sub[:, i])))
-    if np.all(sub[:, 15] > 0):   # sub-stamps of the G build (7 flag barrier, 14 G written, 15 vmcnt drained)
+    if os.environ.get('TRACE_TAIL') == '1' and np.all(sub[:, 15] > 0):
+        # a timing variant with stamps 7 / 14 / 15 moved into the weight-gradient tail (after the
+        # bias sums, after the flag wait, after the barrier): where the tail's cycles go
+        for n, i, j in [('tail: bias sums (waves 0-2)', 11, 7), ('tail: flag wait (tid 0)', 7, 14),
+                        ('tail: barrier', 14, 15), ('tail: G-row loads + bias sum + store', 15, 12),
+                        ('tail: partials park + barrier', 12, 13), ('tail: partial sums + slab', 13, 6)]:
+            print('    %-36s %6d' % (n, np.median(sub[:, j] - sub[:, i])))
+    elif np.all(sub[:, 15] > 0):   # sub-stamps of the G build (7 flag barrier, 14 G written, 15 vmcnt drained)
         for n, i, j in [('G: flag wait + barrier', 0, 7), ('G: loads + LDS writes', 7, 14), ('G: vmcnt(0)', 14, 15),
                         ('G: barrier', 15, 1)]:
             print('    %-26s %6d' % (n, np.median(sub[:, j] - sub[:, i])))
