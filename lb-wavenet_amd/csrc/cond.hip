@@ -40,7 +40,7 @@ constexpr int GC_CSPLIT = 16;   // category chunks of the weight-gradient pass
 constexpr int GC_EMAX = 32;     // n_gc_embed supported by the gradient kernels
 
 // dW(n)[e] = Σ_c emb[c][e] · gcd[c][n], one thread per (e, n), the categories in order
-// (deterministic).  At most 32 VGPRs (scalar index math, batches of 4 loads): it runs on the side
+// (deterministic).  At most 32 VGPRs (scalar index math, batches of 8 loads): it runs on the side
 // stream beside dSKIP's A-in-registers GEMM blocks (2 waves of 240 VGPRs per SIMD leave 32), so it
 // must fit in what they leave free or it waits for them (round 5: 164 us at C4 as a 32-accumulator
 // split-C kernel whose blocks could not start beside dSKIP).
@@ -52,17 +52,17 @@ __global__ __launch_bounds__(256) void gc_wgrad_kernel(const float* __restrict__
   const int e = i / N, n = i - e * N;
   float acc = 0.f;
   int c = 0;
-  for (; c + 4 <= ncat1; c += 4) {
-    float g[4], w[4];
+  for (; c + 8 <= ncat1; c += 8) {
+    float g[8], w[8];
     const float* gp = gcd + c * N + n;
     const float* wp = emb + c * Ge + e;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < 8; ++j) {
       g[j] = gp[j * N];
       w[j] = wp[j * Ge];
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc += w[j] * g[j];
+    for (int j = 0; j < 8; ++j) acc += w[j] * g[j];
   }
   for (; c < ncat1; ++c) acc += emb[c * Ge + e] * gcd[c * N + n];
   *const_cast<float*>(gc_w(dsig, dgate, n, e, Ge, Cd)) = acc;

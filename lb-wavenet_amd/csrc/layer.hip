@@ -3645,32 +3645,51 @@ namespace {
 // gtab[id][l·64 + c] += Σ over tiles with tile_gid == id (in tile order) of the tile's dv column
 // sums slab[l][tile][5120 + c].  Block = (layer, id), thread = column: the block scans the tile ids
 // 64 at a time (one per lane, ballot), then adds its matching tiles' partials in tile order
-// (deterministic; blocks of ids with no uniform tile only scan).  Side stream beside dSKIP: few
-// VGPRs, and the matching tiles' loads four at a time (one dependent load per tile ran 154 us at
-// C4, 1,024 tiles).
+// (deterministic; blocks of ids with no uniform tile only scan).  Side stream beside dSKIP, where
+// every dependent round trip is long: few VGPRs, 1,024 tile ids loaded at once (16 per lane) and
+// the matching tiles listed in LDS in tile order, then their partials loaded 16 at a time (a
+// ballot and a batch of 4 loads per 64 tiles ran 117 us at C4, one load per tile 154 us).
+constexpr int GTS_CHUNK = 1024;
 __global__ __launch_bounds__(64) void gc_tile_sum_kernel(const float* __restrict__ slab, long slab_layer, long tstride,
                                                          int ntiles, const int* __restrict__ tile_gid, float* gtab,
                                                          long ld) {
+  __shared__ int lst[GTS_CHUNK];
   const int l = blockIdx.x, id = blockIdx.y, c = threadIdx.x;
-  const float* sl = slab + l * slab_layer + c;
+  // the layer's partials through a buffer resource: a load's tile offset is one SGPR (the list
+  // entry is wave-uniform), so a batch of 16 costs 16 VGPRs, not 16 64-bit addresses
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(slab + l * slab_layer), (short)0, (int)min(slab_layer * 4, 0x7fffffffL), BUF_DW3);
+  const __amdgpu_buffer_rsrc_t rg =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(tile_gid), (short)0, ntiles * 4, BUF_DW3);
   float acc = 0.f;
   bool any = false;
-  for (int t0 = 0; t0 < ntiles; t0 += 64) {
-    const int t = t0 + c;
-    unsigned long long mask = __ballot(t < ntiles && tile_gid[min(t, ntiles - 1)] == id);
-    any |= mask != 0;
-    while (mask) {   // the matching tiles' loads in batches of 4, added in tile order (+0 past the last)
-      float v[4];
+  for (int s0 = 0; s0 < ntiles; s0 += GTS_CHUNK) {
+    int gid[GTS_CHUNK / 64];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int j = mask ? __ffsll((long long)mask) - 1 : 0;
-        const float x = sl[(long)(t0 + j) * tstride];
-        v[k] = mask ? x : 0.f;
-        mask &= mask - 1;
-      }
+    for (int k = 0; k < GTS_CHUNK / 64; ++k)   // past the end: 0 from the buffer, masked below
+      gid[k] = (int)__builtin_amdgcn_raw_buffer_load_b32(rg, c * 4, (s0 + 64 * k) * 4, 0);
+    int n = 0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) acc += v[k];
+    for (int k = 0; k < GTS_CHUNK / 64; ++k) {
+      const int t = s0 + 64 * k + c;
+      const bool hit = t < ntiles && gid[k] == id;
+      const unsigned long long m = __ballot(hit);
+      if (hit) lst[n + __popcll(m & ((1ull << c) - 1ull))] = t;
+      n += __popcll(m);
     }
+    any |= n > 0;
+    __syncthreads();
+    for (int i = 0; i < n; i += 16) {   // in tile order
+      float v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        v[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            rs, c * 4, __builtin_amdgcn_readfirstlane(lst[min(i + k, n - 1)]) * (int)tstride * 4, 0));
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (i + k < n) acc += v[k];
+    }
+    __syncthreads();   // the list is rewritten by the next chunk
   }
   if (any) gtab[(long)id * ld + (long)l * 64 + c] += acc;
 }

@@ -147,3 +147,31 @@ def test_env_switches_are_all_tested():
     tests = ''.join(open(f).read() for f in glob.glob(os.path.join(ROOT, 'tests', 'test_*.py')))
     untested = sorted(v for v in read if not re.search(r"(['\"]%s['\"]|\b%s=)" % (v, v), tests))
     assert not untested, 'read by the library but set by no test: %s' % untested
+
+
+def test_side_stream_kernels_fit_beside_dskip():
+    """The backward's side stream (dPRE, the slab reduction, the GC gradients) runs beside dSKIP's
+    A-in-registers GEMM only while its kernels fit in the VGPRs that GEMM's two waves per SIMD leave
+    free (512 - 2 x 240): a kernel past that budget waits for dSKIP's blocks instead, with nothing
+    failing (round 6: the GEMM at 242 VGPRs put dPRE 74 -> 306 us at C2).  Read from the gfx950
+    code objects of the built library (tools/kernel_regs.py), no GPU."""
+    import importlib.util
+    import pytest
+    if not os.path.exists('/opt/rocm/lib/llvm/bin/llvm-readelf'):
+        pytest.skip('llvm-readelf not installed')
+    spec = importlib.util.spec_from_file_location('kernel_regs', os.path.join(ROOT, 'tools', 'kernel_regs.py'))
+    kr = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(kr)
+    res = kr.kernel_resources()
+    assert res, 'no gfx950 code objects found in liblbwn.so'
+
+    def regs(pattern):
+        hits = {k: v['vgpr'] + v['agpr'] for k, v in res.items() if re.search(pattern, k)}
+        assert hits, pattern
+        return hits
+    amn = regs(r'gemm_x3q_kernelILi8ELb1E')
+    assert max(amn.values()) <= 240, amn
+    for k in ('pre_grad_part_kernel', 'pre_grad_reduce_kernel', 'layer_reduce_all_kernel', 'gc_tile_sum_kernel',
+              'gc_wgrad_kernel', 'gc_egrad_part_kernel', 'gc_egrad_sum_kernel'):
+        for name, n in regs(k).items():
+            assert n <= 32, (name, n)
