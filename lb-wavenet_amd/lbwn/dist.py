@@ -13,26 +13,22 @@ import torch
 import torch.distributed as dist
 
 
-STATUS_BITS = 8     # the plan's status word uses bits 0-1 (lbwn.h); 8 leave room
-
-
-def status_to_bits(word, out):
-    """int32 status word [1] -> one float per bit [STATUS_BITS], so that the all_reduce SUM of
-    the ranks' words is an OR per bit once thresholded (a SUM of the words themselves would
-    turn two ranks' bit 0 into bit 1 and blame the wrong chain)."""
-    sh = torch.arange(STATUS_BITS, dtype=torch.int32, device=word.device)
-    out.copy_(((word.view(torch.int32) >> sh) & 1).to(torch.float32))
-
-
-def bits_to_status(bits, word):
-    """Inverse of status_to_bits after the reduction: bit k set if any rank set it."""
-    sh = torch.arange(STATUS_BITS, dtype=torch.int32, device=word.device)
-    word.view(torch.int32).copy_(((bits > 0).to(torch.int32) << sh).sum(dtype=torch.int32).view(1))
+def _reduce_status(word):
+    """MAX over ranks of the int32 step status word, in place: a chain timeout on ANY rank makes
+    the word non-zero on every rank, so every rank's optimizer skips the step on the device; the
+    word then holds the highest failure code any rank reported (bit 1, the backward chain, over
+    bit 0).  One in-place collective on the word itself -- no bit expansion kernels on the device
+    path, where every small launch beside dSKIP waits for a CU."""
+    dist.all_reduce(word.view(torch.int32), op=dist.ReduceOp.MAX)
 
 
 class DPContext:
-    def __init__(self, world=1, rank=0, local_rank=0):
+    def __init__(self, world=1, rank=0, local_rank=0, last_on_main=True):
         self.world, self.rank, self.local_rank = world, rank, local_rank
+        # the last bucket (after the whole backward) issued from the main stream itself: two
+        # cross-stream hops (main -> RCCL's stream -> main) before the optimizer instead of four
+        # through the comm stream
+        self.last_on_main = last_on_main
 
     @property
     def enabled(self):
@@ -48,11 +44,11 @@ class DPContext:
 
     def reduce_grads(self, net):
         """Σ over ranks of the raw gradient buffer and of (Σxent, n_valid, Σ|argmax diff|), and
-        the OR of the step status words (a timed-out chain on ANY rank makes every rank's
-        optimizer skip the step on the device, so no rank applies garbage gradients; the bits
-        travel as per-bit counts, status_to_bits).
+        the MAX of the step status words (a timed-out chain on ANY rank makes every rank's
+        optimizer skip the step on the device, so no rank applies garbage gradients;
+        _reduce_status).
 
-        Three buckets, each ONE message (a staging copy of its flat ranges):
+        Three buckets, each one RCCL group call over in-place views:
           0 "head": POST1, POST2, their biases, SKIP_BIAS + the stats + the status word — final
             once the backward chain has completed (lbwn_plan_stream_wait "head_grads"), so its
             all-reduce runs on a side stream beside the backward's tail (dSKIP, the slab
@@ -71,40 +67,44 @@ class DPContext:
         plan = _Buckets.of(net)
         if not net.grad_flat.is_cuda:   # gloo (CPU tests): the same buckets, in order
             for k in range(len(plan.ranges)):
-                plan.pack(k, net)
-                dist.all_reduce(plan.buf[k])
-                plan.unpack(k, net)
+                _all_reduce_many(plan.tensors(k, net), cuda=False)
+                if k == 0:
+                    _reduce_status(net.status_word())
             return
         main = torch.cuda.current_stream(net.grad_flat.device)
         comm = self._comm_stream(net.grad_flat.device)
         # each bucket waits for its point of the backward, or for the whole backward when the
-        # plan has no such point (the comm stream's order keeps the buckets' all-reduces serial)
+        # plan has no such point (the comm stream's order keeps the buckets' all-reduces serial).
+        # Everything is reduced in place -- the gradient ranges, the stats and the status word --
+        # one RCCL group call per bucket: no staging copies or conversion kernels, which beside
+        # dSKIP wait for CUs its 240-VGPR waves leave only to kernels of <= 32 VGPRs and so ran
+        # after it (one-rank RCCL, C2: 144 us per step with staging, tools/dp_overhead.py).
         for k, point in enumerate(('head_grads', 'side_grads', None)):
             if not plan.ranges[k] and k > 0:
+                continue
+            status = net.status_word() if k == 0 else None
+            if point is None and self.last_on_main:
+                _all_reduce_many(plan.tensors(k, net), cuda=True, status=status)   # on main, after the backward
                 continue
             if point is None or not net.wait_point(point, comm):
                 comm.wait_stream(main)
             with torch.cuda.stream(comm):
-                plan.pack(k, net)
-                dist.all_reduce(plan.buf[k])
-                plan.unpack(k, net)
+                _all_reduce_many(plan.tensors(k, net), cuda=True, status=status)
         main.wait_stream(comm)
 
     def reduce_grads_flat(self, net):
-        """The whole gradient + stats + status as one message after the backward (the reference
-        bucketing of tests/test_dropin.py::test_dp_bucketed_equals_flat)."""
+        """The whole gradient + stats as one message after the backward, and the status word's MAX
+        (the reference bucketing of tests/test_dropin.py::test_dp_bucketed_equals_flat)."""
         if not self.enabled:
             return
         n = net.grad_flat.numel()
-        buf = torch.empty(n + 3 + STATUS_BITS, dtype=torch.float32, device=net.grad_flat.device)
-        sw = net.status_word()
+        buf = torch.empty(n + 3, dtype=torch.float32, device=net.grad_flat.device)
         buf[:n].copy_(net.grad_flat)
         buf[n:n + 3].copy_(net.stats[:3])
-        status_to_bits(sw, buf[n + 3:])
         dist.all_reduce(buf)
         net.grad_flat.copy_(buf[:n])
         net.stats[:3].copy_(buf[n:n + 3])
-        bits_to_status(buf[n + 3:], sw)
+        _reduce_status(net.status_word())
 
     def _comm_stream(self, device):
         s = getattr(self, '_comm', None)
@@ -124,10 +124,26 @@ class DPContext:
             dist.barrier()
 
 
+def _all_reduce_many(ts, cuda, status=None):
+    """SUM-all-reduce each tensor in place, as one coalesced RCCL group call on the device path
+    (one launch per bucket instead of one per range; a group takes one dtype and op), then MAX
+    the status word."""
+    if cuda and dist.is_initialized() and len(ts) > 1:
+        from torch.distributed.distributed_c10d import _coalescing_manager
+        with _coalescing_manager(device=ts[0].device):
+            for t in ts:
+                dist.all_reduce(t)
+    else:
+        for t in ts:
+            dist.all_reduce(t)
+    if status is not None:
+        _reduce_status(status)
+
+
 class _Buckets:
-    """Flat ranges of the two all-reduce buckets (lbwn.arch.ParamLayout: weights
+    """Flat ranges of the three all-reduce buckets (lbwn.arch.ParamLayout: weights
     [pre, sig, gate, res, skip, gc.., lc.., post1, post2] then biases [pre_b, sig_b, gate_b,
-    res_b, skip_b, post1_b, post2_b]) and their staging buffers."""
+    res_b, skip_b, post1_b, post2_b]), reduced in place."""
 
     def __init__(self, net):
         lay = net.layout
@@ -151,34 +167,30 @@ class _Buckets:
         covered = sorted(r for rs in self.ranges for r in rs)
         assert covered[0][0] == 0 and covered[-1][1] == lay.n_total and all(
             covered[i][1] == covered[i + 1][0] for i in range(len(covered) - 1)), ('buckets must tile the buffer', covered)
-        sizes = [sum(b - a for a, b in head) + 3 + STATUS_BITS] + [sum(b - a for a, b in r) for r in (side, rest)]
-        self.buf = [torch.empty(n, dtype=torch.float32, device=net.grad_flat.device) for n in sizes]
+        self.device = net.grad_flat.device
 
     @staticmethod
     def of(net):
         b = getattr(net, '_dp_buckets', None)
-        if b is None or b.buf[0].device != net.grad_flat.device:
+        if b is None or b.device != net.grad_flat.device:
             b = _Buckets(net)
             net._dp_buckets = b
         return b
 
-    def pack(self, k, net):
-        o = 0
-        for a, b in self.ranges[k]:
-            self.buf[k][o:o + b - a].copy_(net.grad_flat[a:b])
-            o += b - a
-        if k == 0:
-            self.buf[0][o:o + 3].copy_(net.stats[:3])
-            status_to_bits(net.status_word(), self.buf[0][o + 3:])
-
-    def unpack(self, k, net):
-        o = 0
-        for a, b in self.ranges[k]:
-            net.grad_flat[a:b].copy_(self.buf[k][o:o + b - a])
-            o += b - a
-        if k == 0:
-            net.stats[:3].copy_(self.buf[0][o:o + 3])
-            bits_to_status(self.buf[0][o + 3:], net.status_word())
+    def tensors(self, k, net):
+        """Bucket k's in-place views: its gradient ranges, and for bucket 0 the loss stats (built
+        once per buffer pair: the step's host time is the DP path's budget too)."""
+        key = (k, net.grad_flat.data_ptr(), net.stats.data_ptr())
+        views = getattr(self, '_views', None)
+        if views is None:
+            views = self._views = {}
+        ts = views.get(key)
+        if ts is None:
+            ts = [net.grad_flat[a:b] for a, b in self.ranges[k]]
+            if k == 0:
+                ts.append(net.stats[:3])
+            views[key] = ts
+        return ts
 
 
 def init(backend=None, device_type='cuda'):

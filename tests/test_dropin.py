@@ -286,6 +286,7 @@ def test_dp_buckets_tile_the_gradient(arch_file):
     lay = ParamLayout(load_arch(os.path.join(ROOT, 'par', arch_file + '.json'), num_global_cond=7))
     bk = _Buckets(_FakeNet(torch.zeros(lay.n_total), torch.zeros(4), lay))
     owner = np.full(lay.n_total, -1)
+    assert bk.tensors(0, _FakeNet(torch.zeros(lay.n_total), torch.zeros(4), lay))[-1].numel() == 3   # + the stats
     for k, rs in enumerate(bk.ranges):
         for a, b in rs:
             assert (owner[a:b] == -1).all()
@@ -301,10 +302,10 @@ def test_dp_buckets_tile_the_gradient(arch_file):
 
 def test_dp_bucketed_equals_flat(tmp_path):
     """The three-bucket all-reduce (lbwn.dist: head bucket beside the backward's tail, side
-    bucket beside dSKIP, the rest after it) gives bitwise the flat one-message result, for the gradient, the loss stats and
-    the status word (any rank's timeout reaches every rank as the OR of the words: 0b01 | 0b11
-    = 0b11, where a SUM would read 0b100), over 2 gloo ranks at arch5's layout (GC + LC kinds
-    included)."""
+    bucket beside dSKIP, the rest after it; every range reduced in place) gives bitwise the flat
+    one-message result, for the gradient, the loss stats and the status word (any rank's timeout
+    reaches every rank as the MAX of the words: max(0b01, 0b11) = 0b11, where a SUM would read
+    0b100), over 2 gloo ranks at arch5's layout (GC + LC kinds included)."""
     import torch.multiprocessing as mp
     out = str(tmp_path / 'bk.npz')
     port = 29500 + (os.getpid() + 13) % 1000

@@ -1,7 +1,7 @@
 """The data-parallel reduction's device path (lbwn/dist.py DPContext.reduce_grads)
 on the real training plan, on one GPU.
 
-The CUDA branch packs the head bucket on a comm stream that waits on the plan's "head_grads"
+The CUDA branch reduces the head bucket in place on a comm stream that waits on the plan's "head_grads"
 point (lbwn_plan_stream_wait) while the backward's tail (dSKIP, the slab reduction, dPRE, the
 conditioning gradients) still runs on the main and side streams, and the side bucket (PRE,
 SIGNAL, GATE, RESIDUAL, GC and their biases) at "side_grads" while dSKIP may still run.  An early event, or a tail
@@ -42,9 +42,13 @@ def _diff_names(net, a, b):
 
 
 def _fake_all_reduce(t, op=None, group=None, async_op=False):
-    """SUM over two identical ranks, enqueued on the current stream (as RCCL would be)."""
+    """SUM (x2) or MAX (identity) over two identical ranks, enqueued on the current stream (as RCCL
+    would be)."""
     assert t.is_cuda
-    t.mul_(2.0)
+    if op is None or op == lbdist.dist.ReduceOp.SUM:
+        t.mul_(2.0)
+    else:
+        assert op == lbdist.dist.ReduceOp.MAX
 
 
 def _bits(t):
@@ -117,3 +121,52 @@ def test_dp_device_path_steps_match_single_process(name, B, T, dp2):
     assert np.array_equal(s0, s1)
     assert c0[0] == c1[0] == 3 and c0[3] == c1[3] == 0
     assert c1[1] == 2 * c0[1]                      # VALID_SAMPLES counts the global n_valid
+
+
+def test_dp_device_path_real_rccl_one_rank(monkeypatch):
+    """The CUDA branch of reduce_grads through the real RCCL collective (a one-rank "nccl" process
+    group on 127.0.0.1; SUM over one rank is the identity): the comm stream, the head_grads /
+    side_grads wait points, the three buckets' pack -> all_reduce -> unpack with RCCL's own kernels
+    on the device, and the main stream's wait before the optimizer.  Gradients, stats and the status
+    word equal the un-reduced step's bitwise, and three steps with it equal three plain steps."""
+    import socket
+    import torch.distributed as tdist
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    tdist.init_process_group('nccl', init_method='tcp://127.0.0.1:%d' % port, rank=0, world_size=1,
+                             device_id=torch.device('cuda', 0))
+    try:
+        monkeypatch.setattr(lbdist.DPContext, 'enabled', property(lambda self: True))
+        ctx = lbdist.DPContext(world=1, rank=0, local_rank=0)
+        arch = load_arch(os.path.join(ROOT, 'par', 'arch5.json'))
+        B, T = 2, 4096
+        net = make_net(arch, B, seed=3)
+        q, ids, mel = _batch(arch, B, T, 9)
+        save0 = net.save_flat.clone()
+        net.forward(q, mel, ids)
+        torch.cuda.synchronize()
+        g_raw, s_raw, w_raw = _bits(net.grad_flat), net.stats[:3].cpu().numpy(), _bits(net.status_word())
+        net.save_flat.copy_(save0)
+        net.forward(q, mel, ids)
+        ctx.reduce_grads(net)
+        torch.cuda.synchronize()
+        assert np.array_equal(g_raw, _bits(net.grad_flat)), _diff_names(net, g_raw, _bits(net.grad_flat))[:12]
+        assert np.array_equal(s_raw, net.stats[:3].cpu().numpy())
+        assert w_raw[0] == _bits(net.status_word())[0] == 0
+        out = []
+        for use_dp in (False, True):
+            net = make_net(arch, B, seed=4)
+            opt = AdamOptimizer(1e-3)
+            for k in range(3):
+                q, ids, mel = _batch(arch, B, T, 20 + k)
+                net.forward(q, mel, ids)
+                if use_dp:
+                    ctx.reduce_grads(net)
+                opt.apply(net)
+            torch.cuda.synchronize()
+            net.check_status()
+            out.append(_bits(net.flat))
+        assert np.array_equal(out[0], out[1]), '%d weights differ' % int((out[0] != out[1]).sum())
+    finally:
+        tdist.destroy_process_group()
