@@ -126,6 +126,18 @@ def test_restatement_matches_oracle():
 def test_full_size_forward_backward(arch_name, B, chain_tile):
     """C4 (arch5, B=32) and C2 (arch3, B=8) at T=4096: every layer's z on the HIP path's own
     inputs, z end to end, the skip sum, SAVE, n_valid, mean xent and every gradient."""
+    _full_size(arch_name, B)
+
+
+def test_full_size_c5_per_gpu():
+    """C5's per-GPU share (arch5, B=8, T=4096: the shape each rank of the 8-GPU data-parallel
+    config trains) at full size, default chain form: its LC backward takes the fused upsample
+    backward (128 mel frames; C4's 512 run the per-stage GEMMs) and dlc's deferred split-K
+    partials, which C4 does not exercise."""
+    _full_size('arch5', 8)
+
+
+def _full_size(arch_name, B):
     arch = _arch(arch_name)
     T = 4096
     q, ids, mel = _batch(arch, B, T, 11)
