@@ -3666,8 +3666,8 @@ __global__ __launch_bounds__(64) void gc_tile_sum_kernel(const float* __restrict
   for (int s0 = 0; s0 < ntiles; s0 += GTS_CHUNK) {
     int gid[GTS_CHUNK / 64];
 #pragma unroll
-    for (int k = 0; k < GTS_CHUNK / 64; ++k)   // past the end: 0 from the buffer, masked below
-      gid[k] = (int)__builtin_amdgcn_raw_buffer_load_b32(rg, c * 4, (s0 + 64 * k) * 4, 0);
+    for (int k = 0; k < GTS_CHUNK / 64; ++k)   // past the end: 0 from the range-checked buffer offset, masked below
+      gid[k] = (int)__builtin_amdgcn_raw_buffer_load_b32(rg, (s0 + c) * 4 + 256 * k, 0, 0);
     int n = 0;
 #pragma unroll
     for (int k = 0; k < GTS_CHUNK / 64; ++k) {
