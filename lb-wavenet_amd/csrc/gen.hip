@@ -971,6 +971,9 @@ LBWN_DEV void persist_head(const PersistK& a, int m, float* sm, int b0, int B, l
       if (sb < B && scol16 + cc < Cs) put_granule(a.sg + (long)(b0 + sb) * Cs + scol16 + cc, tag, x);   // B. publish
     }
     if (tr && s == n - 1) tr[2] = wall_clock64();
+    // every head's own stamps (trace only): skip columns published, whole skip vector gathered
+    long long* th = (trace && tid == 0 && s == n - 1) ? trace + 2 * L + 136 + 2 * m : nullptr;
+    if (th) th[0] = wall_clock64();
     // B. gather the whole skip vector: thread k = tid polls column k of every stream
     if (tid < Cs) {
       // as many granule loads per poll as the group has streams, in fours (a group of 10 polled
@@ -988,6 +991,7 @@ LBWN_DEV void persist_head(const PersistK& a, int m, float* sm, int b0, int B, l
     }
     __syncthreads();
     if (tr && s == n - 1) tr[3] = wall_clock64();
+    if (th) th[1] = wall_clock64();
     // C. h = relu(relu(skip + Σb)·POST1[:, cols] + b1) for this block's 16 columns and all 16
     //    stream slots on v_mfma_f32_16x16x4_f32 (exact f32 products): wave wv takes K rows
     //    64wv .. 64wv+63 (16 MFMAs; A[i = stream][k] = RS, B[k][j = column] = P1T), the eight
@@ -1162,7 +1166,7 @@ extern "C" int lbwn_gen_plan_create(const lbwn_arch* a, int B, int64_t max_steps
   p->oGCP = gcarve(cur, 4 * (size_t)p->L * B * 64);
   p->oBSUM = gcarve(cur, 4 * (size_t)p->Cs);
   p->oGIMG = gcarve(cur, 4 * (size_t)p->L * GIMG);
-  p->oTRACE = gcarve(cur, 8 * (size_t)(2 * p->L + 8 + 128));
+  p->oTRACE = gcarve(cur, 8 * (size_t)(2 * p->L + 8 + 128 + 2 * P_NH));
   p->trace = getenv("LBWN_GEN_TRACE") != nullptr;
   // persistent form: every block resident (one 512-thread block per CU), phase A maps
   // (16 skip columns × B streams) onto the threads, the draw's logits fit the tap table's tail
@@ -1206,7 +1210,7 @@ extern "C" int lbwn_gen_tensor(const lbwn_gen_plan* p, const char* name, size_t*
   else if (!strcmp(name, "logits")) { *off = p->oLOG; *bytes = 4 * B * p->Q; }
   else if (!strcmp(name, "step")) { *off = p->oSTEP; *bytes = 8; }
   else if (!strcmp(name, "status")) { *off = p->oSTEP + 8; *bytes = 4; }   // 0, or 5: a persistent hand-off timed out
-  else if (!strcmp(name, "trace")) { *off = p->oTRACE; *bytes = 8 * (size_t)(2 * p->L + 8 + 128); }
+  else if (!strcmp(name, "trace")) { *off = p->oTRACE; *bytes = 8 * (size_t)(2 * p->L + 8 + 128 + 2 * P_NH); }
   else if (!strcmp(name, "rings")) { *off = p->oRING; *bytes = 4 * (size_t)p->n_ring; }
   else if (!strcmp(name, "teacher")) { *off = p->oTEACH; *bytes = 4 * (size_t)std::max<long long>(1, p->n_teacher); }
   else LBWN_REQUIRE(false, "gen_tensor: unknown tensor '%s'", name);

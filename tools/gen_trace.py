@@ -49,6 +49,12 @@ if g.persistent:
     print('  chain 0: logits gathered %.2f (heads 0-15, compute waves), barrier D passed %.2f (heads 16-31, '
           'loader waves), draw done %.2f' % (us(tr[5]), us(tr[7]), us(tr[6])))
     print('  step period ~ %.2f us (draw done - start of the step it drew)' % us(tr[6]))
+    hs = tr[2 * L + 136:2 * L + 136 + 64].reshape(32, 2)
+    if np.all(hs > 0):
+        pub, got = us(hs[:, 0]), us(hs[:, 1])
+        print('  every head: skip columns published %.2f .. %.2f (median %.2f; latest head %d), whole vector gathered '
+              '%.2f .. %.2f' % (pub.min(), pub.max(), np.median(pub), int(np.argmax(pub)), got.min(), got.max()))
+        print('  published by head: ' + ' '.join('%.2f' % x for x in pub))
     sub = tr[8 + L + 128:8 + L + 128 + 48].reshape(8, 6)
     if np.all(sub > 0):
         seg = np.diff(np.concatenate([sub, sub[1:, :1].tolist() + [[sub[-1, 5]]]], axis=1), axis=1)
