@@ -91,6 +91,11 @@ struct lbwn_plan {
   bool up_forked = false;        // this forward launched the fused upsample on aux2
   bool bwd_chain_event = false;  // the last backward recorded ev_chain (lbwn_plan_stream_wait)
   bool bwd_side_event = false;   // ... and ev_join2 at the end of its side-stream work
+  // the bias gradients' final column sums on aux2 beside dPOST2 / dPOST1 (a 41-VGPR kernel that
+  // fits beside their blocks), joined before the backward chain: C2 -7 us per step, C4 neutral
+  // (profiles/r06_ab_colsum_side.txt); LBWN_COLSUM_SIDE=0 (plan creation) keeps them in line
+  bool colsum_side = true;
+  hipEvent_t ev_cs = nullptr, ev_cs_done = nullptr;
   bool wpk_valid = false;        // the f32 layer images were packed this step
   // Weights pre-split into bf16 planes once per step for the bf16-split GEMMs (gemm.hip):
   // [W3_SKIP_F] SKIPcat as skip-fwd B, [W3_POST1_F] POST1 as post1-fwd B, [W3_POST2_F] POST2 as
@@ -105,6 +110,8 @@ struct lbwn_plan {
     if (ev_upb) (void)hipEventDestroy(ev_upb);
     if (ev_dlc) (void)hipEventDestroy(ev_dlc);
     if (ev_join2) (void)hipEventDestroy(ev_join2);
+    if (ev_cs) (void)hipEventDestroy(ev_cs);
+    if (ev_cs_done) (void)hipEventDestroy(ev_cs_done);
   }
   // one-shot event probe
   char probe[32];
@@ -371,6 +378,8 @@ int lbwn_plan_create(const lbwn_arch* a, int B, int T, lbwn_plan** out) {
     p->mbits_ok = !(mv && mv[0] == '0');
     const char* wv = getenv("LBWN_BWD_WGRAD");
     p->wg_out = (wv && wv[0] == '1') && bwd_nw == 8;
+    const char* cv = getenv("LBWN_COLSUM_SIDE");
+    p->colsum_side = !(cv && cv[0] == '0');
   }
   p->Li = a->n_lc_in;
   p->nup = a->n_lc_out > 0 ? a->n_lc_upsample : 0;
@@ -580,6 +589,8 @@ int ensure_device(lbwn_plan* p) {
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_fwd_up, hipEventDisableTiming));
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_upb, hipEventDisableTiming));
     LBWN_HIP(hipEventCreateWithFlags(&p->ev_dlc, hipEventDisableTiming));
+    LBWN_HIP(hipEventCreateWithFlags(&p->ev_cs, hipEventDisableTiming));
+    LBWN_HIP(hipEventCreateWithFlags(&p->ev_cs_done, hipEventDisableTiming));
   }
   return 0;
 }
@@ -1063,6 +1074,9 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
   Probe(p, st, "dz");
   if ((e = lbwn_gemm_launch(g, 1, 1, 1, nullptr, st))) return e;
   Probe::end(p, st, "dz");
+  // (the final sums on aux2 beside dPOST2 / dPOST1, joined before the chain; LBWN_COLSUM_SIDE=0: in line)
+  const bool cs_side = p->colsum_side && p->aux2 && p->chain;
+  bool cs_forked = false;
   // bias gradients (column sums of dlogits, dH1, dS; every layer's SKIP_BIAS gets the same Σ dS):
   // here on the main stream, before the fork (small kernels on the least-priority stream beside a
   // resident chain can wait hundreds of µs for a CU)
@@ -1092,7 +1106,15 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
         fp[nf] = CPART + (long)lbwn_colpart_parts(M) * Cp; fn[nf] = Cs; fo[nf] = G->skip_b;
         np[nf] = lbwn_colpart_parts(M); rp[nf] = L; ++nf;
       }
-      if (nf && (e = lbwn_colsum_final_launch(nf, fp, fn, fo, fa, np, st, rp))) return e;
+      hipStream_t cst = st;
+      if (nf && cs_side) {
+        LBWN_HIP(hipEventRecord(p->ev_cs, st));
+        LBWN_HIP(hipStreamWaitEvent(p->aux2, p->ev_cs, 0));
+        cst = p->aux2;
+      }
+      if (nf && (e = lbwn_colsum_final_launch(nf, fp, fn, fo, fa, np, cst, rp))) return e;
+      if (nf && cs_side) LBWN_HIP(hipEventRecord(p->ev_cs_done, p->aux2));
+      cs_forked = nf && cs_side;
     }
     if (!fcols && G->skip_b && (e = lbwn_bcast_rows_launch(G->skip_b, L, Cs, st))) return e;
   }
@@ -1128,6 +1150,7 @@ int lbwn_train_backward(lbwn_plan* p, const lbwn_params* P, const lbwn_params* G
     return 0;
   };
   if ((e = head_wgrads(st, SPL))) return e;
+  if (cs_forked) LBWN_HIP(hipStreamWaitEvent(st, p->ev_cs_done, 0));
   // residual stack in reverse (conditioning recomputed from the forward's GCTAB / COND)
   Cond cd;
   if (p->Ge > 0) {

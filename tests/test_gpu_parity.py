@@ -630,6 +630,32 @@ def test_mask_bits_equal_f32_masks(monkeypatch):
         assert np.array_equal(g0[n], g1[n]), n
 
 
+@pytest.mark.parametrize('name,B', [('arch3', 4), ('arch5', 2)])
+def test_colsum_side_bitwise(monkeypatch, name, B):
+    """The bias gradients' final column sums run on the side stream beside dPOST2 / dPOST1, joined
+    before the backward chain (default; LBWN_COLSUM_SIDE=0 at plan creation keeps them in line):
+    stats, SAVE and every gradient bit for bit as the in-line order, over two steps (voice ids
+    tile-uniform: no GC atomics)."""
+    from tests.test_gpu_dp import _batch
+    arch = load_arch(os.path.join(ROOT, 'par', name + '.json'))
+    T = 4096
+    q, ids, mel = _batch(arch, B, T, 7)
+    out = []
+    for side in ('0', '1'):
+        monkeypatch.setenv('LBWN_COLSUM_SIDE', side)
+        net = make_net(arch, B)
+        for _ in range(2):
+            net.forward(q, mel, ids, backward=True)
+        torch.cuda.synchronize()
+        assert int(net.plan_tensor(T, 'status').view(torch.int32)[0]) == 0
+        out.append((net.stats[:3].cpu().numpy(), net.save_flat.cpu().numpy(),
+                    {n: g.cpu().numpy() for n, g in net.grads.items()}))
+    (s0, v0, g0), (s1, v1, g1) = out
+    assert np.array_equal(s0, s1) and np.array_equal(v0, v1)
+    for n in g0:
+        assert np.array_equal(g0[n], g1[n]), n
+
+
 def test_chain_trace_build_bitwise(monkeypatch):
     """LBWN_CHAIN_TRACE=<block> (read at plan creation: the chains' traced instantiations, whose
     clock stamps feed tools/chain_trace.py and the bench's C4 dilation sweep) computes exactly what
